@@ -1,0 +1,177 @@
+/* hvit.h -- C ABI of the MI355X (gfx950) HybridViT hot-path library (libhvit.so).
+ *
+ * The reference exposes this path only as the PyTorch nn.Module API of
+ * models/hybrid_vit.py (HybridViT.__init__ :36-170, forward :396-469) with no
+ * native operator or FFI of its own.  This header is the C ABI
+ * that module binds (via ctypes).  Each entry point replaces
+ * the aten op sequence of one reference module, cited per function.
+ *
+ * Conventions
+ *  - Plain pointers to device memory + sizes; no torch types.  The library never
+ *    allocates or frees device memory and keeps no pointer past a call; the
+ *    caller provides every output, saved activation and workspace.
+ *  - Activations are NHWC (channels innermost).  A token tensor [B, N, D] is the
+ *    NHWC image [B, H', W', D] of the patch grid, N = H' * W'.
+ *  - dtype codes: HVIT_F32 (exact-f32 MFMA path, used for 1e-3 parity) or
+ *    HVIT_BF16 (bf16 MFMA, f32 accumulate).  Statistics, the ViT residual
+ *    stream, LayerNorm inputs and all weight gradients are f32.
+ *  - Work is enqueued on `stream` (a hipStream_t); no host synchronisation, no
+ *    allocation: every call is hipGraph-capturable.
+ *  - Return 0 on success; otherwise an HVIT_ERR_* code, with a message from
+ *    hvit_last_error().  There is no fallback path.
+ */
+#ifndef HVIT_H_
+#define HVIT_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { HVIT_F32 = 0, HVIT_BF16 = 1 };
+enum { HVIT_OK = 0, HVIT_ERR_ARG = 1, HVIT_ERR_LAUNCH = 2 };
+enum { HVIT_ACT_NONE = 0, HVIT_ACT_GELU_DUAL = 1, HVIT_ACT_TANH = 2, HVIT_ACT_GELU_BWD = 3 };
+
+/* Counter-based dropout: element i is kept iff a 16-bit hash of (seed, site, i)
+ * is >= round(p * 65536); kept values are scaled by 1/(1-p).  Forward and
+ * backward regenerate identical masks.  p = 0 disables. */
+typedef struct {
+  float p;
+  unsigned long long seed;
+  unsigned int site;
+} hvit_dropout_t;
+
+/* Fused GEMM epilogue (applied in this order):
+ *   v  = acc (+ bias[n]) (+ rowadd[(m % rowadd_rows) * N + n])
+ *   GELU_DUAL: y = v (pre-activation); out2 = dropout(gelu(v))      -> stop
+ *   TANH: v = tanh(v) ; v = dropout(v) ; GELU_BWD: v *= gelu'(aux[m, n])
+ *   resid: v = resid[m, n] + rowscale[m / rows_per_sample] * v     (f32)
+ *   colsum[n] += sum_m v ; y[m, n] = v                                         */
+typedef struct {
+  int act;
+  void* out2;
+  int out2_dt;
+  const void* aux;
+  int aux_dt;
+  hvit_dropout_t dropout;
+  const float* resid;
+  const float* rowscale;
+  int rows_per_sample;
+  const float* rowadd;
+  int rowadd_rows;
+  float* colsum;
+} hvit_epilogue_t;
+
+/* Convolution geometry.  Input image = concat(src1[C1], src2[C2]) (channels)
+ * of an Hs x Ws NHWC source, nearest-upsampled by U; kernel KS x KS, stride,
+ * zero pad.  Output Ho = (Hs*U + 2*pad - KS)/stride + 1 (same for W). */
+typedef struct {
+  const void* src1;
+  int C1;
+  const void* src2;
+  int C2;
+  int N, Hs, Ws, U;
+  int KS, stride, pad;
+  int Cout;
+} hvit_conv_geom_t;
+
+const char* hvit_last_error(void);
+const char* hvit_version(void);
+
+/* ---- Linear (nn.Linear: attention.py:55,58 qkv/proj; components.py:224,227
+ * MLP; hybrid_vit.py:153 to_feature_map; 1x1 skip convs hybrid_vit.py:158-165
+ * as a Linear over NHWC pixels).  w is [N][K] (torch layout). */
+int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int M, int N, int K, void* y,
+                    int y_dt, const hvit_epilogue_t* epi, void* stream);          /* y[M,N] = x[M,K] w^T */
+int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, int N, int K, void* dx, int dx_dt,
+                      const hvit_epilogue_t* epi, void* stream);                 /* dx[M,K] = dy[M,N] w */
+long long hvit_wgrad_workspace(int M, int N, int K);                              /* f32 elements */
+int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* ws,
+                      long long ws_elems, void* stream);                        /* dw[N,K] = dy^T x */
+
+/* ---- Convolution as implicit GEMM (ConvBlock conv components.py:55-62,
+ * TransposeConvBlock upsample+conv components.py:146-158, PatchEmbedding
+ * conv components.py:275-280, decoder concat hybrid_vit.py:389).
+ * Weights are pre-packed with hvit_conv_weight_pack: mode 0 [Cout][KS][KS][Cin]
+ * for fwd / wgrad / patch dgrad; mode 1 (flipped) [Cin][KS][KS][Cout] for the
+ * 3x3 dgrad.  conv_fwd optionally writes BatchNorm partials
+ * [ceil(P/128)][Cout][2] (mean, M2 per 128-row tile) for hvit_bn_finalize; its
+ * epilogue (nullable) may apply tanh (final decoder conv, components.py:166-167),
+ * a row-periodic add (pos_embed, components.py:384) and dropout.
+ * conv_dgrad: same-conv -> gradient of the (upsampled, concatenated) conv input
+ * [N, Hs*U, Ws*U, C1+C2] (finish with hvit_upsample_split_bwd); patch conv
+ * (KS == stride, pad 0) -> gradient of src1 [N, Hs, Ws, C1] directly. */
+int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* bias, void* y, int y_dt,
+                  float* bn_partials, const hvit_epilogue_t* epi, void* stream);
+int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy, const void* w_packed, void* dx, int dx_dt,
+                    void* stream);
+long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g);
+int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy, float* dw_packed, float* ws,
+                    long long ws_elems, void* stream);                           /* dw_packed mode-0 layout */
+int hvit_conv_weight_pack(const float* w, int Cout, int Cin, int KS, int mode, void* out, int out_dt,
+                          void* stream);
+int hvit_conv_weight_unpack(const float* dw_packed, int Cout, int Cin, int KS, float* dw, void* stream);
+
+/* ---- Multi-head self-attention core (attention.py:82-107): softmax(q k^T *
+ * scale) -> dropout -> @ v with qkv [B, N, 3, H, hd] (the qkv Linear output)
+ * and o [B, N, H*hd]; lse [B, H, N] f32.  probs (optional, [B, H, N, N] f32)
+ * receives the post-dropout attention map for return_attentions
+ * (hybrid_vit.py:422-453).  Backward writes dq, dk, dv into dqkv (qkv layout);
+ * delta_ws is [B, H, N] f32 scratch.  head_dim in {16, 32, 64}. */
+int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
+                  const hvit_dropout_t* dropout, void* o, float* lse, float* probs, void* stream);
+int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
+                  int hd, float scale, const hvit_dropout_t* dropout, void* dqkv, float* delta_ws, void* stream);
+
+/* ---- LayerNorm eps (attention.py:152-153, :271): x f32 [M, D] -> y; saves
+ * mean / rstd [M].  Backward: dx = resid + dLN (resid may be NULL or alias dx),
+ * dgamma / dbeta [D] overwritten. */
+int hvit_layernorm_fwd(const float* x, const float* gamma, const float* beta, int M, int D, float eps, void* y,
+                       int y_dt, float* mean, float* rstd, void* stream);
+int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean, const float* rstd,
+                       const float* gamma, int M, int D, const float* resid, float* dx, float* dgamma,
+                       float* dbeta, void* stream);
+
+/* ---- BatchNorm2d -> ReLU -> Dropout2d -> MaxPool2d(pool) tail of ConvBlock /
+ * TransposeConvBlock (components.py:67-85, :161-178).  z is the pre-BN conv
+ * output NHWC [N, H, W, C] (C a power of two <= 256).  Train mode: mean /
+ * invstd from hvit_bn_finalize (which also updates running stats with
+ * momentum and the unbiased variance, and increments num_batches_tracked);
+ * eval: hvit_bn_eval_prep.  Backward: dz from dy = grad of the pooled output;
+ * sums [2][C] receives (dbeta, dgamma). */
+int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C, float* mean,
+                     float* invstd, float* running_mean, float* running_var, long long* num_batches_tracked,
+                     float momentum, float eps, void* stream);
+int hvit_bn_eval_prep(const float* running_mean, const float* running_var, int C, float eps, float* mean,
+                      float* invstd, void* stream);
+int hvit_bn_act_fwd(int dt, const void* z, int N, int H, int W, int C, const float* mean, const float* invstd,
+                    const float* gamma, const float* beta, const hvit_dropout_t* dropout2d, int pool, void* y,
+                    int y_dt, void* stream);
+int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean, const float* invstd,
+                    const float* gamma, const float* beta, const hvit_dropout_t* dropout2d, int pool,
+                    const void* dy, int dy_dt, int training, void* dz, int dz_dt, float* sums, void* stream);
+
+/* ---- Resampling (F.interpolate bilinear align_corners=False, hybrid_vit.py:
+ * 381-386 and :459-465; nearest x2 backward + concat split, components.py:146,
+ * hybrid_vit.py:389).  NHWC. */
+int hvit_bilinear_fwd(const void* x, int x_dt, int N, int Hi, int Wi, int C, int Ho, int Wo, void* y, int y_dt,
+                      void* stream);
+int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int Wo, int C, int Hi, int Wi, void* dx,
+                      int dx_dt, int accumulate, void* stream);
+int hvit_upsample_split_bwd(const void* du, int du_dt, int N, int H, int W, int U, int C1, int C2, void* dx1,
+                            int dx1_dt, void* dx2, int dx2_dt, void* stream);
+
+/* ---- Elementwise / reductions */
+int hvit_cast(const void* src, int src_dt, void* dst, int dst_dt, long long n, void* stream);
+int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, const hvit_dropout_t* dropout,
+                       const float* rowscale, int rows_per_sample, void* out, int out_dt, void* stream);
+int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long long n, void* dz, int dz_dt, void* stream);
+int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate, float* out,
+                     void* stream);                                     /* out[n] (+)= sum_m x[m*ld+n] */
+int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream);
+int hvit_droppath_scale(int B, const hvit_dropout_t* dropout, float* out, void* stream);  /* DropPath
+                                                                     components.py:407-427 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HVIT_H_ */

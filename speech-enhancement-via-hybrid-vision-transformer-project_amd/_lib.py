@@ -1,0 +1,136 @@
+"""ctypes binding of libhvit.so (the C ABI declared in include/hvit.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (csrc/Makefile) and
+loaded from this directory.  There is no fallback: if the library is missing or
+a call fails, a RuntimeError is raised with the library's error message.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhvit.so")
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_longlong
+f32 = C.c_float
+
+
+class Dropout(C.Structure):
+    _fields_ = [("p", C.c_float), ("seed", C.c_ulonglong), ("site", C.c_uint)]
+
+
+class Epilogue(C.Structure):
+    _fields_ = [
+        ("act", i32), ("out2", vp), ("out2_dt", i32), ("aux", vp), ("aux_dt", i32),
+        ("dropout", Dropout), ("resid", vp), ("rowscale", vp), ("rows_per_sample", i32),
+        ("rowadd", vp), ("rowadd_rows", i32), ("colsum", vp),
+    ]
+
+
+class ConvGeom(C.Structure):
+    _fields_ = [
+        ("src1", vp), ("C1", i32), ("src2", vp), ("C2", i32),
+        ("N", i32), ("Hs", i32), ("Ws", i32), ("U", i32),
+        ("KS", i32), ("stride", i32), ("pad", i32), ("Cout", i32),
+    ]
+
+
+P = C.POINTER
+_SIGS = {
+    "hvit_last_error": ([], C.c_char_p),
+    "hvit_version": ([], C.c_char_p),
+    "hvit_linear_fwd": ([i32, vp, vp, vp, i32, i32, i32, vp, i32, P(Epilogue), vp], i32),
+    "hvit_linear_dgrad": ([i32, vp, vp, i32, i32, i32, vp, i32, P(Epilogue), vp], i32),
+    "hvit_wgrad_workspace": ([i32, i32, i32], i64),
+    "hvit_linear_wgrad": ([i32, vp, vp, i32, i32, i32, vp, vp, i64, vp], i32),
+    "hvit_conv_fwd": ([i32, P(ConvGeom), vp, vp, vp, i32, vp, P(Epilogue), vp], i32),
+    "hvit_conv_dgrad": ([i32, P(ConvGeom), vp, vp, vp, i32, vp], i32),
+    "hvit_conv_wgrad_workspace": ([P(ConvGeom)], i64),
+    "hvit_conv_wgrad": ([i32, P(ConvGeom), vp, vp, vp, i64, vp], i32),
+    "hvit_conv_weight_pack": ([vp, i32, i32, i32, i32, vp, i32, vp], i32),
+    "hvit_conv_weight_unpack": ([vp, i32, i32, i32, vp, vp], i32),
+    "hvit_mhsa_fwd": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
+    "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
+    "hvit_layernorm_fwd": ([vp, vp, vp, i32, i32, f32, vp, i32, vp, vp, vp], i32),
+    "hvit_layernorm_bwd": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp], i32),
+    "hvit_bn_finalize": ([vp, i32, i32, i64, i32, vp, vp, vp, vp, vp, f32, f32, vp], i32),
+    "hvit_bn_eval_prep": ([vp, vp, i32, f32, vp, vp, vp], i32),
+    "hvit_bn_act_fwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, vp], i32),
+    "hvit_bn_act_bwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, i32, vp,
+                         i32, vp, vp], i32),
+    "hvit_bilinear_fwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp], i32),
+    "hvit_bilinear_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp], i32),
+    "hvit_upsample_split_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp], i32),
+    "hvit_cast": ([vp, i32, vp, i32, i64, vp], i32),
+    "hvit_dropout_scale": ([vp, i32, i64, i32, P(Dropout), vp, i32, vp, i32, vp], i32),
+    "hvit_tanh_bwd": ([vp, i32, vp, i64, vp, i32, vp], i32),
+    "hvit_reduce_rows": ([vp, i32, i64, i64, i64, i32, vp, vp], i32),
+    "hvit_sum_slabs": ([vp, i32, i64, vp, vp], i32),
+    "hvit_droppath_scale": ([i32, P(Dropout), vp, vp], i32),
+}
+
+EXPORTED = sorted(k for k in _SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libhvit.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"hvit: native library not found at {LIB_PATH}; run __graft_entry__.build() "
+                        "(there is no CPU or PyTorch fallback for the HIP path)")
+                h = C.CDLL(LIB_PATH)
+                for name, (args, res) in _SIGS.items():
+                    fn = getattr(h, name)
+                    fn.argtypes = args
+                    fn.restype = res
+                _lib = h
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().hvit_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+    return rc
+
+
+def stream_ptr(dev=None):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def dt_of(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"hvit: unsupported dtype {t.dtype}")
+
+
+def torch_dtype(dt: int):
+    return torch.float32 if dt == F32 else torch.bfloat16
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def dropout(p=0.0, seed=0, site=0) -> Dropout:
+    return Dropout(float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(site) & 0xFFFFFFFF)

@@ -1,0 +1,124 @@
+// Common device/host helpers for the HybridViT gfx950 kernels.
+//
+// Element types: activations and GEMM operands are either f32 (the parity path,
+// exact-f32 MFMA) or bf16 (the throughput path, bf16 MFMA, f32 accumulate).
+// Statistics, residual stream and weight gradients are always f32.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/hvit.h"
+
+typedef uint16_t bf16_t;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ errors --
+void hvit_set_error(const char* fmt, ...);
+#define HVIT_CHECK(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      hvit_set_error(__VA_ARGS__);            \
+      return HVIT_ERR_ARG;                    \
+    }                                         \
+  } while (0)
+#define HVIT_LAUNCH_CHECK()                                              \
+  do {                                                                   \
+    hipError_t e_ = hipGetLastError();                                   \
+    if (e_ != hipSuccess) {                                              \
+      hvit_set_error("%s: launch failed: %s", __func__, hipGetErrorString(e_)); \
+      return HVIT_ERR_LAUNCH;                                            \
+    }                                                                    \
+  } while (0)
+
+static inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+// ---------------------------------------------------------------- bf16 math --
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  // round-to-nearest-even; NaN stays NaN
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static constexpr int PER16 = 4;  // elements per 16 bytes
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
+};
+template <> struct Elem<bf16_t> {
+  static constexpr int PER16 = 8;
+  __device__ __forceinline__ static float to_f(bf16_t v) { return bf2f(v); }
+  __device__ __forceinline__ static bf16_t from_f(float v) { return f2bf(v); }
+};
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, long i) { return Elem<T>::to_f(p[i]); }
+template <typename T>
+__device__ __forceinline__ void stf(T* p, long i, float v) { p[i] = Elem<T>::from_f(v); }
+
+// runtime-dtype load/store (used by epilogues / elementwise kernels)
+__device__ __forceinline__ float ld_dt(const void* p, long i, int dt) {
+  return dt == HVIT_F32 ? ((const float*)p)[i] : bf2f(((const bf16_t*)p)[i]);
+}
+__device__ __forceinline__ void st_dt(void* p, long i, float v, int dt) {
+  if (dt == HVIT_F32) ((float*)p)[i] = v;
+  else ((bf16_t*)p)[i] = f2bf(v);
+}
+
+// ---------------------------------------------------------------- dropout RNG --
+// Counter-based: one 64-bit mix per group of four elements, 16 bits per element.
+// keep(i) == (u16(i) >= thr) with thr = round(p * 65536).  Forward and backward
+// regenerate identical masks from (seed, site, index).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t rng_u16(uint64_t seed, uint32_t site, uint64_t idx) {
+  uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
+  return (uint32_t)(h >> (16 * (idx & 3))) & 0xffffu;
+}
+__device__ __forceinline__ bool rng_keep(uint64_t seed, uint32_t site, uint64_t idx, uint32_t thr) {
+  return rng_u16(seed, site, idx) >= thr;
+}
+static inline uint32_t drop_threshold(float p) {
+  if (p <= 0.f) return 0;
+  double t = (double)p * 65536.0 + 0.5;
+  if (t > 65536.0) t = 65536.0;
+  return (uint32_t)t;
+}
+
+// ----------------------------------------------------------------- GELU(erf) --
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad(float x) {
+  float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ---------------------------------------------------------- wave reductions --
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,195 @@
+// Small memory-bound kernels around the hot path (gfx950): dtype casts, conv
+// weight (re)packing for the implicit GEMMs, dropout/drop-path gradient
+// scaling, tanh backward, column reductions (bias / pos-embed gradients) and
+// split-K slab reduction.
+#include "common.h"
+
+namespace hvit {
+
+static int grid_for(long n, int per_thread = 1) {
+  long g = (n / per_thread + 255) / 256;
+  if (g > 16384) g = 16384;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define GRID_STRIDE(i, total) \
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < (total); i += (long)gridDim.x * blockDim.x)
+
+__global__ void cast_kernel(const void* s, int sdt, void* d, int ddt, long n) {
+  GRID_STRIDE(i, n) st_dt(d, i, ld_dt(s, i, sdt), ddt);
+}
+
+// mode 0: out[co][ky][kx][ci] = w[co][ci][ky][kx]
+// mode 1: out[ci][ky][kx][co] = w[co][ci][KS-1-ky][KS-1-kx]   (dgrad, flipped)
+__global__ void conv_pack_kernel(const float* w, int Cout, int Cin, int KS, int mode, void* out, int odt) {
+  long total = (long)Cout * Cin * KS * KS;
+  GRID_STRIDE(i, total) {
+    int kx = i % KS;
+    long t = i / KS;
+    int ky = t % KS;
+    t /= KS;
+    int ci = t % Cin;
+    int co = t / Cin;
+    float v = w[i];
+    long o;
+    if (mode == 0) o = (((long)co * KS + ky) * KS + kx) * Cin + ci;
+    else o = (((long)ci * KS + (KS - 1 - ky)) * KS + (KS - 1 - kx)) * Cout + co;
+    st_dt(out, o, v, odt);
+  }
+}
+
+// dw[co][ci][ky][kx] = dwp[co][ky][kx][ci]
+__global__ void conv_unpack_kernel(const float* dwp, int Cout, int Cin, int KS, float* dw) {
+  long total = (long)Cout * Cin * KS * KS;
+  GRID_STRIDE(i, total) {
+    int kx = i % KS;
+    long t = i / KS;
+    int ky = t % KS;
+    t /= KS;
+    int ci = t % Cin;
+    int co = t / Cin;
+    dw[i] = dwp[(((long)co * KS + ky) * KS + kx) * Cin + ci];
+  }
+}
+
+// out[m][n] = g[m][n] * keep(m*N+n)/(1-p) * rowscale[m / rps]
+__global__ void dropout_scale_kernel(const void* g, int gdt, void* out, int odt, long M, int N, uint32_t thr,
+                                     float ds, unsigned long long seed, uint32_t site, const float* rowscale,
+                                     int rps) {
+  long total = M * N;
+  GRID_STRIDE(i, total) {
+    float v = ld_dt(g, i, gdt);
+    if (thr) v = rng_keep(seed, site, (uint64_t)i, thr) ? v * ds : 0.f;
+    if (rowscale) v *= rowscale[(i / N) / rps];
+    st_dt(out, i, v, odt);
+  }
+}
+
+__global__ void tanh_bwd_kernel(const void* dy, int dydt, const float* y, void* dz, int dzdt, long n) {
+  GRID_STRIDE(i, n) {
+    float t = y[i];
+    st_dt(dz, i, ld_dt(dy, i, dydt) * (1.f - t * t), dzdt);
+  }
+}
+
+// out[n] += sum_m x[m*ld + n]; block = 256 columns x row-chunk
+__global__ void reduce_rows_kernel(const void* x, int dt, long M, long N, long ld, int rows_per_block,
+                                   float* out) {
+  long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  long m0 = (long)blockIdx.y * rows_per_block;
+  long m1 = m0 + rows_per_block < M ? m0 + rows_per_block : M;
+  float s = 0.f;
+  for (long m = m0; m < m1; ++m) s += ld_dt(x, m * ld + n, dt);
+  atomicAdd(out + n, s);
+}
+
+__global__ void sum_slabs_kernel(const float* ws, int splits, long n, float* out) {
+  GRID_STRIDE(i, n) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(long)k * n + i];
+    out[i] = s;
+  }
+}
+
+__global__ void droppath_scale_kernel(int B, uint32_t thr, float ds, unsigned long long seed, uint32_t site,
+                                      float* out) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) out[b] = rng_keep(seed, site, (uint64_t)b, thr) ? ds : 0.f;
+}
+
+}  // namespace hvit
+
+using namespace hvit;
+
+extern "C" int hvit_cast(const void* src, int src_dt, void* dst, int dst_dt, long long n, void* stream) {
+  HVIT_CHECK(src && dst, "hvit_cast: null pointer");
+  if (n <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, src, src_dt, dst,
+                     dst_dt, (long)n);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_conv_weight_pack(const float* w, int Cout, int Cin, int KS, int mode, void* out,
+                                     int out_dt, void* stream) {
+  HVIT_CHECK(w && out, "hvit_conv_weight_pack: null pointer");
+  HVIT_CHECK(mode == 0 || mode == 1, "hvit_conv_weight_pack: mode");
+  long n = (long)Cout * Cin * KS * KS;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS,
+                     mode, out, out_dt);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_conv_weight_unpack(const float* dw_packed, int Cout, int Cin, int KS, float* dw,
+                                       void* stream) {
+  HVIT_CHECK(dw_packed && dw, "hvit_conv_weight_unpack: null pointer");
+  long n = (long)Cout * Cin * KS * KS;
+  hipLaunchKernelGGL(conv_unpack_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dw_packed, Cout,
+                     Cin, KS, dw);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, const hvit_dropout_t* dropout,
+                                  const float* rowscale, int rows_per_sample, void* out, int out_dt,
+                                  void* stream) {
+  HVIT_CHECK(g && out, "hvit_dropout_scale: null pointer");
+  HVIT_CHECK(!rowscale || rows_per_sample > 0, "hvit_dropout_scale: rows_per_sample");
+  uint32_t thr = dropout ? drop_threshold(dropout->p) : 0;
+  float ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
+  long total = (long)M * N;
+  if (total <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(dropout_scale_kernel, dim3(grid_for(total, 4)), dim3(256), 0, (hipStream_t)stream, g, g_dt,
+                     out, out_dt, (long)M, N, thr, ds, dropout ? dropout->seed : 0ull,
+                     dropout ? dropout->site : 0u, rowscale, rows_per_sample);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long long n, void* dz, int dz_dt,
+                             void* stream) {
+  HVIT_CHECK(dy && y && dz, "hvit_tanh_bwd: null pointer");
+  if (n <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(tanh_bwd_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, dy, dy_dt, y, dz,
+                     dz_dt, (long)n);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate,
+                                float* out, void* stream) {
+  HVIT_CHECK(x && out, "hvit_reduce_rows: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
+  if (M <= 0 || N <= 0) return HVIT_OK;
+  int rpb = 64;
+  long gy = (M + rpb - 1) / rpb;
+  long gx = (N + 255) / 256;
+  while (gx * gy > 65536 && rpb < (1 << 20)) { rpb *= 2; gy = (M + rpb - 1) / rpb; }
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, x, dt, (long)M,
+                     (long)N, (long)ld, rpb, out);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream) {
+  HVIT_CHECK(ws && out && splits > 0, "hvit_sum_slabs: bad args");
+  if (n <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, splits, (long)n,
+                     out);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_droppath_scale(int B, const hvit_dropout_t* dropout, float* out, void* stream) {
+  HVIT_CHECK(out && dropout && B > 0, "hvit_droppath_scale: bad args");
+  uint32_t thr = drop_threshold(dropout->p);
+  float ds = dropout->p > 0.f ? 1.f / (1.f - dropout->p) : 1.f;
+  hipLaunchKernelGGL(droppath_scale_kernel, dim3(cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, B, thr, ds,
+                     dropout->seed, dropout->site, out);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}

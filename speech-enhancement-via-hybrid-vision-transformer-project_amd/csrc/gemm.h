@@ -1,0 +1,432 @@
+// Tiled MFMA GEMM for gfx950 with pluggable operand loaders and fused epilogues.
+//
+//   C[m][n] = sum_k A(m, k) * B(n, k)         (both operands "row x reduction")
+//
+// Operands are staged global -> registers -> LDS as [rows][64 bytes of k] tiles
+// (k contiguous, 16-byte row pad).  Each lane reads one 16-byte fragment per
+// 16x16 sub-tile and issues
+//   bf16: one  v_mfma_f32_16x16x32_bf16 (8 k per lane)
+//   f32 : four v_mfma_f32_16x16x4_f32   (4 k per lane; the k-slots of the four
+//         MFMAs are a permutation of the 16 k's, identical for A and B)
+// so both precisions share the tile/LDS/fragment code.  Loaders either read k
+// contiguously (16-byte vectors straight into the LDS row) or read the row
+// dimension contiguously and scatter-transpose into LDS (wgrad / dgrad roles).
+// Implicit-GEMM loaders gather conv taps from NHWC activations on the fly
+// (3x3 same conv with optional nearest x2 upsample and two concatenated
+// sources; the 4x4/stride-4 patch embedding), so no im2col buffer exists.
+#pragma once
+#include "common.h"
+
+namespace hvit {
+
+constexpr int GEMM_THREADS = 256;
+constexpr int ROWB = 80;  // LDS row pitch in bytes (64 data + 16 pad)
+
+// ------------------------------------------------------------ loaders --------
+// vec(a, b): KC  -> 16 bytes of elements (row a, k = b .. b+E-1)
+//            !KC -> 16 bytes of elements (rows a .. a+E-1, k = b)
+template <typename T, bool KC_>
+struct LdDense {
+  static constexpr bool KC = KC_;
+  static constexpr int E = Elem<T>::PER16;
+  const T* p;
+  long ld;     // KC: elements between rows; !KC: elements between k
+  int rows;    // row extent
+  int K;       // reduction extent
+  bool vok;    // base 16-byte aligned and ld % E == 0 (vector loads legal)
+  __device__ __forceinline__ u32x4 vec(int a, int b) const {
+    u32x4 r = {0u, 0u, 0u, 0u};
+    if (KC) {
+      if (a >= rows || b >= K) return r;
+      const T* q = p + (long)a * ld + b;
+      if (vok && b + E <= K) return *(const u32x4*)q;
+      T tmp[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) tmp[e] = (b + e < K) ? q[e] : (T)0;
+      return *(u32x4*)tmp;
+    } else {
+      if (b >= K || a >= rows) return r;
+      const T* q = p + (long)b * ld + a;
+      if (vok && a + E <= rows) return *(const u32x4*)q;
+      T tmp[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) tmp[e] = (a + e < rows) ? q[e] : (T)0;
+      return *(u32x4*)tmp;
+    }
+  }
+};
+
+// Implicit im2col over NHWC sources.  Row index = output pixel (n, oy, ox) of a
+// Ho x Wo grid; reduction index = (ky*KS + kx)*Ctot + c.  The conv input image
+// is concat(src1[C1], src2[C2]) upsampled (nearest) by U from Hs x Ws.
+template <typename T, bool KC_>
+struct LdConv {
+  static constexpr bool KC = KC_;
+  static constexpr int E = Elem<T>::PER16;
+  const T* src1;
+  const T* src2;
+  int C1, C2, Ctot;
+  int Hs, Ws, U, Hi, Wi;  // source dims, upsample, conv-input dims
+  int KS, S, Pd;          // kernel, stride, pad
+  int Ho, Wo;             // output grid
+  int P;                  // number of output pixels (N*Ho*Wo)
+  int Kt;                 // KS*KS*Ctot
+  bool vec_ok;            // C1 % E == 0 && C2 % E == 0
+
+  __device__ __forceinline__ float elem_f(int p, int k) const {
+    if (p >= P || k >= Kt) return 0.f;
+    int hw = Ho * Wo;
+    int n = p / hw, rem = p - n * hw;
+    int oy = rem / Wo, ox = rem - oy * Wo;
+    int tap = k / Ctot, c = k - tap * Ctot;
+    int ky = tap / KS, kx = tap - ky * KS;
+    int iy = oy * S - Pd + ky, ix = ox * S - Pd + kx;
+    if (iy < 0 || ix < 0 || iy >= Hi || ix >= Wi) return 0.f;
+    int sy = iy / U, sx = ix / U;
+    long pix = ((long)n * Hs + sy) * Ws + sx;
+    return c < C1 ? Elem<T>::to_f(src1[pix * C1 + c]) : Elem<T>::to_f(src2[pix * C2 + (c - C1)]);
+  }
+  // E consecutive reduction indices k..k+E-1 at pixel p
+  __device__ __forceinline__ u32x4 gather(int p, int k) const {
+    u32x4 r = {0u, 0u, 0u, 0u};
+    if (vec_ok) {
+      if (p >= P || k >= Kt) return r;
+      int hw = Ho * Wo;
+      int n = p / hw, rem = p - n * hw;
+      int oy = rem / Wo, ox = rem - oy * Wo;
+      int tap = k / Ctot, c = k - tap * Ctot;
+      int ky = tap / KS, kx = tap - ky * KS;
+      int iy = oy * S - Pd + ky, ix = ox * S - Pd + kx;
+      if (iy < 0 || ix < 0 || iy >= Hi || ix >= Wi) return r;
+      int sy = iy / U, sx = ix / U;
+      long pix = ((long)n * Hs + sy) * Ws + sx;
+      const T* q = c < C1 ? src1 + pix * C1 + c : src2 + pix * C2 + (c - C1);
+      return *(const u32x4*)q;
+    }
+    T tmp[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) tmp[e] = Elem<T>::from_f(elem_f(p, k + e));
+    return *(u32x4*)tmp;
+  }
+  // role A (KC): a = pixel, b = k.   role B (!KC, wgrad): a = im2col k, b = pixel
+  __device__ __forceinline__ u32x4 vec(int a, int b) const {
+    return KC ? gather(a, b) : gather(b, a);
+  }
+};
+
+// ------------------------------------------------------------ epilogue -------
+enum EpiMode { EPI_STORE = 0, EPI_SLAB = 1, EPI_PATCH = 2, EPI_SPLIT2 = 3 };
+enum EpiAct { ACT_NONE = 0, ACT_GELU_DUAL = 1, ACT_TANH = 2, ACT_GELU_BWD = 3 };
+
+struct Epi {
+  int mode = EPI_STORE;
+  void* out = nullptr;
+  int out_dt = HVIT_F32;
+  long ldo = 0;
+  void* out2 = nullptr;  // GELU_DUAL: activation output; SPLIT2: columns >= split_col
+  int out2_dt = HVIT_F32;
+  long ldo2 = 0;
+  int split_col = 0;
+  const float* bias = nullptr;
+  const float* rowadd = nullptr;  // v += rowadd[(m % rowadd_mod) * rowadd_ld + n]
+  long rowadd_ld = 0;
+  int rowadd_mod = 1;
+  int act = ACT_NONE;
+  const void* aux = nullptr;  // GELU_BWD: pre-activation h[m][n]
+  int aux_dt = HVIT_F32;
+  long ldaux = 0;
+  uint32_t drop_thr = 0;  // dropout keep test (0 = off)
+  float drop_scale = 1.f;
+  unsigned long long seed = 0;
+  uint32_t site = 0;
+  const float* resid = nullptr;  // v = resid[m][n] + rowscale[m / rps] * v
+  long ldr = 0;
+  const float* rowscale = nullptr;
+  int rows_per_sample = 1;
+  float* stats = nullptr;   // BN partials [row_tile][N][2] = (mean, M2)
+  float* colsum = nullptr;  // atomic column sums of the final v
+  // EPI_PATCH: m = token (b, py, px) of Hp x Wp, n = (ky*P + kx)*C + c
+  int pP = 0, pC = 0, pHp = 0, pWp = 0, pH = 0, pW = 0;
+};
+
+template <typename T, int BM, int BN, class LA, class LB>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M, int N, int K,
+                                                            int kps, Epi ep) {
+  constexpr int E = Elem<T>::PER16;
+  constexpr int BK = 64 / sizeof(T);
+  constexpr int WM = 2, WN = 2;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int CA = BM * 4 / GEMM_THREADS;  // 16-byte chunks per thread
+  constexpr int CB = BN * 4 / GEMM_THREADS;
+  static_assert(CA >= 1 && CB >= 1, "tile too small");
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB];
+  char* As = smem;
+  char* Bs = smem + 2 * BM * ROWB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * kps;
+  const int kend = min(K, kbeg + kps);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[CA], rb[CB];
+
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      int ch = tid + c * GEMM_THREADS;
+      if (LA::KC) {
+        int r = ch >> 2, kc = ch & 3;
+        int kk = k0 + kc * E;
+        ra[c] = (kk < kend) ? la.vec(m0 + r, kk) : (u32x4){0u, 0u, 0u, 0u};
+      } else {
+        int kr = ch / (BM / E), mc = ch % (BM / E);
+        int kk = k0 + kr;
+        ra[c] = (kk < kend) ? la.vec(m0 + mc * E, kk) : (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      int ch = tid + c * GEMM_THREADS;
+      if (LB::KC) {
+        int r = ch >> 2, kc = ch & 3;
+        int kk = k0 + kc * E;
+        rb[c] = (kk < kend) ? lb.vec(n0 + r, kk) : (u32x4){0u, 0u, 0u, 0u};
+      } else {
+        int kr = ch / (BN / E), nc = ch % (BN / E);
+        int kk = k0 + kr;
+        rb[c] = (kk < kend) ? lb.vec(n0 + nc * E, kk) : (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  auto stash = [&](int buf) {
+    char* a = As + buf * BM * ROWB;
+    char* b = Bs + buf * BN * ROWB;
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      int ch = tid + c * GEMM_THREADS;
+      if (LA::KC) {
+        int r = ch >> 2, kc = ch & 3;
+        *(u32x4*)(a + r * ROWB + kc * 16) = ra[c];
+      } else {
+        int kr = ch / (BM / E), mc = ch % (BM / E);
+        const T* v = (const T*)&ra[c];
+#pragma unroll
+        for (int e = 0; e < E; ++e) *(T*)(a + (mc * E + e) * ROWB + kr * sizeof(T)) = v[e];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      int ch = tid + c * GEMM_THREADS;
+      if (LB::KC) {
+        int r = ch >> 2, kc = ch & 3;
+        *(u32x4*)(b + r * ROWB + kc * 16) = rb[c];
+      } else {
+        int kr = ch / (BN / E), nc = ch % (BN / E);
+        const T* v = (const T*)&rb[c];
+#pragma unroll
+        for (int e = 0; e < E; ++e) *(T*)(b + (nc * E + e) * ROWB + kr * sizeof(T)) = v[e];
+      }
+    }
+  };
+
+  if (nk > 0) {
+    fetch(kbeg);
+    stash(0);
+    __syncthreads();
+  }
+  const int frow = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) fetch(kbeg + (t + 1) * BK);
+    const char* a = As + buf * BM * ROWB + (wm * WTM + frow) * ROWB + fq * 16;
+    const char* b = Bs + buf * BN * ROWB + (wn * WTN + frow) * ROWB + fq * 16;
+    u32x4 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = *(const u32x4*)(a + i * 16 * ROWB);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = *(const u32x4*)(b + j * 16 * ROWB);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (sizeof(T) == 2) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(s16x8, fa[i]), __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+        } else {
+          f32x4 va = __builtin_bit_cast(f32x4, fa[i]);
+          f32x4 vb = __builtin_bit_cast(f32x4, fb[j]);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[0], vb[0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[1], vb[1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[2], vb[2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[3], vb[3], acc[i][j], 0, 0, 0);
+        }
+      }
+    if (t + 1 < nk) stash(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------- epilogue ---
+  // element (i, j, r): m = m0 + wm*WTM + i*16 + fq*4 + r ; n = n0 + wn*WTN + j*16 + frow
+  const int mb = m0 + wm * WTM + fq * 4;
+  const int nb = n0 + wn * WTN + frow;
+  if (ep.mode == EPI_SLAB) {
+    float* slab = (float*)ep.out + (long)blockIdx.z * M * ep.ldo;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int m = mb + i * 16 + r, n = nb + j * 16;
+          if (m < M && n < N) slab[(long)m * ep.ldo + n] = acc[i][j][r];
+        }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int m = mb + i * 16 + r, n = nb + j * 16;
+        if (m >= M || n >= N) continue;
+        float v = acc[i][j][r];
+        if (ep.bias) v += ep.bias[n];
+        if (ep.rowadd) v += ep.rowadd[(long)(m % ep.rowadd_mod) * ep.rowadd_ld + n];
+        uint64_t didx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
+        if (ep.act == ACT_GELU_DUAL) {
+          st_dt(ep.out, (long)m * ep.ldo + n, v, ep.out_dt);
+          float g = gelu_f(v);
+          if (ep.drop_thr && !rng_keep(ep.seed, ep.site, didx, ep.drop_thr)) g = 0.f;
+          else g *= ep.drop_scale;
+          st_dt(ep.out2, (long)m * ep.ldo2 + n, g, ep.out2_dt);
+          acc[i][j][r] = v;
+          continue;
+        }
+        if (ep.act == ACT_TANH) v = tanhf(v);
+        if (ep.drop_thr) v = rng_keep(ep.seed, ep.site, didx, ep.drop_thr) ? v * ep.drop_scale : 0.f;
+        else if (ep.drop_scale != 1.f) v *= ep.drop_scale;
+        if (ep.act == ACT_GELU_BWD) v *= gelu_grad(ld_dt(ep.aux, (long)m * ep.ldaux + n, ep.aux_dt));
+        if (ep.resid) {
+          float s = ep.rowscale ? ep.rowscale[m / ep.rows_per_sample] : 1.f;
+          v = ep.resid[(long)m * ep.ldr + n] + s * v;
+        }
+        acc[i][j][r] = v;
+        if (ep.mode == EPI_STORE) {
+          st_dt(ep.out, (long)m * ep.ldo + n, v, ep.out_dt);
+        } else if (ep.mode == EPI_SPLIT2) {
+          if (n < ep.split_col) st_dt(ep.out, (long)m * ep.ldo + n, v, ep.out_dt);
+          else st_dt(ep.out2, (long)m * ep.ldo2 + (n - ep.split_col), v, ep.out2_dt);
+        } else {  // EPI_PATCH
+          int hw = ep.pHp * ep.pWp;
+          int b = m / hw, rem = m - b * hw;
+          int py = rem / ep.pWp, px = rem - py * ep.pWp;
+          int tap = n / ep.pC, c = n - tap * ep.pC;
+          int ky = tap / ep.pP, kx = tap - ky * ep.pP;
+          long o = (((long)b * ep.pH + py * ep.pP + ky) * ep.pW + px * ep.pP + kx) * ep.pC + c;
+          st_dt(ep.out, o, v, ep.out_dt);
+        }
+      }
+
+  if (ep.colsum) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (mb + i * 16 + r < M) s += acc[i][j][r];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      int n = nb + j * 16;
+      if (fq == 0 && n < N) atomicAdd(ep.colsum + n, s);
+    }
+  }
+
+  if (ep.stats) {
+    // per-column (mean, M2) over this tile's valid rows, two passes on-chip
+    float* red = (float*)smem;  // [WM][BN]
+    const int rows_valid = min(BM, M - m0);
+    float colmean[FN];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (mb + i * 16 + r < M) {
+              float v = acc[i][j][r];
+              if (pass == 0) s += v;
+              else { float d = v - colmean[j]; s += d * d; }
+            }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (fq == 0) red[wm * BN + wn * WTN + j * 16 + frow] = s;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        int cl = wn * WTN + j * 16 + frow;
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) tot += red[w * BN + cl];
+        if (pass == 0) colmean[j] = tot / (float)rows_valid;
+        else if (wm == 0 && fq == 0 && n0 + cl < N) {
+          float* o = ep.stats + ((long)blockIdx.x * N + n0 + cl) * 2;
+          o[0] = colmean[j];
+          o[1] = tot;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// host-side launcher --------------------------------------------------------
+template <typename T, class LA, class LB>
+int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep, hipStream_t st,
+                int force_tile = 0) {
+  if (M <= 0 || N <= 0) return HVIT_OK;
+  constexpr int BK = 64 / sizeof(T);
+  if (splits < 1) splits = 1;
+  int kps = (K + splits - 1) / splits;
+  kps = ((kps + BK - 1) / BK) * BK;
+  splits = K > 0 ? (K + kps - 1) / kps : 1;
+  if (splits > 1 && ep.mode != EPI_SLAB) {
+    hvit_set_error("launch_gemm: split-K requires EPI_SLAB");
+    return HVIT_ERR_ARG;
+  }
+  int big = force_tile ? (force_tile == 128)
+                       : ((long)cdiv(M, 128) * cdiv(N, 128) * splits >= 160);
+  if (ep.stats) big = 1;  // stats partial layout is per 128-row tile
+  if (big) {
+    dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
+    hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb,
+                       M, N, K, kps, ep);
+  } else {
+    dim3 g(cdiv(M, 64), cdiv(N, 64), splits);
+    hipLaunchKernelGGL((gemm_kernel<T, 64, 64, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb, M,
+                       N, K, kps, ep);
+  }
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+}  // namespace hvit

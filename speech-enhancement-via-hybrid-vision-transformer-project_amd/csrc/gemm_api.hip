@@ -1,0 +1,289 @@
+// C-ABI entry points built on the MFMA GEMM template (gemm.h):
+//   Linear fwd / dgrad / wgrad  (nn.Linear in attention.py:55,58 and
+//     components.py:224,227; to_feature_map hybrid_vit.py:153; the 1x1 skip
+//     projections hybrid_vit.py:158-165 on NHWC pixels)
+//   Conv fwd / dgrad / wgrad     (3x3 ConvBlock / TransposeConvBlock convs,
+//     components.py:55-62, :149-158, with nearest-x2 upsample and the decoder's
+//     channel concat folded into the operand gather; the k=s=4 patch embedding,
+//     components.py:275-280, with the [B,N,D] token layout written directly).
+#include "gemm.h"
+
+using namespace hvit;
+
+namespace {
+
+Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
+  Epi ep;
+  ep.out = out;
+  ep.out_dt = out_dt;
+  ep.ldo = ldo;
+  if (!e) return ep;
+  ep.act = e->act;
+  ep.out2 = e->out2;
+  ep.out2_dt = e->out2_dt;
+  ep.ldo2 = ldo;
+  ep.aux = e->aux;
+  ep.aux_dt = e->aux_dt;
+  ep.ldaux = ldo;
+  if (e->dropout.p > 0.f) {
+    ep.drop_thr = drop_threshold(e->dropout.p);
+    ep.drop_scale = 1.f / (1.f - e->dropout.p);
+    ep.seed = e->dropout.seed;
+    ep.site = e->dropout.site;
+  }
+  ep.resid = e->resid;
+  ep.ldr = ldo;
+  ep.rowscale = e->rowscale;
+  ep.rows_per_sample = e->rows_per_sample > 0 ? e->rows_per_sample : 1;
+  ep.rowadd = e->rowadd;
+  ep.rowadd_ld = ldo;
+  ep.rowadd_mod = e->rowadd_rows > 0 ? e->rowadd_rows : 1;
+  ep.colsum = e->colsum;
+  return ep;
+}
+
+int check_epi(const hvit_epilogue_t* e) {
+  if (!e) return HVIT_OK;
+  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_GELU_BWD, "epilogue: bad act %d", e->act);
+  HVIT_CHECK(e->act != HVIT_ACT_GELU_DUAL || e->out2, "epilogue: GELU_DUAL needs out2");
+  HVIT_CHECK(e->act != HVIT_ACT_GELU_BWD || e->aux, "epilogue: GELU_BWD needs aux");
+  HVIT_CHECK(!(e->dropout.p < 0.f || e->dropout.p >= 1.f), "epilogue: dropout p out of range");
+  return HVIT_OK;
+}
+
+// choose split-K so that a wgrad launch has enough workgroups
+int wgrad_splits(long M, long N, long K, int bk) {
+  long tiles = (long)cdiv(M, 64) * cdiv(N, 64);
+  long want = (512 + tiles - 1) / tiles;
+  long maxs = K / (4 * bk);
+  if (want > maxs) want = maxs;
+  if (want > 256) want = 256;
+  if (want < 1) want = 1;
+  return (int)want;
+}
+
+template <typename T>
+LdConv<T, true> conv_a(const hvit_conv_geom_t* g, const void* s1, int C1, const void* s2, int C2, int Hs, int Ws,
+                       int U, int KS, int S, int Pd) {
+  LdConv<T, true> l;
+  l.src1 = (const T*)s1;
+  l.src2 = (const T*)s2;
+  l.C1 = C1;
+  l.C2 = C2;
+  l.Ctot = C1 + C2;
+  l.Hs = Hs;
+  l.Ws = Ws;
+  l.U = U;
+  l.Hi = Hs * U;
+  l.Wi = Ws * U;
+  l.KS = KS;
+  l.S = S;
+  l.Pd = Pd;
+  l.Ho = (l.Hi + 2 * Pd - KS) / S + 1;
+  l.Wo = (l.Wi + 2 * Pd - KS) / S + 1;
+  l.P = g->N * l.Ho * l.Wo;
+  l.Kt = KS * KS * l.Ctot;
+  constexpr int E = Elem<T>::PER16;
+  l.vec_ok = (C1 % E == 0) && (C2 % E == 0) && aligned16(s1) && (!s2 || aligned16(s2));
+  return l;
+}
+
+template <typename T, bool KC>
+LdDense<T, KC> dense(const void* p, long ld, int rows, int K) {
+  LdDense<T, KC> l;
+  l.p = (const T*)p;
+  l.ld = ld;
+  l.rows = rows;
+  l.K = K;
+  l.vok = aligned16(p) && (ld % Elem<T>::PER16 == 0);
+  return l;
+}
+
+int check_geom(const hvit_conv_geom_t* g) {
+  HVIT_CHECK(g && g->src1, "conv: null geometry/source");
+  HVIT_CHECK(g->C1 > 0 && g->C2 >= 0 && (g->C2 == 0 || g->src2), "conv: bad channels");
+  HVIT_CHECK(g->N > 0 && g->Hs > 0 && g->Ws > 0 && g->U >= 1 && g->KS > 0 && g->stride > 0 && g->pad >= 0,
+             "conv: bad geometry");
+  HVIT_CHECK(g->Cout > 0, "conv: bad Cout");
+  return HVIT_OK;
+}
+
+}  // namespace
+
+#define DT_DISPATCH(dt, ...)                   \
+  if ((dt) == HVIT_BF16) {                     \
+    using T = bf16_t;                          \
+    __VA_ARGS__;                               \
+  } else if ((dt) == HVIT_F32) {               \
+    using T = float;                           \
+    __VA_ARGS__;                               \
+  } else {                                     \
+    hvit_set_error("bad dtype %d", (int)(dt)); \
+    return HVIT_ERR_ARG;                       \
+  }
+
+extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int M, int N, int K,
+                               void* y, int y_dt, const hvit_epilogue_t* epi, void* stream) {
+  HVIT_CHECK(x && w && y, "hvit_linear_fwd: null pointer");
+  HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_fwd: bad shape M=%d N=%d K=%d", M, N, K);
+  HVIT_CHECK(aligned16(x) && aligned16(w), "hvit_linear_fwd: x/w must be 16-byte aligned");
+  if (int rc = check_epi(epi)) return rc;
+  Epi ep = to_epi(epi, y, y_dt, N);
+  ep.bias = bias;
+  DT_DISPATCH(dt, {
+    HVIT_CHECK(K % Elem<T>::PER16 == 0, "hvit_linear_fwd: K=%d must be a multiple of %d", K, Elem<T>::PER16);
+    return launch_gemm<T>(dense<T, true>(x, K, M, K), dense<T, true>(w, K, N, K), M, N, K, 1, ep,
+                          (hipStream_t)stream);
+  });
+}
+
+extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, int N, int K, void* dx, int dx_dt,
+                                 const hvit_epilogue_t* epi, void* stream) {
+  HVIT_CHECK(dy && w && dx, "hvit_linear_dgrad: null pointer");
+  HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_dgrad: bad shape");
+  HVIT_CHECK(aligned16(dy) && aligned16(w), "hvit_linear_dgrad: alignment");
+  if (int rc = check_epi(epi)) return rc;
+  Epi ep = to_epi(epi, dx, dx_dt, K);
+  DT_DISPATCH(dt, {
+    HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_dgrad: N, K alignment");
+    return launch_gemm<T>(dense<T, true>(dy, N, M, N), dense<T, false>(w, K, K, N), M, K, N, 1, ep,
+                          (hipStream_t)stream);
+  });
+}
+
+extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
+  // dw is [N_out x K_in] reduced over M rows ; slabs only when splitting
+  int s = wgrad_splits(N, K, M, 32);
+  return s > 1 ? (long long)s * N * K : 0;
+}
+
+extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* ws,
+                                 long long ws_elems, void* stream) {
+  HVIT_CHECK(dy && x && dw, "hvit_linear_wgrad: null pointer");
+  HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_wgrad: bad shape");
+  HVIT_CHECK(aligned16(dy) && aligned16(x), "hvit_linear_wgrad: alignment");
+  hipStream_t st = (hipStream_t)stream;
+  int splits = wgrad_splits(N, K, M, 32);
+  if ((long long)splits * N * K > ws_elems || !ws) splits = 1;
+  if (M == 0) {
+    (void)hipMemsetAsync(dw, 0, sizeof(float) * N * K, st);
+    return HVIT_OK;
+  }
+  Epi ep;
+  ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
+  ep.out = splits > 1 ? (void*)ws : (void*)dw;
+  ep.out_dt = HVIT_F32;
+  ep.ldo = K;
+  DT_DISPATCH(dt, {
+    HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_wgrad: N, K alignment");
+    int rc = launch_gemm<T>(dense<T, false>(dy, N, N, M), dense<T, false>(x, K, K, M), N, K, M, splits, ep, st,
+                            splits > 1 ? 64 : 0);
+    if (rc) return rc;
+  });
+  if (splits > 1) return hvit_sum_slabs(ws, splits, (long long)N * K, dw, stream);
+  return HVIT_OK;
+}
+
+extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* bias,
+                             void* y, int y_dt, float* bn_partials, const hvit_epilogue_t* epi, void* stream) {
+  if (int rc = check_geom(g)) return rc;
+  HVIT_CHECK(w_packed && y, "hvit_conv_fwd: null pointer");
+  if (int rc = check_epi(epi)) return rc;
+  HVIT_CHECK(!epi || epi->act == HVIT_ACT_NONE || epi->act == HVIT_ACT_TANH,
+             "hvit_conv_fwd: act must be NONE or TANH");
+  HVIT_CHECK(!epi || !epi->resid, "hvit_conv_fwd: residual epilogue unsupported");
+  HVIT_CHECK(aligned16(w_packed), "hvit_conv_fwd: weight alignment");
+  Epi ep = to_epi(epi, y, y_dt, g->Cout);
+  ep.bias = bias;
+  ep.stats = bn_partials;
+  DT_DISPATCH(dt, {
+    auto la = conv_a<T>(g, g->src1, g->C1, g->src2, g->C2, g->Hs, g->Ws, g->U, g->KS, g->stride, g->pad);
+    HVIT_CHECK(la.Ho > 0 && la.Wo > 0, "hvit_conv_fwd: empty output");
+    int Kt = la.Kt;
+    // odd reduction length (Cin=1 first conv): weights take the scalar load path
+    return launch_gemm<T>(la, dense<T, true>(w_packed, Kt, g->Cout, Kt), la.P, g->Cout, Kt, 1, ep,
+                          (hipStream_t)stream);
+  });
+}
+
+extern "C" int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy, const void* w, void* dx,
+                               int dx_dt, void* stream) {
+  if (int rc = check_geom(g)) return rc;
+  HVIT_CHECK(dy && w && dx, "hvit_conv_dgrad: null pointer");
+  HVIT_CHECK(aligned16(dy) && aligned16(w), "hvit_conv_dgrad: alignment");
+  hipStream_t st = (hipStream_t)stream;
+  const int Ctot = g->C1 + g->C2;
+  const int Hi = g->Hs * g->U, Wi = g->Ws * g->U;
+  const int Ho = (Hi + 2 * g->pad - g->KS) / g->stride + 1;
+  const int Wo = (Wi + 2 * g->pad - g->KS) / g->stride + 1;
+  if (g->KS == g->stride && g->pad == 0) {
+    // non-overlapping patches: dX[patch pixel] = dT[token] . W  scattered back (col2im)
+    HVIT_CHECK(g->U == 1 && g->C2 == 0, "hvit_conv_dgrad: patch path needs U=1, one source");
+    if (Ho * g->KS != Hi || Wo * g->KS != Wi)
+      (void)hipMemsetAsync(dx, 0, (size_t)g->N * Hi * Wi * Ctot * (dx_dt == HVIT_F32 ? 4 : 2), st);
+    Epi ep;
+    ep.mode = EPI_PATCH;
+    ep.out = dx;
+    ep.out_dt = dx_dt;
+    ep.pP = g->KS;
+    ep.pC = Ctot;
+    ep.pHp = Ho;
+    ep.pWp = Wo;
+    ep.pH = Hi;
+    ep.pW = Wi;
+    const int Kt = g->KS * g->KS * Ctot;
+    const int M = g->N * Ho * Wo;
+    DT_DISPATCH(dt, {
+      HVIT_CHECK(g->Cout % Elem<T>::PER16 == 0 && Kt % Elem<T>::PER16 == 0, "hvit_conv_dgrad: patch alignment");
+      return launch_gemm<T>(dense<T, true>(dy, g->Cout, M, g->Cout), dense<T, false>(w, Kt, Kt, g->Cout), M, Kt,
+                            g->Cout, 1, ep, st);
+    });
+  }
+  HVIT_CHECK(g->stride == 1 && g->pad == g->KS / 2 && (g->KS & 1), "hvit_conv_dgrad: only odd same-convs");
+  Epi ep;
+  ep.out = dx;
+  ep.out_dt = dx_dt;
+  ep.ldo = Ctot;
+  DT_DISPATCH(dt, {
+    // dU = conv(dy, flipped/transposed W): im2col over dy (Cout channels, stride 1)
+    auto la = conv_a<T>(g, dy, g->Cout, nullptr, 0, Ho, Wo, 1, g->KS, 1, g->pad);
+    int Kt = la.Kt;
+    return launch_gemm<T>(la, dense<T, true>(w, Kt, Ctot, Kt), la.P, Ctot, Kt, 1, ep, st);
+  });
+}
+
+extern "C" long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g) {
+  if (!g) return 0;
+  const int Hi = g->Hs * g->U, Wi = g->Ws * g->U;
+  const long Ho = (Hi + 2 * g->pad - g->KS) / g->stride + 1;
+  const long Wo = (Wi + 2 * g->pad - g->KS) / g->stride + 1;
+  const long Kt = (long)g->KS * g->KS * (g->C1 + g->C2);
+  int s = wgrad_splits(g->Cout, Kt, g->N * Ho * Wo, 32);
+  return s > 1 ? (long long)s * g->Cout * Kt : 0;
+}
+
+extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy, float* dw_packed, float* ws,
+                               long long ws_elems, void* stream) {
+  if (int rc = check_geom(g)) return rc;
+  HVIT_CHECK(dy && dw_packed, "hvit_conv_wgrad: null pointer");
+  HVIT_CHECK(aligned16(dy), "hvit_conv_wgrad: alignment");
+  hipStream_t st = (hipStream_t)stream;
+  DT_DISPATCH(dt, {
+    auto la = conv_a<T>(g, g->src1, g->C1, g->src2, g->C2, g->Hs, g->Ws, g->U, g->KS, g->stride, g->pad);
+    LdConv<T, false> lb;
+    static_assert(sizeof(lb) == sizeof(la), "layout");
+    __builtin_memcpy(&lb, &la, sizeof(la));
+    const int M = g->Cout, N = la.Kt, K = la.P;
+    int splits = wgrad_splits(M, N, K, 32);
+    if ((long long)splits * M * N > ws_elems || !ws) splits = 1;
+    Epi ep;
+    ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
+    ep.out = splits > 1 ? (void*)ws : (void*)dw_packed;
+    ep.out_dt = HVIT_F32;
+    ep.ldo = N;
+    int rc = launch_gemm<T>(dense<T, false>(dy, M, M, K), lb, M, N, K, splits, ep, st, splits > 1 ? 64 : 0);
+    if (rc) return rc;
+    if (splits > 1) return hvit_sum_slabs(ws, splits, (long long)M * N, dw_packed, stream);
+    return HVIT_OK;
+  });
+}

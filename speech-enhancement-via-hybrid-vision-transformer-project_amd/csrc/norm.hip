@@ -1,0 +1,421 @@
+// LayerNorm (attention.py:152-153, :271) and the BatchNorm2d -> ReLU ->
+// Dropout2d -> MaxPool2d tail of ConvBlock / TransposeConvBlock
+// (components.py:55-99, :144-192) for gfx950.
+//
+// LayerNorm: one wave per row, float4 lanes, two-pass mean/variance in
+// registers.  Backward writes dx into the f32 residual-gradient stream and
+// accumulates dgamma/dbeta per workgroup (64 rows) before one atomic per column.
+//
+// BatchNorm (train): the producing conv GEMM writes per-128-row-tile
+// (mean, M2) partials; bn_finalize merges them (Chan et al.) into the batch
+// mean / inverse std and updates running stats (momentum, unbiased variance)
+// exactly as torch does.  bn_act_fwd applies normalise + affine + ReLU +
+// per-(sample, channel) dropout mask + 2x2 max-pool in one pass over NHWC.
+// Backward recomputes the pre-pool activations from z to route the pooled
+// gradient to the first maximum of each window (torch's tie rule), then a
+// reduce pass (sum g, sum g*xhat per channel) and an apply pass.
+#include "common.h"
+
+namespace hvit {
+
+// ------------------------------------------------------------- LayerNorm ---
+template <typename TY, int MAXV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                    const float* __restrict__ b, TY* __restrict__ y,
+                                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                    int M, int D, float eps) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long)row * D;
+  f32x4 v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    int c = lane * 4 + i * 256;
+    v[i] = c < D ? *(const f32x4*)(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    int c = lane * 4 + i * 256;
+    if (c < D)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { float d = v[i][e] - mean; q += d * d; }
+  }
+  float var = wave_sum(q) / (float)D;
+  float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    int c = lane * 4 + i * 256;
+    if (c < D)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        y[(long)row * D + c + e] = Elem<TY>::from_f((v[i][e] - mean) * rstd * g[c + e] + b[c + e]);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// rows per workgroup for the backward (4 waves x 16 rows)
+constexpr int LNB_ROWS = 64;
+
+template <typename TD, int MAXV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, const float* __restrict__ x,
+                                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                    const float* __restrict__ g, const float* __restrict__ resid,
+                                                    float* __restrict__ dx, float* __restrict__ dgamma,
+                                                    float* __restrict__ dbeta, int M, int D) {
+  __shared__ float red[4][2][1024];
+  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x4 ag[MAXV], ab[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) ag[i] = ab[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int rr = 0; rr < LNB_ROWS / 4; ++rr) {
+    int row = blockIdx.x * LNB_ROWS + w * (LNB_ROWS / 4) + rr;
+    if (row >= M) break;
+    float mu = mean[row], rs = rstd[row];
+    f32x4 xh[MAXV], gy[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      int c = lane * 4 + i * 256;
+      if (c < D) {
+        f32x4 xv = *(const f32x4*)(x + (long)row * D + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float d = Elem<TD>::to_f(dy[(long)row * D + c + e]);
+          float xhat = (xv[e] - mu) * rs;
+          xh[i][e] = xhat;
+          gy[i][e] = d * g[c + e];
+          s1 += gy[i][e];
+          s2 += gy[i][e] * xhat;
+          ag[i][e] += d * xhat;
+          ab[i][e] += d;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)D;
+    s2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      int c = lane * 4 + i * 256;
+      if (c < D) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (gy[i][e] - s1 - xh[i][e] * s2);
+        if (resid) o += *(const f32x4*)(resid + (long)row * D + c);
+        *(f32x4*)(dx + (long)row * D + c) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    int c = lane * 4 + i * 256;
+    if (c < D)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { red[w][0][c + e] = ag[i][e]; red[w][1][c + e] = ab[i][e]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    float bb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    atomicAdd(dgamma + c, a);
+    atomicAdd(dbeta + c, bb);
+  }
+}
+
+// ------------------------------------------------------------- BatchNorm ---
+// partials[t][c] = (mean, M2) over cnt_t rows; cnt_t = tile_rows except the last.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int ntiles, int tile_rows,
+                                                         long M, int C, float* __restrict__ mean_out,
+                                                         float* __restrict__ invstd_out, float* __restrict__ rmean,
+                                                         float* __restrict__ rvar, float momentum, float eps,
+                                                         long long* nbt) {
+  __shared__ float sn[256], sm[256], sq[256];
+  int c = blockIdx.x;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int t = threadIdx.x; t < ntiles; t += 256) {
+    float nb = (float)min((long)tile_rows, M - (long)t * tile_rows);
+    float mb = part[((long)t * C + c) * 2], qb = part[((long)t * C + c) * 2 + 1];
+    float nn = n + nb;
+    float d = mb - mu;
+    mu += d * (nb / nn);
+    m2 += qb + d * d * (n * nb / nn);
+    n = nn;
+  }
+  sn[threadIdx.x] = n; sm[threadIdx.x] = mu; sq[threadIdx.x] = m2;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      float na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
+      float nn = na + nb;
+      if (nb > 0.f) {
+        float d = sm[threadIdx.x + s] - sm[threadIdx.x];
+        sm[threadIdx.x] += d * (nb / nn);
+        sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * (na * nb / nn);
+        sn[threadIdx.x] = nn;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float mean = sm[0], var = sq[0] / (float)M;
+    mean_out[c] = mean;
+    invstd_out[c] = rsqrtf(var + eps);
+    if (rmean) {
+      float unb = M > 1 ? sq[0] / (float)(M - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+    }
+    if (nbt && c == 0) *nbt += 1;
+  }
+}
+
+__global__ void bn_eval_prep_kernel(const float* rmean, const float* rvar, int C, float eps, float* mean_out,
+                                    float* invstd_out) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    mean_out[c] = rmean[c];
+    invstd_out[c] = rsqrtf(rvar[c] + eps);
+  }
+}
+
+struct BnAct {
+  const void* z; int dt;      // pre-BN conv output, NHWC [N, H, W, C]
+  int N, H, W, C, pool;       // pool: 1 or 2
+  const float* mean; const float* invstd; const float* gamma; const float* beta;
+  uint32_t thr; float dscale; unsigned long long seed; uint32_t site;  // dropout2d
+};
+
+__device__ __forceinline__ float bn_relu(const BnAct& a, float z, int c) {
+  float v = (z - a.mean[c]) * a.invstd[c] * a.gamma[c] + a.beta[c];
+  return v > 0.f ? v : 0.f;
+}
+__device__ __forceinline__ float drop2d(const BnAct& a, int n, int c) {
+  if (!a.thr) return 1.f;
+  return rng_keep(a.seed, a.site, (uint64_t)n * a.C + c, a.thr) ? a.dscale : 0.f;
+}
+
+// y[n, oy, ox, c] = max over window of drop2d(relu(bn(z)))
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnAct a, void* y, int y_dt) {
+  int Ho = a.H / a.pool, Wo = a.W / a.pool;
+  long total = (long)a.N * Ho * Wo * a.C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = i % a.C;
+    long p = i / a.C;
+    int ox = p % Wo;
+    long t = p / Wo;
+    int oy = t % Ho;
+    int n = t / Ho;
+    float best = -INFINITY;
+    for (int dy = 0; dy < a.pool; ++dy)
+      for (int dx = 0; dx < a.pool; ++dx) {
+        long zi = (((long)n * a.H + oy * a.pool + dy) * a.W + ox * a.pool + dx) * a.C + c;
+        float v = bn_relu(a, ld_dt(a.z, zi, a.dt), c);
+        best = fmaxf(best, v);
+      }
+    st_dt(y, i, best * drop2d(a, n, c), y_dt);
+  }
+}
+
+// gradient wrt the pre-BN activation's BN output (g) at full-res element i,
+// and xhat; dy is the gradient of the pooled block output.
+__device__ __forceinline__ void bn_act_grad(const BnAct& a, const void* dy, int dy_dt, long i, float& g,
+                                            float& xhat) {
+  int c = i % a.C;
+  long p = i / a.C;
+  int x = p % a.W;
+  long t = p / a.W;
+  int y = t % a.H;
+  int n = t / a.H;
+  float z = ld_dt(a.z, i, a.dt);
+  xhat = (z - a.mean[c]) * a.invstd[c];
+  g = 0.f;
+  float me = bn_relu(a, z, c);
+  if (me <= 0.f) return;  // relu'(0) = 0
+  int Ho = a.H / a.pool, Wo = a.W / a.pool;
+  int oy = y / a.pool, ox = x / a.pool;
+  if (oy >= Ho || ox >= Wo) return;
+  if (a.pool > 1) {
+    // first maximum in window scan order wins (torch max_pool2d)
+    for (int dy2 = 0; dy2 < a.pool; ++dy2)
+      for (int dx2 = 0; dx2 < a.pool; ++dx2) {
+        int yy = oy * a.pool + dy2, xx = ox * a.pool + dx2;
+        if (yy == y && xx == x) goto mine;
+        long zi = (((long)n * a.H + yy) * a.W + xx) * a.C + c;
+        if (bn_relu(a, ld_dt(a.z, zi, a.dt), c) >= me) return;
+      }
+  }
+mine:
+  g = ld_dt(dy, (((long)n * Ho + oy) * Wo + ox) * a.C + c, dy_dt) * drop2d(a, n, c);
+}
+
+// sums[0][c] = sum g ; sums[1][c] = sum g*xhat   (atomic, caller zeroes)
+__global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnAct a, const void* dy, int dy_dt,
+                                                               float* __restrict__ sums) {
+  __shared__ float s1[256], s2[256];
+  long total = (long)a.N * a.H * a.W * a.C;
+  // each thread keeps a fixed channel: stride is a multiple of C
+  int per = 256 / a.C;  // pixels per block-iteration (C <= 256, power of two)
+  int c = threadIdx.x % a.C;
+  int pofs = threadIdx.x / a.C;
+  float acc1 = 0.f, acc2 = 0.f;
+  if (pofs < per) {
+    long npix = total / a.C;
+    for (long p = (long)blockIdx.x * per + pofs; p < npix; p += (long)gridDim.x * per) {
+      float g, xh;
+      bn_act_grad(a, dy, dy_dt, p * a.C + c, g, xh);
+      acc1 += g;
+      acc2 += g * xh;
+    }
+  }
+  s1[threadIdx.x] = acc1;
+  s2[threadIdx.x] = acc2;
+  __syncthreads();
+  if (threadIdx.x < a.C) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int k = threadIdx.x; k < per * a.C; k += a.C) { t1 += s1[k]; t2 += s2[k]; }
+    atomicAdd(sums + threadIdx.x, t1);
+    atomicAdd(sums + a.C + threadIdx.x, t2);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnAct a, const void* dy, int dy_dt,
+                                                              const float* __restrict__ sums, int training,
+                                                              void* dz, int dz_dt) {
+  long total = (long)a.N * a.H * a.W * a.C;
+  float invM = 1.f / (float)(total / a.C);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = i % a.C;
+    float g, xh;
+    bn_act_grad(a, dy, dy_dt, i, g, xh);
+    float k = a.gamma[c] * a.invstd[c];
+    float v = training ? k * (g - sums[c] * invM - xh * sums[a.C + c] * invM) : k * g;
+    st_dt(dz, i, v, dz_dt);
+  }
+}
+
+static int grid_for(long n) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace hvit
+
+using namespace hvit;
+
+extern "C" int hvit_layernorm_fwd(const float* x, const float* gamma, const float* beta, int M, int D,
+                                  float eps, void* y, int y_dt, float* mean, float* rstd, void* stream) {
+  HVIT_CHECK(x && gamma && beta && y && mean && rstd, "hvit_layernorm_fwd: null pointer");
+  HVIT_CHECK(D % 4 == 0 && D <= 1024 && D > 0, "hvit_layernorm_fwd: D=%d must be a multiple of 4, <= 1024", D);
+  HVIT_CHECK(aligned16(x), "hvit_layernorm_fwd: x must be 16-byte aligned");
+  if (M <= 0) return HVIT_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(cdiv(M, 4));
+#define LNF(TY, V) hipLaunchKernelGGL((ln_fwd_kernel<TY, V>), g, dim3(256), 0, st, x, gamma, beta, (TY*)y, mean, rstd, M, D, eps)
+  if (y_dt == HVIT_F32) { if (D <= 256) LNF(float, 1); else if (D <= 512) LNF(float, 2); else LNF(float, 4); }
+  else { if (D <= 256) LNF(bf16_t, 1); else if (D <= 512) LNF(bf16_t, 2); else LNF(bf16_t, 4); }
+#undef LNF
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean,
+                                  const float* rstd, const float* gamma, int M, int D, const float* resid,
+                                  float* dx, float* dgamma, float* dbeta, void* stream) {
+  HVIT_CHECK(dy && x && mean && rstd && gamma && dx && dgamma && dbeta, "hvit_layernorm_bwd: null pointer");
+  HVIT_CHECK(D % 4 == 0 && D <= 1024 && D > 0, "hvit_layernorm_bwd: bad D=%d", D);
+  HVIT_CHECK(aligned16(x) && aligned16(dx) && (!resid || aligned16(resid)), "hvit_layernorm_bwd: alignment");
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(dgamma, 0, sizeof(float) * D, st);
+  (void)hipMemsetAsync(dbeta, 0, sizeof(float) * D, st);
+  if (M <= 0) return HVIT_OK;
+  dim3 g(cdiv(M, LNB_ROWS));
+#define LNB(TD, V) hipLaunchKernelGGL((ln_bwd_kernel<TD, V>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma, resid, dx, dgamma, dbeta, M, D)
+  if (dy_dt == HVIT_F32) { if (D <= 256) LNB(float, 1); else if (D <= 512) LNB(float, 2); else LNB(float, 4); }
+  else { if (D <= 256) LNB(bf16_t, 1); else if (D <= 512) LNB(bf16_t, 2); else LNB(bf16_t, 4); }
+#undef LNB
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C,
+                                float* mean, float* invstd, float* running_mean, float* running_var,
+                                long long* num_batches_tracked, float momentum, float eps, void* stream) {
+  HVIT_CHECK(partials && mean && invstd, "hvit_bn_finalize: null pointer");
+  HVIT_CHECK(M > 0 && C > 0 && ntiles > 0, "hvit_bn_finalize: bad sizes");
+  HVIT_CHECK((running_mean == nullptr) == (running_var == nullptr), "hvit_bn_finalize: running stats pair");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partials, ntiles,
+                     tile_rows, (long)M, C, mean, invstd, running_mean, running_var, momentum, eps,
+                     num_batches_tracked);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_bn_eval_prep(const float* running_mean, const float* running_var, int C, float eps,
+                                 float* mean, float* invstd, void* stream) {
+  HVIT_CHECK(running_mean && running_var && mean && invstd, "hvit_bn_eval_prep: null pointer");
+  hipLaunchKernelGGL(bn_eval_prep_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+                     running_mean, running_var, C, eps, mean, invstd);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+static int make_bnact(BnAct& a, int dt, const void* z, int N, int H, int W, int C, int pool,
+                      const float* mean, const float* invstd, const float* gamma, const float* beta,
+                      const hvit_dropout_t* dr) {
+  HVIT_CHECK(z && mean && invstd && gamma && beta, "bn_act: null pointer");
+  HVIT_CHECK(pool == 1 || pool == 2, "bn_act: pool must be 1 or 2");
+  HVIT_CHECK(C > 0 && C <= 256 && (C & (C - 1)) == 0, "bn_act: C=%d must be a power of two <= 256", C);
+  a.z = z; a.dt = dt; a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
+  a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.beta = beta;
+  a.thr = dr ? drop_threshold(dr->p) : 0;
+  a.dscale = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
+  a.seed = dr ? dr->seed : 0;
+  a.site = dr ? dr->site : 0;
+  return HVIT_OK;
+}
+
+extern "C" int hvit_bn_act_fwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               const hvit_dropout_t* dropout2d, int pool, void* y, int y_dt, void* stream) {
+  BnAct a;
+  int rc = make_bnact(a, dt, z, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d);
+  if (rc) return rc;
+  HVIT_CHECK(y, "hvit_bn_act_fwd: null y");
+  long total = (long)N * (H / pool) * (W / pool) * C;
+  if (total <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a, y, y_dt);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               const hvit_dropout_t* dropout2d, int pool, const void* dy, int dy_dt,
+                               int training, void* dz, int dz_dt, float* sums, void* stream) {
+  BnAct a;
+  int rc = make_bnact(a, dt, z, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d);
+  if (rc) return rc;
+  HVIT_CHECK(dy && dz && sums, "hvit_bn_act_bwd: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st);
+  long total = (long)N * H * W * C;
+  if (total <= 0) return HVIT_OK;
+  long npix = total / C;
+  int per = 256 / C;
+  hipLaunchKernelGGL(bn_act_bwd_reduce_kernel, dim3(grid_for(npix * 256 / per / 16 + 1)), dim3(256), 0, st, a,
+                     dy, dy_dt, sums);
+  HVIT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, a, dy, dy_dt,
+                     (const float*)sums, training, dz, dz_dt);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}

@@ -1,0 +1,171 @@
+// Spatial resampling on NHWC activations for gfx950:
+//  * bilinear resize, align_corners=False (F.interpolate as used by the skip
+//    connections, models/hybrid_vit.py:381-386, and the final resize, :459-465)
+//    with torch's source-index rule (area_pixel_compute_source_index: src =
+//    scale*(dst+0.5)-0.5 clamped at 0, scale = in/out in f32);
+//  * its backward as a GATHER (each input pixel sums the output pixels that
+//    sample it) -- deterministic, no atomics;
+//  * the backward of nearest x2 upsample fused with the split of the
+//    concatenated decoder input (components.py:146 + hybrid_vit.py:389).
+#include "common.h"
+
+namespace hvit {
+
+struct LinIdx {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ LinIdx lin_idx(int o, int in, float scale) {
+  float src = scale * ((float)o + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  int i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  int p = i0 < in - 1 ? 1 : 0;
+  LinIdx r;
+  r.i0 = i0;
+  r.i1 = i0 + p;
+  r.l1 = src - (float)i0;
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+__global__ __launch_bounds__(256) void bilinear_fwd_kernel(const void* x, int x_dt, void* y, int y_dt, int N,
+                                                          int Hi, int Wi, int C, int Ho, int Wo, float sh,
+                                                          float sw) {
+  long total = (long)N * Ho * Wo * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = i % C;
+    long p = i / C;
+    int ox = p % Wo;
+    long t = p / Wo;
+    int oy = t % Ho;
+    int n = t / Ho;
+    LinIdx ly = lin_idx(oy, Hi, sh), lx = lin_idx(ox, Wi, sw);
+    long b = (long)n * Hi;
+    float v00 = ld_dt(x, ((b + ly.i0) * Wi + lx.i0) * C + c, x_dt);
+    float v01 = ld_dt(x, ((b + ly.i0) * Wi + lx.i1) * C + c, x_dt);
+    float v10 = ld_dt(x, ((b + ly.i1) * Wi + lx.i0) * C + c, x_dt);
+    float v11 = ld_dt(x, ((b + ly.i1) * Wi + lx.i1) * C + c, x_dt);
+    float v = ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11);
+    st_dt(y, i, v, y_dt);
+  }
+}
+
+// weight with which output index o samples input index i along one dim
+__device__ __forceinline__ float lin_w(int o, int i, int in, float scale) {
+  LinIdx l = lin_idx(o, in, scale);
+  float w = 0.f;
+  if (l.i0 == i) w += l.l0;
+  if (l.i1 == i) w += l.l1;
+  return w;
+}
+__device__ __forceinline__ void out_range(int i, int in, int out, float scale, int& lo, int& hi) {
+  // outputs whose source lies in [i-1, i+1]
+  float inv = 1.f / scale;
+  lo = (int)floorf(((float)i - 1.f + 0.5f) * inv - 0.5f) - 1;
+  hi = (int)ceilf(((float)i + 1.f + 0.5f) * inv - 0.5f) + 1;
+  if (lo < 0) lo = 0;
+  if (hi > out - 1) hi = out - 1;
+}
+
+__global__ __launch_bounds__(256) void bilinear_bwd_kernel(const void* dy, int dy_dt, void* dx, int dx_dt, int N,
+                                                          int Hi, int Wi, int C, int Ho, int Wo, float sh,
+                                                          float sw, int accumulate) {
+  long total = (long)N * Hi * Wi * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = i % C;
+    long p = i / C;
+    int ix = p % Wi;
+    long t = p / Wi;
+    int iy = t % Hi;
+    int n = t / Hi;
+    int ylo, yhi, xlo, xhi;
+    out_range(iy, Hi, Ho, sh, ylo, yhi);
+    out_range(ix, Wi, Wo, sw, xlo, xhi);
+    float acc = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      float wy = lin_w(oy, iy, Hi, sh);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        float wx = lin_w(ox, ix, Wi, sw);
+        if (wx == 0.f) continue;
+        row += wx * ld_dt(dy, (((long)n * Ho + oy) * Wo + ox) * C + c, dy_dt);
+      }
+      acc += wy * row;
+    }
+    if (accumulate) acc += ld_dt(dx, i, dx_dt);
+    st_dt(dx, i, acc, dx_dt);
+  }
+}
+
+// dU [N, H*U, W*U, C1+C2] -> dx1 [N, H, W, C1], dx2 [N, H, W, C2] (sum over U x U)
+__global__ __launch_bounds__(256) void up_split_bwd_kernel(const void* du, int du_dt, int N, int H, int W, int U,
+                                                          int C1, int C2, void* dx1, int dx1_dt, void* dx2,
+                                                          int dx2_dt) {
+  int Ct = C1 + C2;
+  long total = (long)N * H * W * Ct;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = i % Ct;
+    long p = i / Ct;
+    int x = p % W;
+    long t = p / W;
+    int y = t % H;
+    int n = t / H;
+    float s = 0.f;
+    for (int a = 0; a < U; ++a)
+      for (int b = 0; b < U; ++b)
+        s += ld_dt(du, (((long)n * H * U + y * U + a) * (W * U) + x * U + b) * Ct + c, du_dt);
+    if (c < C1) st_dt(dx1, p * C1 + c, s, dx1_dt);
+    else st_dt(dx2, p * C2 + (c - C1), s, dx2_dt);
+  }
+}
+
+static int grid_for(long n) {
+  long g = (n + 255) / 256;
+  if (g > 16384) g = 16384;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace hvit
+
+using namespace hvit;
+
+extern "C" int hvit_bilinear_fwd(const void* x, int x_dt, int N, int Hi, int Wi, int C, int Ho, int Wo,
+                                 void* y, int y_dt, void* stream) {
+  HVIT_CHECK(x && y, "hvit_bilinear_fwd: null pointer");
+  HVIT_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0, "hvit_bilinear_fwd: bad sizes");
+  long total = (long)N * Ho * Wo * C;
+  if (total <= 0) return HVIT_OK;
+  float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
+  hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, x_dt,
+                     y, y_dt, N, Hi, Wi, C, Ho, Wo, sh, sw);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int Wo, int C, int Hi, int Wi,
+                                 void* dx, int dx_dt, int accumulate, void* stream) {
+  HVIT_CHECK(dy && dx, "hvit_bilinear_bwd: null pointer");
+  HVIT_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0, "hvit_bilinear_bwd: bad sizes");
+  long total = (long)N * Hi * Wi * C;
+  if (total <= 0) return HVIT_OK;
+  float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
+  hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dy, dy_dt,
+                     dx, dx_dt, N, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_upsample_split_bwd(const void* du, int du_dt, int N, int H, int W, int U, int C1, int C2,
+                                       void* dx1, int dx1_dt, void* dx2, int dx2_dt, void* stream) {
+  HVIT_CHECK(du && dx1 && (C2 == 0 || dx2), "hvit_upsample_split_bwd: null pointer");
+  HVIT_CHECK(U >= 1 && C1 > 0 && C2 >= 0, "hvit_upsample_split_bwd: bad sizes");
+  long total = (long)N * H * W * (C1 + C2);
+  if (total <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(up_split_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, du, du_dt,
+                     N, H, W, U, C1, C2, dx1, dx1_dt, dx2, dx2_dt);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}

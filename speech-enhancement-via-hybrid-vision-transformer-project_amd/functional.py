@@ -1,0 +1,515 @@
+"""Autograd functions that run the HybridViT hot path on libhvit.so.
+
+Each Function covers one reference module (cited) and chains C-ABI calls;
+PyTorch autograd only sequences them and sums gradients where a tensor has two
+consumers (the U-Net skips).  Activations are NHWC in the compute dtype
+``dt`` (f32 parity path or bf16 throughput path); the ViT residual stream,
+LayerNorm statistics, BatchNorm statistics and all parameter gradients are f32.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr
+
+F32, BF16 = L.F32, L.BF16
+
+
+def _empty(shape, dt, dev):
+    return torch.empty(shape, dtype=L.torch_dtype(dt), device=dev)
+
+
+def cast(t: torch.Tensor, dt: int) -> torch.Tensor:
+    """Contiguous copy of ``t`` in dtype ``dt`` (no copy if already there)."""
+    t = t.contiguous()
+    if L.dt_of(t) == dt:
+        return t
+    out = _empty(t.shape, dt, t.device)
+    call("hvit_cast", t.data_ptr(), L.dt_of(t), out.data_ptr(), dt, t.numel(), stream_ptr())
+    return out
+
+
+def pack_conv(w: torch.Tensor, mode: int, dt: int) -> torch.Tensor:
+    w = w.detach().contiguous()
+    if w.dtype != torch.float32:
+        raise TypeError("hvit: conv weights must be float32 parameters")
+    co, ci, ks, _ = w.shape
+    out = _empty((w.numel(),), dt, w.device)
+    call("hvit_conv_weight_pack", w.data_ptr(), co, ci, ks, mode, out.data_ptr(), dt, stream_ptr())
+    return out
+
+
+def unpack_conv(dwp: torch.Tensor, shape) -> torch.Tensor:
+    co, ci, ks, _ = shape
+    dw = torch.empty(shape, dtype=torch.float32, device=dwp.device)
+    call("hvit_conv_weight_unpack", dwp.data_ptr(), co, ci, ks, dw.data_ptr(), stream_ptr())
+    return dw
+
+
+def col_sum(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    out = torch.empty(cols, dtype=torch.float32, device=x.device)
+    call("hvit_reduce_rows", x.data_ptr(), L.dt_of(x), rows, cols, cols, 0, out.data_ptr(), stream_ptr())
+    return out
+
+
+def linear_wgrad(dt, dy, x, M, N, K) -> torch.Tensor:
+    dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
+    call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), ws_n,
+         stream_ptr())
+    return dw
+
+
+def epilogue(act=L.ACT_NONE, out2=None, aux=None, drop=None, resid=None, rowscale=None, rps=1, rowadd=None,
+             rowadd_rows=1, colsum=None):
+    e = L.Epilogue()
+    e.act = act
+    e.out2 = ptr(out2)
+    e.out2_dt = L.dt_of(out2) if out2 is not None else 0
+    e.aux = ptr(aux)
+    e.aux_dt = L.dt_of(aux) if aux is not None else 0
+    e.dropout = drop if drop is not None else L.dropout()
+    e.resid = ptr(resid)
+    e.rowscale = ptr(rowscale)
+    e.rows_per_sample = rps
+    e.rowadd = ptr(rowadd)
+    e.rowadd_rows = rowadd_rows
+    e.colsum = ptr(colsum)
+    return e
+
+
+def geom(src1, C1, src2, C2, N, Hs, Ws, U, KS, stride, pad, Cout) -> L.ConvGeom:
+    return L.ConvGeom(ptr(src1), C1, ptr(src2), C2, N, Hs, Ws, U, KS, stride, pad, Cout)
+
+
+def conv_wgrad(dt, g: L.ConvGeom, dz, wshape) -> torch.Tensor:
+    co, ci, ks, _ = wshape
+    dwp = torch.empty(co * ci * ks * ks, dtype=torch.float32, device=dz.device)
+    ws_n = L.lib().hvit_conv_wgrad_workspace(g)
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dz.device)
+    call("hvit_conv_wgrad", dt, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, stream_ptr())
+    return unpack_conv(dwp, wshape)
+
+
+@dataclass
+class Drop:
+    """A dropout site: probability, per-forward seed and site id."""
+    p: float = 0.0
+    seed: int = 0
+    site: int = 0
+
+    def c(self):
+        return L.dropout(self.p, self.seed, self.site)
+
+
+# ----------------------------------------------------------------------------
+class CastFn(torch.autograd.Function):
+    """Input cast to the compute dtype (gradient cast back)."""
+
+    @staticmethod
+    def forward(ctx, x, dt):
+        ctx.src_dt = L.dt_of(x)
+        return cast(x, dt)
+
+    @staticmethod
+    def backward(ctx, g):
+        return cast(g, ctx.src_dt), None
+
+
+class ConvBNActFn(torch.autograd.Function):
+    """[nearest up U] -> Conv KSxKS (no bias) over concat(x1, x2) -> BatchNorm2d
+    -> ReLU -> Dropout2d -> [MaxPool 2]  (ConvBlock components.py:15-99,
+    TransposeConvBlock components.py:102-192 with the decoder concat of
+    hybrid_vit.py:389).  NHWC in / out."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, w, gamma, beta, rmean, rvar, nbt, U, pool, training, drop: Drop, momentum, eps, dt):
+        N, Hs, Ws, C1 = x1.shape
+        C2 = x2.shape[3] if x2 is not None else 0
+        Cout, Cin, KS, _ = w.shape
+        assert Cin == C1 + C2, (Cin, C1, C2)
+        H, W = Hs * U, Ws * U
+        dev = x1.device
+        s = stream_ptr()
+        wp = pack_conv(w, 0, dt)
+        z = _empty((N, H, W, Cout), dt, dev)
+        g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
+        mean = torch.empty(Cout, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        if training:
+            P = N * H * W
+            nt = (P + 127) // 128
+            part = torch.empty((nt, Cout, 2), dtype=torch.float32, device=dev)
+            call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, part.data_ptr(), None, s)
+            call("hvit_bn_finalize", part.data_ptr(), nt, 128, P, Cout, mean.data_ptr(), invstd.data_ptr(),
+                 ptr(rmean), ptr(rvar), ptr(nbt), momentum, eps, s)
+        else:
+            call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, None, None, s)
+            call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
+                 invstd.data_ptr(), s)
+        y = _empty((N, H // pool, W // pool, Cout), dt, dev)
+        dr = drop.c() if training else L.dropout()
+        call("hvit_bn_act_fwd", dt, z.data_ptr(), N, H, W, Cout, mean.data_ptr(), invstd.data_ptr(),
+             gamma.data_ptr(), beta.data_ptr(), dr, pool, y.data_ptr(), dt, s)
+        ctx.save_for_backward(x1, x2, w, gamma, beta)
+        ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
+        ctx.meta = (U, pool, training, dr, dt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x1, x2, w, gamma, beta = ctx.saved_tensors
+        U, pool, training, dr, dt = ctx.meta
+        z = ctx.z
+        N, H, W, Cout = z.shape
+        Hs, Ws, C1 = x1.shape[1], x1.shape[2], x1.shape[3]
+        C2 = x2.shape[3] if x2 is not None else 0
+        KS = w.shape[2]
+        dev = z.device
+        s = stream_ptr()
+        dy = dy.contiguous()
+        dz = _empty(z.shape, dt, dev)
+        sums = torch.empty(2 * Cout, dtype=torch.float32, device=dev)
+        call("hvit_bn_act_bwd", dt, z.data_ptr(), N, H, W, Cout, ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
+             gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
+             dz.data_ptr(), dt, sums.data_ptr(), s)
+        dbeta, dgamma = sums[:Cout].clone(), sums[Cout:].clone()
+        g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
+        dw = conv_wgrad(dt, g, dz, w.shape)
+        dx1 = dx2 = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            wd = pack_conv(w, 1, dt)
+            du = _empty((N, H, W, C1 + C2), dt, dev)
+            call("hvit_conv_dgrad", dt, g, dz.data_ptr(), wd.data_ptr(), du.data_ptr(), dt, s)
+            if U == 1 and C2 == 0:
+                dx1 = du
+            else:
+                dx1 = _empty((N, Hs, Ws, C1), dt, dev)
+                dx2 = _empty((N, Hs, Ws, C2), dt, dev) if C2 else None
+                call("hvit_upsample_split_bwd", du.data_ptr(), dt, N, Hs, Ws, U, C1, C2, dx1.data_ptr(), dt,
+                     ptr(dx2), dt, s)
+        return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 10
+
+
+class PatchEmbedFn(torch.autograd.Function):
+    """PatchEmbedding conv k=s=P + flatten/transpose (components.py:282-307),
+    + pos_embed[:, :N] and dropout (PositionalEncoding components.py:371-386).
+    NHWC feature map -> f32 tokens [B, N, D]."""
+
+    @staticmethod
+    def forward(ctx, feat, w, b, pos, Pp, drop: Drop, training, dt):
+        N, H, W, C = feat.shape
+        D = w.shape[0]
+        Hp, Wp = H // Pp, W // Pp
+        Nt = Hp * Wp
+        if Nt > pos.shape[1]:
+            raise ValueError(f"hvit: {Nt} patches exceed the positional table ({pos.shape[1]})")
+        dev = feat.device
+        s = stream_ptr()
+        wp = pack_conv(w, 0, dt)
+        x0 = torch.empty((N, Nt, D), dtype=torch.float32, device=dev)
+        g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
+        dr = drop.c() if training else L.dropout()
+        e = epilogue(drop=dr, rowadd=pos, rowadd_rows=Nt)
+        call("hvit_conv_fwd", dt, g, wp.data_ptr(), b.data_ptr(), x0.data_ptr(), F32, None, e, s)
+        ctx.save_for_backward(feat, w)
+        ctx.wp = wp
+        ctx.meta = (Pp, dr, dt, Nt, pos.shape)
+        return x0
+
+    @staticmethod
+    def backward(ctx, dx0):
+        feat, w = ctx.saved_tensors
+        Pp, dr, dt, Nt, pshape = ctx.meta
+        N, H, W, C = feat.shape
+        D = w.shape[0]
+        dev = feat.device
+        s = stream_ptr()
+        dx0 = dx0.contiguous()
+        M = N * Nt
+        gd = _empty((M, D), dt, dev)
+        call("hvit_dropout_scale", dx0.data_ptr(), L.dt_of(dx0), M, D, dr, None, 1, gd.data_ptr(), dt, s)
+        db = col_sum(gd, M, D)
+        dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
+        call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
+        g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
+        dw = conv_wgrad(dt, g, gd, w.shape)
+        dfeat = None
+        if ctx.needs_input_grad[0]:
+            dfeat = _empty(feat.shape, dt, dev)
+            call("hvit_conv_dgrad", dt, g, gd.data_ptr(), ctx.wp.data_ptr(), dfeat.data_ptr(), dt, s)
+        return dfeat, dw, db, dpos, None, None, None, None
+
+
+def _ln(x2d, gw, gb, dt):
+    M, D = x2d.shape
+    y = _empty((M, D), dt, x2d.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x2d.device)
+    rstd = torch.empty_like(mean)
+    call("hvit_layernorm_fwd", x2d.data_ptr(), gw.data_ptr(), gb.data_ptr(), M, D, 1e-5, y.data_ptr(), dt,
+         mean.data_ptr(), rstd.data_ptr(), stream_ptr())
+    return y, mean, rstd
+
+
+def _ln_bwd(dy, x, mean, rstd, gw, resid):
+    M, D = x.shape
+    dx = torch.empty((M, D), dtype=torch.float32, device=x.device)
+    dgw = torch.empty(D, dtype=torch.float32, device=x.device)
+    dgb = torch.empty_like(dgw)
+    call("hvit_layernorm_bwd", dy.data_ptr(), L.dt_of(dy), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+         gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), stream_ptr())
+    return dx, dgw, dgb
+
+
+def droppath_scale(B, p, seed, site, dev):
+    if p <= 0:
+        return None
+    out = torch.empty(B, dtype=torch.float32, device=dev)
+    call("hvit_droppath_scale", B, L.dropout(p, seed, site), out.data_ptr(), stream_ptr())
+    return out
+
+
+class ViTBlockFn(torch.autograd.Function):
+    """Pre-norm TransformerEncoderBlock (attention.py:176-213):
+    x1 = x + DropPath(Dropout(proj(MHSA(LN1 x))));  x2 = x1 + DropPath(FFN(LN2 x1))
+    with MHSA attention.py:65-115 and FeedForward components.py:223-241.
+    f32 residual stream [B, N, D] in and out."""
+
+    @staticmethod
+    def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, H, drops, dpr, training,
+                dt, want_probs):
+        B, Nt, D = x.shape
+        M = B * Nt
+        hd = D // H
+        hid = f1w.shape[0]
+        dev = x.device
+        s = stream_ptr()
+        scale = hd ** -0.5
+        x2d = x.contiguous().view(M, D)
+        d_attn, d_proj, d_fc1, d_fc2, dp_seed = drops if training else (Drop(),) * 4 + (0,)
+        rs1 = droppath_scale(B, dpr if training else 0.0, dp_seed, 1, dev)
+        rs2 = droppath_scale(B, dpr if training else 0.0, dp_seed, 2, dev)
+        xn1, m1, r1 = _ln(x2d, n1w, n1b, dt)
+        Wqkv = cast(qkvw, dt)
+        qkv = _empty((M, 3 * D), dt, dev)
+        call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
+             qkv.data_ptr(), dt, None, s)
+        o = _empty((M, D), dt, dev)
+        lse = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
+        probs = torch.empty((B, H, Nt, Nt), dtype=torch.float32, device=dev) if want_probs else None
+        call("hvit_mhsa_fwd", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(), lse.data_ptr(),
+             ptr(probs), s)
+        Wp = cast(pw, dt)
+        x1 = torch.empty((M, D), dtype=torch.float32, device=dev)
+        call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D, x1.data_ptr(), F32,
+             epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), s)
+        xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
+        W1 = cast(f1w, dt)
+        h = _empty((M, hid), dt, dev)
+        a = _empty((M, hid), dt, dev)
+        call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, h.data_ptr(), dt,
+             epilogue(act=L.ACT_GELU_DUAL, out2=a, drop=d_fc1.c()), s)
+        W2 = cast(f2w, dt)
+        x2 = torch.empty((M, D), dtype=torch.float32, device=dev)
+        call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid, x2.data_ptr(), F32,
+             epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
+        ctx.save_for_backward(n1w, n2w)
+        ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2)
+        ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
+        if want_probs:
+            ctx.mark_non_differentiable(probs)
+        return x2.view(B, Nt, D), probs
+
+    @staticmethod
+    def backward(ctx, dx2, _dprobs=None):
+        n1w, n2w = ctx.saved_tensors
+        (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2) = ctx.t
+        B, Nt, D, H, hid, scale, dt, dra, drp, drf1, drf2 = ctx.meta
+        M = B * Nt
+        dev = x1.device
+        s = stream_ptr()
+        dx2 = dx2.contiguous().view(M, D)
+        if dx2.dtype != torch.float32:
+            dx2 = dx2.float()
+        # MLP branch
+        g2 = _empty((M, D), dt, dev)
+        call("hvit_dropout_scale", dx2.data_ptr(), F32, M, D, drf2, ptr(rs2), Nt, g2.data_ptr(), dt, s)
+        df2b = col_sum(g2, M, D)
+        df2w = linear_wgrad(dt, g2, a, M, D, hid)
+        dh = _empty((M, hid), dt, dev)
+        call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
+             epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1), s)
+        df1b = col_sum(dh, M, hid)
+        df1w = linear_wgrad(dt, dh, xn2, M, hid, D)
+        dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
+        call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
+        dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2)
+        # attention branch
+        g1 = _empty((M, D), dt, dev)
+        call("hvit_dropout_scale", dx1.data_ptr(), F32, M, D, drp, ptr(rs1), Nt, g1.data_ptr(), dt, s)
+        dpb = col_sum(g1, M, D)
+        dpw = linear_wgrad(dt, g1, o, M, D, D)
+        do = _empty((M, D), dt, dev)
+        call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
+        dqkv = _empty((M, 3 * D), dt, dev)
+        delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
+        call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H, D // H,
+             scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
+        dqkvb = col_sum(dqkv, M, 3 * D)
+        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D)
+        dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
+        call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None, s)
+        dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1)
+        return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
+                None, None, None, None, None, None)
+
+
+class HeadFn(torch.autograd.Function):
+    """Final LayerNorm (attention.py:300) + to_feature_map Linear and the
+    [B,N,C] -> NCHW reshape (hybrid_vit.py:342-348), which in NHWC is the
+    identity: f32 tokens [B, N, D] -> NHWC feature map [B, Hp, Wp, C]."""
+
+    @staticmethod
+    def forward(ctx, x, nw, nb, w, b, hw, dt):
+        B, Nt, D = x.shape
+        M = B * Nt
+        C = w.shape[0]
+        x2d = x.contiguous().view(M, D)
+        xn, m, r = _ln(x2d, nw, nb, dt)
+        W = cast(w, dt)
+        y = _empty((B, hw[0], hw[1], C), dt, x.device)
+        call("hvit_linear_fwd", dt, xn.data_ptr(), W.data_ptr(), b.data_ptr(), M, C, D, y.data_ptr(), dt, None,
+             stream_ptr())
+        ctx.save_for_backward(nw)
+        ctx.t = (x2d, xn, m, r, W)
+        ctx.meta = (B, Nt, D, C, dt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (nw,) = ctx.saved_tensors
+        x2d, xn, m, r, W = ctx.t
+        B, Nt, D, C, dt = ctx.meta
+        M = B * Nt
+        dy = cast(dy, dt)
+        db = col_sum(dy, M, C)
+        dw = linear_wgrad(dt, dy, xn, M, C, D)
+        dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
+        call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32, None,
+             stream_ptr())
+        dx, dnw, dnb = _ln_bwd(dxn, x2d, m, r, nw, None)
+        return dx.view(B, Nt, D), dnw, dnb, dw, db, None, None
+
+
+class SkipFn(torch.autograd.Function):
+    """Skip projection 1x1 conv (bias) + bilinear resize to the decoder grid
+    (hybrid_vit.py:376-386).  Both are linear and the bilinear weights sum to
+    one, so resize-then-project equals the reference's project-then-resize and
+    the GEMM runs on the (up to 16x) smaller grid.  NHWC in / out."""
+
+    @staticmethod
+    def forward(ctx, e, w, b, Ho, Wo, dt):
+        N, He, We, Ce = e.shape
+        Cd = w.shape[0]
+        dev = e.device
+        s = stream_ptr()
+        if (He, We) != (Ho, Wo):
+            r = _empty((N, Ho, Wo, Ce), dt, dev)
+            call("hvit_bilinear_fwd", e.data_ptr(), dt, N, He, We, Ce, Ho, Wo, r.data_ptr(), dt, s)
+        else:
+            r = e.contiguous()
+        W = cast(w.view(Cd, Ce), dt)
+        y = _empty((N, Ho, Wo, Cd), dt, dev)
+        M = N * Ho * Wo
+        call("hvit_linear_fwd", dt, r.data_ptr(), W.data_ptr(), b.data_ptr(), M, Cd, Ce, y.data_ptr(), dt, None, s)
+        ctx.t = (r, W)
+        ctx.meta = (N, He, We, Ce, Ho, Wo, Cd, dt, tuple(w.shape))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        r, W = ctx.t
+        N, He, We, Ce, Ho, Wo, Cd, dt, wshape = ctx.meta
+        M = N * Ho * Wo
+        dev = r.device
+        s = stream_ptr()
+        dy = cast(dy, dt)
+        db = col_sum(dy, M, Cd)
+        dw = linear_wgrad(dt, dy, r, M, Cd, Ce).view(wshape)
+        de = None
+        if ctx.needs_input_grad[0]:
+            dr = _empty((N, Ho, Wo, Ce), dt, dev)
+            call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, Cd, Ce, dr.data_ptr(), dt, None, s)
+            if (He, We) != (Ho, Wo):
+                de = _empty((N, He, We, Ce), dt, dev)
+                call("hvit_bilinear_bwd", dr.data_ptr(), dt, N, Ho, Wo, Ce, He, We, de.data_ptr(), dt, 0, s)
+            else:
+                de = dr
+        return de, dw, db, None, None, None
+
+
+class FinalFn(torch.autograd.Function):
+    """Final TransposeConvBlock ([up U] -> Conv -> Tanh, components.py:146-167)
+    and the resize to the input size (hybrid_vit.py:459-465).  NHWC dt in,
+    f32 NHWC [B, F, T, Cout] out."""
+
+    @staticmethod
+    def forward(ctx, x, w, U, out_hw, dt):
+        N, Hs, Ws, C = x.shape
+        Cout, Cin, KS, _ = w.shape
+        H, W = Hs * U, Ws * U
+        dev = x.device
+        s = stream_ptr()
+        wp = pack_conv(w, 0, dt)
+        y = torch.empty((N, H, W, Cout), dtype=torch.float32, device=dev)
+        g = geom(x, C, None, 0, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
+        call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, y.data_ptr(), F32, None, epilogue(act=L.ACT_TANH), s)
+        F, T = out_hw
+        if (H, W) != (F, T):
+            out = torch.empty((N, F, T, Cout), dtype=torch.float32, device=dev)
+            call("hvit_bilinear_fwd", y.data_ptr(), F32, N, H, W, Cout, F, T, out.data_ptr(), F32, s)
+        else:
+            out = y.clone()
+        ctx.save_for_backward(x, w)
+        ctx.y = y
+        ctx.meta = (U, out_hw, dt)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w = ctx.saved_tensors
+        U, (F, T), dt = ctx.meta
+        y = ctx.y
+        N, H, W, Cout = y.shape
+        Hs, Ws, C = x.shape[1], x.shape[2], x.shape[3]
+        KS = w.shape[2]
+        dev = x.device
+        s = stream_ptr()
+        dout = dout.contiguous().float()
+        if (H, W) != (F, T):
+            dy = torch.empty((N, H, W, Cout), dtype=torch.float32, device=dev)
+            call("hvit_bilinear_bwd", dout.data_ptr(), F32, N, F, T, Cout, H, W, dy.data_ptr(), F32, 0, s)
+        else:
+            dy = dout
+        dz = _empty((N, H, W, Cout), dt, dev)
+        call("hvit_tanh_bwd", dy.data_ptr(), F32, y.data_ptr(), dy.numel(), dz.data_ptr(), dt, s)
+        g = geom(x, C, None, 0, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
+        dw = conv_wgrad(dt, g, dz, w.shape)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wd = pack_conv(w, 1, dt)
+            du = _empty((N, H, W, C), dt, dev)
+            call("hvit_conv_dgrad", dt, g, dz.data_ptr(), wd.data_ptr(), du.data_ptr(), dt, s)
+            if U == 1:
+                dx = du
+            else:
+                dx = _empty((N, Hs, Ws, C), dt, dev)
+                call("hvit_upsample_split_bwd", du.data_ptr(), dt, N, Hs, Ws, U, C, 0, dx.data_ptr(), dt, None, dt, s)
+        return dx, dw, None, None, None

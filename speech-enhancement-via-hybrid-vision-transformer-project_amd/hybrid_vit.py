@@ -1,0 +1,445 @@
+"""Drop-in ``HybridViT`` (reference: models/hybrid_vit.py, models/attention.py,
+models/components.py) whose forward/backward run on libhvit.so (gfx950).
+
+The constructor signature and defaults, the submodule tree, parameter names,
+the 122 ``state_dict`` keys and shapes, the weight initialisation,
+``forward(x, return_attentions=False)``, ``forward_encoder`` /
+``forward_transformer`` / ``forward_decoder``, ``count_parameters`` and
+``create_hybrid_vit(config)`` all follow the reference, so reference
+checkpoints load with ``strict=True`` and Trainer / AudioEnhancer callers work
+unchanged.  The torch submodules (Conv2d, BatchNorm2d, LayerNorm, Linear) are
+kept as parameter containers only: their ``forward`` is never called.
+
+Precision: ``precision="fp32"`` runs the exact-f32 MFMA path (parity with the
+reference within 1e-3 rel); ``"bf16"`` runs bf16 MFMA with f32 accumulation, f32
+residual stream / statistics / weight gradients; ``"auto"`` (default) picks bf16
+inside a CUDA autocast region (the reference's trainer.py:148 AMP context) and
+fp32 otherwise.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import functional as HF
+
+
+# ------------------------------------------------------------ containers ----
+class ConvBlock(nn.Module):
+    """components.py:15-99 (Conv no-bias, BN, ReLU, Dropout2d, MaxPool)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1, pool_size=2,
+                 activation="relu", use_batchnorm=True, dropout=0.0):
+        super().__init__()
+        if activation != "relu" or not use_batchnorm or stride != 1 or padding != kernel_size // 2:
+            raise NotImplementedError("hvit ConvBlock: relu + batchnorm same-conv only (the HybridViT use)")
+        if pool_size not in (None, 1, 2):
+            raise NotImplementedError("hvit ConvBlock: pool_size must be 1 or 2")
+        layers = [nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False),
+                  nn.BatchNorm2d(out_channels), nn.ReLU(inplace=True)]
+        if dropout > 0:
+            layers.append(nn.Dropout2d(dropout))
+        if pool_size is not None and pool_size > 1:
+            layers.append(nn.MaxPool2d(kernel_size=pool_size))
+        self.block = nn.Sequential(*layers)
+        self.pool = pool_size if (pool_size is not None and pool_size > 1) else 1
+        self.p = dropout
+
+    @property
+    def conv(self):
+        return self.block[0]
+
+    @property
+    def bn(self):
+        return self.block[1]
+
+
+class TransposeConvBlock(nn.Module):
+    """components.py:102-192 ([nearest Up], Conv no-bias, BN / Tanh, ReLU, Dropout2d)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1, output_padding=0,
+                 upsample_factor=2, activation="relu", use_batchnorm=True, dropout=0.0, final_layer=False):
+        super().__init__()
+        if activation != "relu" or not use_batchnorm or stride != 1 or padding != kernel_size // 2:
+            raise NotImplementedError("hvit TransposeConvBlock: relu + batchnorm same-conv only")
+        layers = []
+        self.up = upsample_factor if (upsample_factor is not None and upsample_factor > 1) else 1
+        if self.up > 1:
+            layers.append(nn.Upsample(scale_factor=upsample_factor, mode="nearest"))
+        layers.append(nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=False))
+        if not final_layer:
+            layers.append(nn.BatchNorm2d(out_channels))
+        layers.append(nn.Tanh() if final_layer else nn.ReLU(inplace=True))
+        if dropout > 0 and not final_layer:
+            layers.append(nn.Dropout2d(dropout))
+        self.block = nn.Sequential(*layers)
+        self.final = final_layer
+        self.p = dropout if not final_layer else 0.0
+
+    @property
+    def conv(self):
+        return self.block[1 if self.up > 1 else 0]
+
+    @property
+    def bn(self):
+        return self.block[2 if self.up > 1 else 1]
+
+
+class PatchEmbedding(nn.Module):
+    """components.py:244-307."""
+
+    def __init__(self, in_channels, embed_dim, patch_size=4, flatten=True):
+        super().__init__()
+        self.patch_size = patch_size
+        self.flatten = flatten
+        self.projection = nn.Conv2d(in_channels, embed_dim, kernel_size=patch_size, stride=patch_size)
+
+
+class PositionalEncoding(nn.Module):
+    """components.py:310-386 (learnable table, the HybridViT configuration)."""
+
+    def __init__(self, embed_dim, max_len=5000, learnable=True, dropout=0.1):
+        super().__init__()
+        if not learnable:
+            raise NotImplementedError("hvit: HybridViT uses the learnable positional table")
+        self.embed_dim = embed_dim
+        self.learnable = learnable
+        self.dropout = nn.Dropout(dropout)
+        self.pos_embed = nn.Parameter(torch.zeros(1, max_len, embed_dim))
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+
+
+class DropPath(nn.Module):
+    """components.py:389-427 (per-sample stochastic depth)."""
+
+    def __init__(self, drop_prob=0.0):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+
+class FeedForward(nn.Module):
+    """components.py:195-241."""
+
+    def __init__(self, dim, hidden_dim=None, dropout=0.0):
+        super().__init__()
+        hidden_dim = hidden_dim or 4 * dim
+        self.net = nn.Sequential(nn.Linear(dim, hidden_dim), nn.GELU(), nn.Dropout(dropout),
+                                 nn.Linear(hidden_dim, dim), nn.Dropout(dropout))
+
+
+class MultiHeadSelfAttention(nn.Module):
+    """attention.py:17-115."""
+
+    def __init__(self, embed_dim, num_heads=8, qkv_bias=True, attn_dropout=0.0, proj_dropout=0.0):
+        super().__init__()
+        assert embed_dim % num_heads == 0, \
+            f"embed_dim ({embed_dim}) must be divisible by num_heads ({num_heads})"
+        self.embed_dim = embed_dim
+        self.num_heads = num_heads
+        self.head_dim = embed_dim // num_heads
+        if self.head_dim not in (16, 32, 64):
+            raise NotImplementedError(f"hvit: head_dim {self.head_dim} unsupported (16, 32, 64)")
+        self.scale = self.head_dim ** -0.5
+        if not qkv_bias:
+            raise NotImplementedError("hvit: qkv_bias=False unsupported")
+        self.qkv = nn.Linear(embed_dim, embed_dim * 3, bias=qkv_bias)
+        self.proj = nn.Linear(embed_dim, embed_dim)
+        self.attn_dropout = nn.Dropout(attn_dropout)
+        self.proj_dropout = nn.Dropout(proj_dropout)
+
+
+class TransformerEncoderBlock(nn.Module):
+    """attention.py:118-213 (pre-norm)."""
+
+    def __init__(self, embed_dim, num_heads=8, mlp_ratio=4.0, qkv_bias=True, dropout=0.0, attn_dropout=0.0,
+                 drop_path=0.0):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(embed_dim)
+        self.norm2 = nn.LayerNorm(embed_dim)
+        self.attn = MultiHeadSelfAttention(embed_dim, num_heads, qkv_bias, attn_dropout, dropout)
+        self.mlp = FeedForward(embed_dim, int(embed_dim * mlp_ratio), dropout)
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
+        self.dpr = drop_path
+        self.p = dropout
+        self.p_attn = attn_dropout
+
+
+class VisionTransformer(nn.Module):
+    """attention.py:216-304."""
+
+    def __init__(self, embed_dim, num_layers=6, num_heads=8, mlp_ratio=4.0, qkv_bias=True, dropout=0.0,
+                 attn_dropout=0.0, drop_path_rate=0.0):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.num_layers = num_layers
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, num_layers)]
+        self.blocks = nn.ModuleList([
+            TransformerEncoderBlock(embed_dim, num_heads, mlp_ratio, qkv_bias, dropout, attn_dropout, dpr[i])
+            for i in range(num_layers)])
+        self.norm = nn.LayerNorm(embed_dim)
+
+
+# ------------------------------------------------------------------ model ---
+class HybridViT(nn.Module):
+    """HybridViT (models/hybrid_vit.py:21-489) on the gfx950 HIP path."""
+
+    def __init__(
+        self,
+        input_channels: int = 1,
+        output_channels: int = 1,
+        encoder_channels: List[int] = [64, 128, 256],
+        encoder_kernel_sizes: List[int] = [3, 3, 3],
+        encoder_pool_sizes: List[int] = [2, 2, 1],
+        embed_dim: int = 512,
+        num_heads: int = 8,
+        num_layers: int = 6,
+        mlp_ratio: float = 4.0,
+        patch_size: int = 4,
+        decoder_channels: List[int] = [256, 128, 64, 1],
+        decoder_kernel_sizes: List[int] = [3, 3, 3, 3],
+        decoder_upsample_factors: List[int] = [1, 2, 2, 1],
+        dropout: float = 0.1,
+        attn_dropout: float = 0.1,
+        drop_path_rate: float = 0.1,
+        use_skip_connections: bool = True,
+        use_cls_token: bool = False,
+        precision: str = "auto",
+    ):
+        super().__init__()
+        if use_cls_token:
+            raise NotImplementedError("hvit: use_cls_token=True is not on the hot path (never set by "
+                                      "create_hybrid_vit)")
+        self.input_channels = input_channels
+        self.output_channels = output_channels
+        self.embed_dim = embed_dim
+        self.patch_size = patch_size
+        self.use_skip_connections = use_skip_connections
+        self.use_cls_token = use_cls_token
+        self.num_heads = num_heads
+        self.dropout_p = dropout
+        self.precision = precision
+
+        self.encoder = nn.ModuleList()
+        in_ch = input_channels
+        for out_ch, k, pool in zip(encoder_channels, encoder_kernel_sizes, encoder_pool_sizes):
+            self.encoder.append(ConvBlock(in_ch, out_ch, k, padding=k // 2, pool_size=pool if pool > 1 else None,
+                                          dropout=dropout))
+            in_ch = out_ch
+        enc_out = encoder_channels[-1]
+        self.patch_embed = PatchEmbedding(enc_out, embed_dim, patch_size, flatten=True)
+        self.cls_token = None
+        self.pos_encoding = PositionalEncoding(embed_dim, max_len=10000, learnable=True, dropout=dropout)
+        self.transformer = VisionTransformer(embed_dim, num_layers, num_heads, mlp_ratio, True, dropout,
+                                             attn_dropout, drop_path_rate)
+        self.to_feature_map = nn.Linear(embed_dim, enc_out)
+        self.decoder = nn.ModuleList()
+        nd = len(decoder_channels)
+        for i, (out_ch, k, up) in enumerate(zip(decoder_channels, decoder_kernel_sizes,
+                                                decoder_upsample_factors)):
+            in_c = decoder_channels[0] if i == 0 else decoder_channels[i - 1]
+            if use_skip_connections and i < nd - 1:
+                in_c = in_c + out_ch
+            final = i == nd - 1
+            self.decoder.append(TransposeConvBlock(in_c, out_ch, k, padding=k // 2,
+                                                   upsample_factor=up if up > 1 else None,
+                                                   dropout=dropout if not final else 0.0, final_layer=final))
+        if use_skip_connections:
+            self.skip_projections = nn.ModuleList([
+                nn.Conv2d(ec, dc, kernel_size=1) for ec, dc in zip(encoder_channels[::-1], decoder_channels[:-1])])
+        else:
+            self.skip_projections = None
+        self.apply(self._init_weights)
+
+    @staticmethod
+    def _init_weights(m):
+        """hybrid_vit.py:265-284."""
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, (nn.BatchNorm2d, nn.LayerNorm)):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+
+    # -------------------------------------------------------------- helpers --
+    def _dt(self) -> int:
+        p = self.precision
+        if p == "auto":
+            return L.BF16 if torch.is_autocast_enabled("cuda") else L.F32
+        if p in ("bf16", "bfloat16"):
+            return L.BF16
+        if p in ("fp32", "float32"):
+            return L.F32
+        raise ValueError(f"hvit: unknown precision {p!r}")
+
+    def _check_device(self, x):
+        if not x.is_cuda:
+            raise RuntimeError("hvit: the HIP path needs GPU tensors (call .to('cuda')); there is no CPU path")
+        lib = L.lib()  # noqa: F841  (fails loudly when libhvit.so is missing)
+
+    def _seed(self) -> int:
+        return int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
+
+    @staticmethod
+    def _nhwc(t: torch.Tensor) -> torch.Tensor:
+        """NCHW logical tensor (possibly a channels-last view) -> NHWC contiguous."""
+        return t.permute(0, 2, 3, 1).contiguous()
+
+    @staticmethod
+    def _nchw(t: torch.Tensor) -> torch.Tensor:
+        """NHWC storage -> NCHW logical view (channels-last strides, no copy)."""
+        return t.permute(0, 3, 1, 2)
+
+    # ---------------------------------------------------------- stage runners --
+    def _encoder(self, xh, dt, seed):
+        skips = []
+        h = xh
+        for i, blk in enumerate(self.encoder):
+            bn = blk.bn
+            h = HF.ConvBNActFn.apply(h, None, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     bn.num_batches_tracked, 1, blk.pool, self.training,
+                                     HF.Drop(blk.p, seed, 100 + i), bn.momentum, bn.eps, dt)
+            skips.append(h)
+        return h, skips
+
+    def _tokens(self, feat, dt, seed):
+        P = self.patch_size
+        pe = self.patch_embed.projection
+        t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, self.pos_encoding.pos_embed, P,
+                                  HF.Drop(self.dropout_p, seed, 200), self.training, dt)
+        return t, (feat.shape[1] // P, feat.shape[2] // P)
+
+    def _vit(self, t, dt, seed, want_attn=False):
+        attns = []
+        for l, blk in enumerate(self.transformer.blocks):
+            a, m = blk.attn, blk.mlp.net
+            base = 300 + 10 * l
+            drops = (HF.Drop(blk.p_attn, seed, base), HF.Drop(blk.p, seed, base + 1),
+                     HF.Drop(blk.p, seed, base + 2), HF.Drop(blk.p, seed, base + 3), seed ^ (base << 20))
+            t, probs = HF.ViTBlockFn.apply(t, blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias,
+                                           a.proj.weight, a.proj.bias, blk.norm2.weight, blk.norm2.bias,
+                                           m[0].weight, m[0].bias, m[3].weight, m[3].bias, a.num_heads, drops,
+                                           blk.dpr, self.training, dt, want_attn)
+            attns.append(probs)
+        return t, attns
+
+    def _head(self, t, hw, dt):
+        n = self.transformer.norm
+        return HF.HeadFn.apply(t, n.weight, n.bias, self.to_feature_map.weight, self.to_feature_map.bias, hw, dt)
+
+    def _decoder(self, x, skips, out_hw, dt, seed):
+        skips = skips[::-1]
+        nd = len(self.decoder)
+        for i, blk in enumerate(self.decoder):
+            if blk.final:
+                return HF.FinalFn.apply(x, blk.conv.weight, blk.up, out_hw, dt)
+            s = None
+            if self.use_skip_connections and i < nd - 1 and i < len(skips):
+                sp = self.skip_projections[i]
+                s = HF.SkipFn.apply(skips[i], sp.weight, sp.bias, x.shape[1], x.shape[2], dt)
+            bn = blk.bn
+            x = HF.ConvBNActFn.apply(x, s, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     bn.num_batches_tracked, blk.up, 1, self.training,
+                                     HF.Drop(blk.p, seed, 500 + i), bn.momentum, bn.eps, dt)
+        raise RuntimeError("hvit: decoder has no final layer")
+
+    # -------------------------------------------------------- reference API --
+    def forward_encoder(self, x: torch.Tensor) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+        """hybrid_vit.py:286-307.  Returns NCHW views (channels-last storage)."""
+        self._check_device(x)
+        dt = self._dt()
+        h, skips = self._encoder(HF.CastFn.apply(self._nhwc(x), dt), dt, self._seed())
+        return self._nchw(h), [self._nchw(s) for s in skips]
+
+    def forward_transformer(self, x: torch.Tensor, spatial_shape: Tuple[int, int]) -> torch.Tensor:
+        """hybrid_vit.py:309-350: patch tokens [B, N, D] (without pos-enc) -> [B, C, H, W]."""
+        self._check_device(x)
+        dt = self._dt()
+        seed = self._seed()
+        B, N, D = x.shape
+        pos = self.pos_encoding.pos_embed[:, :N, :]
+        t = x.float() + pos
+        if self.training and self.dropout_p > 0:
+            t = torch.nn.functional.dropout(t, self.dropout_p)
+        t, _ = self._vit(t.contiguous(), dt, seed)
+        return self._nchw(self._head(t, spatial_shape, dt))
+
+    def forward_decoder(self, x: torch.Tensor, skip_features: List[torch.Tensor]) -> torch.Tensor:
+        """hybrid_vit.py:352-394 (output before the final resize)."""
+        self._check_device(x)
+        dt = self._dt()
+        xh = HF.CastFn.apply(self._nhwc(x), dt)
+        skips = [HF.CastFn.apply(self._nhwc(s), dt) for s in skip_features]
+        U = self.decoder[-1].up
+        H = xh.shape[1]
+        W = xh.shape[2]
+        for blk in self.decoder[:-1]:
+            H, W = H * blk.up, W * blk.up
+        out = self._decoder(xh, skips, (H * U, W * U), dt, self._seed())
+        return self._nchw(out)
+
+    def forward(self, x: torch.Tensor, return_attentions: bool = False):
+        """hybrid_vit.py:396-469."""
+        self._check_device(x)
+        if x.dim() != 4:
+            raise ValueError(f"hvit: expected [B, C, F, T], got {tuple(x.shape)}")
+        dt = self._dt()
+        seed = self._seed()
+        F, T = x.shape[2], x.shape[3]
+        xh = HF.CastFn.apply(self._nhwc(x.float() if x.dtype != torch.float32 else x), dt)
+        feat, skips = self._encoder(xh, dt, seed)
+        t, hw = self._tokens(feat, dt, seed)
+        t, attns = self._vit(t, dt, seed, return_attentions)
+        f = self._head(t, hw, dt)
+        out = self._decoder(f, skips, (F, T), dt, seed)
+        out = self._nchw(out)
+        if return_attentions:
+            return out, attns
+        return out
+
+    def count_parameters(self) -> Dict[str, int]:
+        """hybrid_vit.py:471-489."""
+        return {
+            "encoder": sum(p.numel() for p in self.encoder.parameters()),
+            "transformer": sum(p.numel() for p in self.transformer.parameters()),
+            "decoder": sum(p.numel() for p in self.decoder.parameters()),
+            "total": sum(p.numel() for p in self.parameters()),
+            "trainable": sum(p.numel() for p in self.parameters() if p.requires_grad),
+        }
+
+
+def create_hybrid_vit(config: Optional[Dict] = None, **overrides) -> HybridViT:
+    """hybrid_vit.py:492-525 (same config keys and defaults)."""
+    config = config or {}
+    mc = config.get("model", {})
+    enc, tr, dec = mc.get("encoder", {}), mc.get("transformer", {}), mc.get("decoder", {})
+    kw = dict(
+        input_channels=mc.get("input_channels", 1),
+        output_channels=mc.get("output_channels", 1),
+        encoder_channels=enc.get("channels", [64, 128, 256]),
+        encoder_kernel_sizes=enc.get("kernel_sizes", [3, 3, 3]),
+        encoder_pool_sizes=enc.get("pool_sizes", [2, 2, 1]),
+        embed_dim=tr.get("embed_dim", 512),
+        num_heads=tr.get("num_heads", 8),
+        num_layers=tr.get("num_layers", 6),
+        mlp_ratio=tr.get("mlp_ratio", 4),
+        patch_size=tr.get("patch_size", 4),
+        decoder_channels=dec.get("channels", [256, 128, 64, 1]),
+        decoder_kernel_sizes=dec.get("kernel_sizes", [3, 3, 3, 3]),
+        decoder_upsample_factors=dec.get("upsample_factors", [1, 2, 2, 1]),
+        dropout=enc.get("dropout", 0.1),
+        attn_dropout=tr.get("attention_dropout", 0.1),
+        drop_path_rate=tr.get("drop_path_rate", 0.1),
+        use_skip_connections=dec.get("use_skip_connections", True),
+    )
+    kw.update(overrides)
+    return HybridViT(**kw)

@@ -1,0 +1,384 @@
+"""GPU: each libhvit kernel family against a plain PyTorch fp32 reference of
+the same op on the same device (f32 path: tight; bf16 path: bf16 tolerances).
+Dropout masks are checked bit-exactly against the numpy mirror of the hash."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import keep_mask
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _setup():
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    torch.manual_seed(0)
+
+
+def rel(a, b):
+    a = a.double()
+    b = b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def tol(dt):
+    return 2e-5 if dt == "f32" else 2e-2
+
+
+def tdt(dt):
+    return torch.float32 if dt == "f32" else torch.bfloat16
+
+
+def L(hv):
+    return hv._lib
+
+
+def s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ----------------------------------------------------------------- linear ---
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(333, 136, 72), (8192, 512, 512), (64, 1536, 64), (5, 24, 16)])
+def test_linear_fwd(hv, dt, M, N, K):
+    l = L(hv)
+    x = torch.randn(M, K, device=DEV).to(tdt(dt))
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(tdt(dt))
+    b = torch.randn(N, device=DEV)
+    y = torch.empty(M, N, device=DEV)
+    l.call("hvit_linear_fwd", l.dt_of(x), x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, y.data_ptr(), l.F32,
+           None, s())
+    ref = x.float() @ w.float().t() + b
+    assert rel(y, ref) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_linear_fwd_epilogues(hv, dt):
+    l = L(hv)
+    from importlib import import_module
+    HF = import_module("hvit_amd.functional")
+    M, N, K, Nt = 256, 128, 64, 64
+    x = torch.randn(M, K, device=DEV).to(tdt(dt))
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(tdt(dt))
+    b = torch.randn(N, device=DEV)
+    ref = x.float() @ w.float().t() + b
+    # GELU_DUAL + dropout
+    h = torch.empty(M, N, device=DEV, dtype=tdt(dt))
+    a = torch.empty(M, N, device=DEV, dtype=tdt(dt))
+    dr = l.dropout(0.25, 99, 5)
+    l.call("hvit_linear_fwd", l.dt_of(x), x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, h.data_ptr(),
+           l.dt_of(h), HF.epilogue(act=l.ACT_GELU_DUAL, out2=a, drop=dr), s())
+    mask = torch.as_tensor(keep_mask(99, 5, M * N, 0.25).reshape(M, N), device=DEV)
+    assert rel(h.float(), ref) < tol(dt)
+    assert rel(a.float(), F.gelu(ref) * mask / 0.75) < tol(dt)
+    # residual + per-sample scale + dropout
+    resid = torch.randn(M, N, device=DEV)
+    rs = torch.tensor([0.0, 1.25, 1.25, 0.5], device=DEV)
+    y = torch.empty(M, N, device=DEV)
+    l.call("hvit_linear_fwd", l.dt_of(x), x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, y.data_ptr(), l.F32,
+           HF.epilogue(drop=dr, resid=resid, rowscale=rs, rps=Nt), s())
+    exp = resid + rs.repeat_interleave(Nt)[:, None] * (ref * mask / 0.75)
+    assert rel(y, exp) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_linear_dgrad_gelu_bwd(hv, dt):
+    l = L(hv)
+    HF = __import__("hvit_amd.functional", fromlist=["x"])
+    M, N, K = 300, 256, 512
+    dy = torch.randn(M, N, device=DEV).to(tdt(dt))
+    w = (torch.randn(N, K, device=DEV) / N ** 0.5).to(tdt(dt))
+    hpre = torch.randn(M, K, device=DEV).to(tdt(dt))
+    dx = torch.empty(M, K, device=DEV)
+    l.call("hvit_linear_dgrad", l.dt_of(dy), dy.data_ptr(), w.data_ptr(), M, N, K, dx.data_ptr(), l.F32, None, s())
+    ref = dy.float() @ w.float()
+    assert rel(dx, ref) < tol(dt)
+    dr = l.dropout(0.1, 7, 3)
+    l.call("hvit_linear_dgrad", l.dt_of(dy), dy.data_ptr(), w.data_ptr(), M, N, K, dx.data_ptr(), l.F32,
+           HF.epilogue(act=l.ACT_GELU_BWD, aux=hpre, drop=dr), s())
+    hp = hpre.float().requires_grad_(True)
+    F.gelu(hp).backward(torch.ones_like(hp))
+    mask = torch.as_tensor(keep_mask(7, 3, M * K, 0.1).reshape(M, K), device=DEV)
+    assert rel(dx, ref * mask / 0.9 * hp.grad) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 512), (8192, 1536, 512), (100, 40, 24), (131072, 64, 64)])
+def test_linear_wgrad(hv, dt, M, N, K):
+    l = L(hv)
+    dy = torch.randn(M, N, device=DEV).to(tdt(dt))
+    x = torch.randn(M, K, device=DEV).to(tdt(dt))
+    dw = torch.empty(N, K, device=DEV)
+    ws_n = l.lib().hvit_wgrad_workspace(M, N, K)
+    ws = torch.empty(max(ws_n, 1), device=DEV)
+    l.call("hvit_linear_wgrad", l.dt_of(dy), dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(),
+           ws_n, s())
+    ref = dy.float().t() @ x.float()
+    assert rel(dw, ref) < (1e-4 if dt == "f32" else 2e-2)
+
+
+def test_reduce_rows_and_cast(hv):
+    l = L(hv)
+    x = torch.randn(1000, 300, device=DEV)
+    out = torch.empty(300, device=DEV)
+    l.call("hvit_reduce_rows", x.data_ptr(), l.F32, 1000, 300, 300, 0, out.data_ptr(), s())
+    assert rel(out, x.sum(0)) < 1e-5
+    xb = torch.empty(1000, 300, device=DEV, dtype=torch.bfloat16)
+    l.call("hvit_cast", x.data_ptr(), l.F32, xb.data_ptr(), l.BF16, x.numel(), s())
+    assert torch.equal(xb, x.to(torch.bfloat16))
+
+
+# ------------------------------------------------------------------- conv ---
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2)
+
+
+def pack(hv, w, mode, dt):
+    from importlib import import_module
+    return import_module("hvit_amd.functional").pack_conv(w, mode, hv._lib.F32 if dt == "f32" else hv._lib.BF16)
+
+
+CONV_CASES = [
+    # N, Hs, Ws, C1, C2, U, Cout, KS
+    (2, 16, 16, 64, 0, 1, 128, 3),
+    (2, 8, 8, 256, 128, 2, 128, 3),
+    (1, 9, 7, 32, 16, 2, 16, 3),
+    (2, 33, 47, 1, 0, 1, 8, 3),
+    (2, 12, 10, 64, 0, 1, 1, 3),
+]
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv3x3_fwd_bwd(hv, dt, case):
+    l = L(hv)
+    HF = __import__("hvit_amd.functional", fromlist=["x"])
+    N, Hs, Ws, C1, C2, U, Cout, KS = case
+    x1 = torch.randn(N, C1, Hs, Ws, device=DEV).to(tdt(dt))
+    x2 = torch.randn(N, C2, Hs, Ws, device=DEV).to(tdt(dt)) if C2 else None
+    w = torch.randn(Cout, C1 + C2, KS, KS, device=DEV) / ((C1 + C2) * KS * KS) ** 0.5
+    wq = w.to(tdt(dt)).float()
+    # torch reference in fp32 on the rounded operands
+    xr = torch.cat([x1.float(), x2.float()], 1) if C2 else x1.float()
+    xr.requires_grad_(True)
+    xu = F.interpolate(xr, scale_factor=U, mode="nearest") if U > 1 else xr
+    wr = wq.clone().requires_grad_(True)
+    ref = F.conv2d(xu, wr, None, 1, KS // 2)
+    H, W = Hs * U, Ws * U
+    dtc = l.F32 if dt == "f32" else l.BF16
+    a1, a2 = nhwc(x1), (nhwc(x2) if C2 else None)
+    g = HF.geom(a1, C1, a2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
+    wp = pack(hv, w, 0, dt)
+    z = torch.empty(N, H, W, Cout, device=DEV)
+    nt = (N * H * W + 127) // 128
+    part = torch.empty(nt, Cout, 2, device=DEV)
+    l.call("hvit_conv_fwd", dtc, g, wp.data_ptr(), None, z.data_ptr(), l.F32, part.data_ptr(), None, s())
+    assert rel(nchw(z), ref) < tol(dt)
+    # BatchNorm statistics from the fused partials
+    mean = torch.empty(Cout, device=DEV)
+    inv = torch.empty(Cout, device=DEV)
+    l.call("hvit_bn_finalize", part.data_ptr(), nt, 128, N * H * W, Cout, mean.data_ptr(), inv.data_ptr(), None,
+           None, None, 0.1, 1e-5, s())
+    rm = ref.detach().mean((0, 2, 3))
+    rv = ref.detach().var((0, 2, 3), unbiased=False)
+    assert (mean - rm).abs().max().item() < 1e-3 * (rv.max().sqrt().item())
+    assert rel(inv, (rv + 1e-5).rsqrt()) < 1e-3
+    # backward
+    gz = torch.randn_like(ref)
+    ref.backward(gz)
+    dz = nhwc(gz).to(tdt(dt))
+    ws_n = l.lib().hvit_conv_wgrad_workspace(g)
+    ws = torch.empty(max(ws_n, 1), device=DEV)
+    dwp = torch.empty(w.numel(), device=DEV)
+    l.call("hvit_conv_wgrad", dtc, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, s())
+    dw = HF.unpack_conv(dwp, w.shape)
+    assert rel(dw, wr.grad) < (1e-4 if dt == "f32" else 3e-2)
+    wd = pack(hv, w, 1, dt)
+    du = torch.empty(N, H, W, C1 + C2, device=DEV, dtype=tdt(dt))
+    l.call("hvit_conv_dgrad", dtc, g, dz.data_ptr(), wd.data_ptr(), du.data_ptr(), dtc, s())
+    dx1 = torch.empty(N, Hs, Ws, C1, device=DEV)
+    dx2 = torch.empty(N, Hs, Ws, max(C2, 1), device=DEV)
+    l.call("hvit_upsample_split_bwd", du.data_ptr(), dtc, N, Hs, Ws, U, C1, C2, dx1.data_ptr(), l.F32,
+           dx2.data_ptr() if C2 else None, l.F32, s())
+    gx = xr.grad
+    assert rel(nchw(dx1), gx[:, :C1]) < (1e-4 if dt == "f32" else 3e-2)
+    if C2:
+        assert rel(nchw(dx2), gx[:, C1:]) < (1e-4 if dt == "f32" else 3e-2)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("case", [(2, 64, 64, 256, 512, 4), (1, 64, 62, 32, 64, 4), (2, 8, 11, 32, 64, 4)])
+def test_patch_embed_conv(hv, dt, case):
+    l = L(hv)
+    HF = __import__("hvit_amd.functional", fromlist=["x"])
+    N, H, W, C, D, P = case
+    x = torch.randn(N, C, H, W, device=DEV).to(tdt(dt))
+    w = torch.randn(D, C, P, P, device=DEV) / (C * P * P) ** 0.5
+    b = torch.randn(D, device=DEV)
+    pos = torch.randn(1, 100, D, device=DEV)
+    xr = x.float().requires_grad_(True)
+    wr = w.to(tdt(dt)).float().requires_grad_(True)
+    t = F.conv2d(xr, wr, b, P)
+    Hp, Wp = t.shape[2], t.shape[3]
+    ref = t.flatten(2).transpose(1, 2) + pos[:, : Hp * Wp]
+    dtc = l.F32 if dt == "f32" else l.BF16
+    xa = nhwc(x)
+    g = HF.geom(xa, C, None, 0, N, H, W, 1, P, P, 0, D)
+    wp = pack(hv, w, 0, dt)
+    out = torch.empty(N, Hp * Wp, D, device=DEV)
+    l.call("hvit_conv_fwd", dtc, g, wp.data_ptr(), b.data_ptr(), out.data_ptr(), l.F32, None,
+           HF.epilogue(rowadd=pos, rowadd_rows=Hp * Wp), s())
+    assert rel(out, ref) < tol(dt)
+    gt = torch.randn_like(ref)
+    ref.backward(gt)
+    gq = gt.to(tdt(dt)).contiguous()
+    dx = torch.empty(N, H, W, C, device=DEV, dtype=tdt(dt))
+    l.call("hvit_conv_dgrad", dtc, g, gq.data_ptr(), wp.data_ptr(), dx.data_ptr(), dtc, s())
+    assert rel(nchw(dx.float()), xr.grad) < (1e-4 if dt == "f32" else 3e-2)
+    dw = HF.conv_wgrad(dtc, g, gq, w.shape)
+    assert rel(dw, wr.grad) < (1e-4 if dt == "f32" else 3e-2)
+
+
+# -------------------------------------------------------------- attention ---
+def attn_ref(qkv, B, N, H, hd, p=0.0, mask=None):
+    q, k, v = qkv.view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    a = (q @ k.transpose(-2, -1)) * hd ** -0.5
+    a = a.softmax(-1)
+    if mask is not None:
+        a = a * mask / (1 - p)
+    o = (a @ v).transpose(1, 2).reshape(B * N, H * hd)
+    return o, a
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("B,N,H,hd,p", [(2, 256, 8, 64, 0.0), (1, 240, 8, 64, 0.1), (2, 16, 4, 16, 0.0),
+                                        (1, 4, 4, 16, 0.2), (3, 100, 2, 32, 0.0), (2, 300, 2, 64, 0.1)])
+def test_mhsa_fwd_bwd(hv, dt, B, N, H, hd, p):
+    l = L(hv)
+    D = H * hd
+    qkv = (torch.randn(B * N, 3 * D, device=DEV) * 0.7).to(tdt(dt))
+    dtc = l.F32 if dt == "f32" else l.BF16
+    dr = l.dropout(p, 4242, 17)
+    mask = None
+    if p > 0:
+        mask = torch.as_tensor(keep_mask(4242, 17, B * H * N * N, p).reshape(B, H, N, N), device=DEV).float()
+    xr = qkv.float().requires_grad_(True)
+    o_ref, a_ref = attn_ref(xr, B, N, H, hd, p, mask)
+    o = torch.empty(B * N, D, device=DEV, dtype=tdt(dt))
+    lse = torch.empty(B, H, N, device=DEV)
+    probs = torch.empty(B, H, N, N, device=DEV)
+    l.call("hvit_mhsa_fwd", dtc, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+           probs.data_ptr(), s())
+    assert rel(o.float(), o_ref) < tol(dt)
+    assert rel(probs, a_ref) < tol(dt)
+    go = torch.randn_like(o_ref)
+    o_ref.backward(go)
+    gq = go.to(tdt(dt)).contiguous()
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B, H, N, device=DEV)
+    l.call("hvit_mhsa_bwd", dtc, qkv.data_ptr(), o.data_ptr(), gq.data_ptr(), lse.data_ptr(), B, N, H, hd,
+           hd ** -0.5, dr, dqkv.data_ptr(), delta.data_ptr(), s())
+    g = dqkv.float().view(B * N, 3, D)
+    r = xr.grad.view(B * N, 3, D)
+    for i in range(3):
+        assert rel(g[:, i], r[:, i]) < (1e-4 if dt == "f32" else 4e-2), "qkv"[i]
+
+
+# ------------------------------------------------------------- layernorm ---
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("M,D", [(8192, 512), (37, 64), (16, 768)])
+def test_layernorm(hv, dt, M, D):
+    l = L(hv)
+    x = (torch.randn(M, D, device=DEV) * 3 + 1).requires_grad_(True)
+    g = (torch.rand(D, device=DEV) + 0.5).requires_grad_(True)
+    b = torch.randn(D, device=DEV).requires_grad_(True)
+    ref = F.layer_norm(x, (D,), g, b, 1e-5)
+    dtc = l.F32 if dt == "f32" else l.BF16
+    y = torch.empty(M, D, device=DEV, dtype=tdt(dt))
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    l.call("hvit_layernorm_fwd", x.data_ptr(), g.data_ptr(), b.data_ptr(), M, D, 1e-5, y.data_ptr(), dtc,
+           mean.data_ptr(), rstd.data_ptr(), s())
+    assert rel(y.float(), ref) < (1e-5 if dt == "f32" else 1e-2)
+    dy = torch.randn(M, D, device=DEV)
+    ref.backward(dy)
+    resid = torch.randn(M, D, device=DEV)
+    dx = torch.empty(M, D, device=DEV)
+    dg = torch.empty(D, device=DEV)
+    db = torch.empty(D, device=DEV)
+    l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), s())
+    assert rel(dx - resid, x.grad) < 1e-4
+    assert rel(dg, g.grad) < 1e-4
+    assert rel(db, b.grad) < 1e-4
+
+
+# ------------------------------------------------------------- batchnorm ---
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("N,H,W,C,pool,p", [(2, 32, 32, 64, 2, 0.0), (3, 15, 17, 16, 2, 0.3),
+                                            (2, 16, 16, 256, 1, 0.1), (1, 8, 8, 8, 1, 0.0)])
+def test_bn_act(hv, dt, N, H, W, C, pool, p):
+    l = L(hv)
+    z = torch.randn(N, C, H, W, device=DEV).to(tdt(dt)).float()
+    zr = z.clone().requires_grad_(True)
+    gamma = (torch.rand(C, device=DEV) + 0.5).requires_grad_(True)
+    beta = (torch.randn(C, device=DEV) * 0.3).requires_grad_(True)
+    m = zr.mean((0, 2, 3))
+    v = zr.var((0, 2, 3), unbiased=False)
+    bn = (zr - m[None, :, None, None]) * (v[None, :, None, None] + 1e-5).rsqrt()
+    y = F.relu(bn * gamma[None, :, None, None] + beta[None, :, None, None])
+    mask = torch.ones(N, C, device=DEV)
+    if p > 0:
+        mask = torch.as_tensor(keep_mask(31, 9, N * C, p).reshape(N, C), device=DEV).float() / (1 - p)
+    y = y * mask[:, :, None, None]
+    if pool > 1:
+        y = F.max_pool2d(y, pool)
+    dtc = l.F32 if dt == "f32" else l.BF16
+    za = nhwc(z).to(tdt(dt))
+    mean = m.detach().contiguous()
+    inv = (v.detach() + 1e-5).rsqrt().contiguous()
+    out = torch.empty(N, H // pool, W // pool, C, device=DEV)
+    dr = l.dropout(p, 31, 9)
+    l.call("hvit_bn_act_fwd", dtc, za.data_ptr(), N, H, W, C, mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+           beta.data_ptr(), dr, pool, out.data_ptr(), l.F32, s())
+    assert rel(nchw(out), y) < 1e-5
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    dz = torch.empty(N, H, W, C, device=DEV)
+    sums = torch.empty(2 * C, device=DEV)
+    gya = nhwc(gy)
+    l.call("hvit_bn_act_bwd", dtc, za.data_ptr(), N, H, W, C, mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+           beta.data_ptr(), dr, pool, gya.data_ptr(), l.F32, 1, dz.data_ptr(), l.F32, sums.data_ptr(), s())
+    assert rel(nchw(dz), zr.grad) < 1e-4
+    assert rel(sums[:C], beta.grad) < 1e-4
+    assert rel(sums[C:], gamma.grad) < 1e-4
+
+
+# -------------------------------------------------------------- bilinear ---
+@pytest.mark.parametrize("N,Hi,Wi,C,Ho,Wo", [(2, 64, 64, 256, 16, 16), (2, 64, 64, 1, 256, 256),
+                                             (1, 8, 8, 1, 33, 47), (2, 16, 23, 8, 4, 4), (1, 64, 60, 1, 257, 251),
+                                             (1, 128, 125, 64, 32, 30)])
+def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
+    l = L(hv)
+    x = torch.randn(N, C, Hi, Wi, device=DEV, requires_grad=True)
+    ref = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=False)
+    xa = nhwc(x.detach())
+    y = torch.empty(N, Ho, Wo, C, device=DEV)
+    l.call("hvit_bilinear_fwd", xa.data_ptr(), l.F32, N, Hi, Wi, C, Ho, Wo, y.data_ptr(), l.F32, s())
+    assert rel(nchw(y), ref) < 1e-5
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    ga = nhwc(g)
+    dx = torch.empty(N, Hi, Wi, C, device=DEV)
+    l.call("hvit_bilinear_bwd", ga.data_ptr(), l.F32, N, Ho, Wo, C, Hi, Wi, dx.data_ptr(), l.F32, 0, s())
+    assert rel(nchw(dx), x.grad) < 1e-5

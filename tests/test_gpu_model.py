@@ -1,0 +1,166 @@
+"""GPU: the whole HybridViT forward/backward on libhvit.so against the golden
+vectors recorded from the reference (tests/golden, via tools/gen_golden.py) and
+against the CPU oracle.  North-star bar: fp32 forward within 1e-3 relative of
+the reference; bf16 path within bf16 tolerances."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import closed_form as CF
+from oracle import hvit_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FP32_TOL = 1e-3      # north_star: forward within 1e-3 rel (fp32)
+BF16_TOL = 5e-2
+
+
+def rel(a, b):
+    a = torch.as_tensor(np.asarray(a)).double()
+    b = torch.as_tensor(np.asarray(b)).double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def relnorm(a, b):
+    a = torch.as_tensor(np.asarray(a)).double()
+    b = torch.as_tensor(np.asarray(b)).double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+CASES = [("tiny_64", O.TINY), ("tiny_odd", O.TINY), ("tiny_clip", O.TINY), ("default_256", {}),
+         ("default_clip", {})]
+
+
+def build(hv, kw, precision, train):
+    cfg = O.HViTConfig(**kw)
+    if train:
+        cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
+    W = CF.weights(O.state_dict_shapes(cfg))
+    m = hv.HybridViT(**cfg.as_kwargs(), precision=precision).cuda()
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
+    return m
+
+
+@pytest.mark.parametrize("name,kw", CASES)
+def test_eval_forward_fp32(hv, name, kw):
+    g = golden(name)
+    m = build(hv, kw, "fp32", False).eval()
+    x = torch.as_tensor(g["x"]).cuda()
+    with torch.no_grad():
+        if "eval_attn0" in g:
+            y, attn = m(x, return_attentions=True)
+            for l, a in enumerate(attn):
+                assert rel(a.cpu(), g[f"eval_attn{l}"]) < FP32_TOL
+        else:
+            y = m(x)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == tuple(g["eval_out"].shape)
+    assert rel(y.cpu(), g["eval_out"]) < FP32_TOL, name
+
+
+@pytest.mark.parametrize("name,kw", CASES)
+def test_train_step_fp32(hv, name, kw):
+    g = golden(name)
+    m = build(hv, kw, "fp32", True).train()
+    x = torch.as_tensor(g["x"]).cuda()
+    y = m(x)
+    loss = hv.CombinedLoss()(y, torch.as_tensor(g["target"]).cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel(y.detach().cpu(), g["train_out"]) < FP32_TOL
+    assert abs(loss.item() - float(g["train_loss"])) < 1e-4 * abs(float(g["train_loss"]))
+    named = dict(m.named_parameters())
+    checked = 0
+    for k, p in named.items():
+        gk = f"grad.{k}"
+        ref_norm = float(g[f"gnorm.{k}"])
+        got = p.grad.detach().cpu()
+        if ref_norm > 1e-8:
+            assert abs(got.double().norm().item() - ref_norm) < 2e-3 * ref_norm, k
+        if gk in g:
+            gr = got
+            if k == "pos_encoding.pos_embed":
+                gr = gr[:, : g[gk].shape[1]]
+            assert relnorm(gr, g[gk]) < 2e-3, k
+            checked += 1
+    assert checked >= 6
+    bufs = dict(m.named_buffers())
+    for k in bufs:
+        if f"buf.{k}" in g:
+            assert rel(bufs[k].cpu(), g[f"buf.{k}"]) < 1e-4, k
+
+
+@pytest.mark.parametrize("name,kw", [("tiny_64", O.TINY), ("default_256", {}), ("default_clip", {})])
+def test_bf16_path(hv, name, kw):
+    g = golden(name)
+    m = build(hv, kw, "bf16", False).eval()
+    with torch.no_grad():
+        y = m(torch.as_tensor(g["x"]).cuda())
+    assert rel(y.cpu(), g["eval_out"]) < BF16_TOL
+    m = build(hv, kw, "bf16", True).train()
+    y = m(torch.as_tensor(g["x"]).cuda())
+    loss = hv.CombinedLoss()(y, torch.as_tensor(g["target"]).cuda())
+    loss.backward()
+    assert abs(loss.item() - float(g["train_loss"])) < 2e-2 * abs(float(g["train_loss"]))
+    qk = "transformer.blocks.0.attn.qkv.weight"
+    gq = dict(m.named_parameters())[qk].grad.cpu()
+    assert abs(gq.double().norm().item() - float(g[f"gnorm.{qk}"])) < 0.1 * float(g[f"gnorm.{qk}"])
+
+
+def test_autocast_selects_bf16(hv):
+    m = build(hv, O.TINY, "auto", False).eval()
+    x = torch.as_tensor(CF.spectrogram((2, 1, 64, 64), 5)).cuda()
+    with torch.no_grad():
+        y32 = m(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y16 = m(x)
+    assert y32.dtype == torch.float32 and y16.dtype == torch.float32
+    d = (y32 - y16).abs().max().item()
+    assert 0 < d < 0.05
+
+
+def test_dropout_train_mode_is_seeded(hv):
+    cfg = dict(O.TINY)
+    m = hv.HybridViT(**cfg, precision="fp32").cuda().train()
+    x = torch.as_tensor(CF.spectrogram((2, 1, 64, 64), 6)).cuda()
+    torch.manual_seed(1)
+    y1 = m(x)
+    torch.manual_seed(1)
+    y2 = m(x)
+    torch.manual_seed(2)
+    y3 = m(x)
+    assert torch.equal(y1, y2)
+    assert not torch.equal(y1, y3)
+    y1.sum().backward()
+    for n, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
+def test_forward_encoder_transformer_decoder_api(hv):
+    g = golden("tiny_64")
+    m = build(hv, O.TINY, "fp32", False).eval()
+    x = torch.as_tensor(g["x"]).cuda()
+    with torch.no_grad():
+        feat, skips = m.forward_encoder(x)
+        for i, sk in enumerate(skips):
+            assert rel(sk.cpu(), g[f"eval_enc{i}"]) < FP32_TOL
+        tokens = torch.as_tensor(g["eval_tokens"]).cuda()
+        f = m.forward_transformer(tokens, (feat.shape[2] // 4, feat.shape[3] // 4))
+        out = m.forward_decoder(f, skips)
+    assert out.shape[2:] == (16, 16)
+
+
+def test_oracle_agreement_random_weights(hv):
+    """Random torch-initialised weights (not the closed form), fp32, vs oracle."""
+    torch.manual_seed(3)
+    cfg = O.HViTConfig(**O.TINY)
+    m = hv.HybridViT(**cfg.as_kwargs(), precision="fp32").eval()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda()
+    x = torch.rand(2, 1, 48, 80)
+    with torch.no_grad():
+        y = m(x.cuda()).cpu()
+        yo = O.forward(sd, x, cfg)
+    assert rel(y, yo) < FP32_TOL
