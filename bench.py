@@ -1,0 +1,214 @@
+"""HybridViT training-step throughput on MI355X (BASELINE.json metric).
+
+One step = one HybridViT forward (train mode, dropout on) + CombinedLoss +
+backward + [DP gradient all-reduce] + clip_grad_norm_(1.0) + AdamW step, at
+batch 32 per GPU of 1x256x256 synthetic magnitude spectrograms, bf16 compute
+(f32 master weights / statistics / gradients).  A frame is one STFT column, so
+one spectrogram = 256 frames.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints one JSON line.  ``roofline`` times the dominant kernel (the
+bf16 MLP fc1 GEMM with its fused GELU/dropout epilogue, the largest MFMA
+launch of the step) with HIP events on the stream it runs on;
+``cpu_baseline`` times the CPU oracle (oracle/, fp32 PyTorch restatement of
+the reference) on a bounded sample of the same step, on this host's cores.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FRAMES = 256
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    return ap.parse_args()
+
+
+def dominant_kernel_roofline(hv, batch):
+    """fc1 of one ViT block: [B*256, 512] x [512, 2048]^T + bias, GELU (dual
+    output) + dropout, bf16 MFMA.  2*M*N*K algorithmic FLOPs per launch."""
+    L = hv._lib
+    HF = sys.modules["hvit_amd.functional"]
+    M, N, K = batch * 256, 2048, 512
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.zeros(N, device="cuda")
+    h = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    a = torch.empty_like(h)
+    e = HF.epilogue(act=L.ACT_GELU_DUAL, out2=a, drop=L.dropout(0.1, 1, 1))
+    st = torch.cuda.current_stream()
+    args = (L.BF16, x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, h.data_ptr(), L.BF16, e, st.cuda_stream)
+    for _ in range(5):
+        L.call("hvit_linear_fwd", *args)
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        L.call("hvit_linear_fwd", *args)
+    e1.record(st)
+    e1.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3 / reps
+    flops = 2.0 * M * N * K
+    achieved = flops / sec / 1e12
+    return {"kernel": "hvit gemm_kernel<bf16,128,128,LdDense,LdDense> (fc1 + GELU_DUAL epilogue)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "flops_per_launch": flops, "avg_launch_us": round(sec * 1e6, 2)}
+
+
+def cpu_baseline(batch, budget_s):
+    """Oracle (fp32 PyTorch CPU restatement of the reference) train step:
+    fwd + CombinedLoss + bwd + AdamW, same shapes, bounded by ``budget_s``."""
+    from oracle import closed_form as CF
+    from oracle import hvit_oracle as O
+
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1))))
+    cfg = O.HViTConfig()
+    shapes = O.state_dict_shapes(cfg)
+    sd = O.make_state(shapes, CF.weights(shapes), requires_grad=True)
+    params = [v for k, v in sd.items() if v.requires_grad]
+    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=0.01)
+    x = torch.rand(batch, 1, 256, 256)
+    t = torch.rand(batch, 1, 256, 256)
+
+    def step():
+        y = O.forward(sd, x, cfg, training=True)
+        loss = O.combined_loss(y, t)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    step()  # warmup
+    n, t0 = 0, time.perf_counter()
+    while n < 3 and (time.perf_counter() - t0) < budget_s:
+        step()
+        n += 1
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(batch * FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/hvit_oracle.py fp32 train step (fwd+CombinedLoss+bwd+clip+AdamW), B={batch}, "
+                      f"1x256x256, 1 warmup + {n} timed steps, {dt:.2f} s/step"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import hvit_amd_loader
+
+    hv = hvit_amd_loader.load()
+    from hvit_amd.data import spectrogram_batch
+    from hvit_amd.dp import GradAllReducer, broadcast_module
+
+    torch.manual_seed(1234)
+    model = hv.HybridViT(precision=args.precision).cuda().train()
+    reducer = None
+    if world > 1:
+        broadcast_module(model)
+        reducer = GradAllReducer(model, bucket_mb=25, sliced={"pos_encoding.pos_embed": FRAMES})
+    try:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
+    except Exception:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True)
+    crit = hv.CombinedLoss()
+    noisy, clean = spectrogram_batch(args.batch, seed=1234 + rank * args.batch)
+    noisy, clean = noisy.cuda(), clean.cuda()
+    torch.manual_seed(1000 + rank)
+
+    def step():
+        y = model(noisy)
+        loss = crit(y, clean)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        te = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = te.item()
+    ms = elapsed / args.steps * 1e3
+    spectros = world * args.batch * args.steps / elapsed
+    value = spectros * FRAMES
+    if not torch.isfinite(loss).item():
+        raise RuntimeError("non-finite loss")
+
+    out = None
+    if rank == 0:
+        roof = dominant_kernel_roofline(hv, args.batch)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.batch, args.cpu_seconds)
+        out = {
+            "metric": "spectrogram-frames/sec/GPU (fwd+bwd) on 256x256 mag-spec, batch 32; 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "spectrogram-frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (harmonic+noise 16 kHz waveforms, host STFT 512/128 hann, min-max, 256x256)",
+            "config": {"workload": "HybridViT default (enc 64/128/256, 6x8-head d512 ViT, dec 256/128/64/1) train "
+                                   "step: fwd + CombinedLoss + bwd + clip + AdamW",
+                       "global_batch": world * args.batch, "seq_len": 256, "input": [args.batch, 1, 256, 256],
+                       "parallelism": f"dp{world}"},
+            "spectrograms_per_s": round(spectros, 2),
+            "frames_per_s_per_gpu": round(value / world, 1),
+            "final_loss": round(loss.item(), 6),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

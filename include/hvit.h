@@ -94,7 +94,7 @@ int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K
  * Weights are pre-packed with hvit_conv_weight_pack: mode 0 [Cout][KS][KS][Cin]
  * for fwd / wgrad / patch dgrad; mode 1 (flipped) [Cin][KS][KS][Cout] for the
  * 3x3 dgrad.  conv_fwd optionally writes BatchNorm partials
- * [ceil(P/128)][Cout][2] (mean, M2 per 128-row tile) for hvit_bn_finalize; its
+ * [ceil(P/64)][Cout][2] (mean, M2 per 64-row tile) for hvit_bn_finalize; its
  * epilogue (nullable) may apply tanh (final decoder conv, components.py:166-167),
  * a row-periodic add (pos_embed, components.py:384) and dropout.
  * conv_dgrad: same-conv -> gradient of the (upsampled, concatenated) conv input

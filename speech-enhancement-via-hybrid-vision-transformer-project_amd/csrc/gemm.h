@@ -143,11 +143,119 @@ struct Epi {
   long ldr = 0;
   const float* rowscale = nullptr;
   int rows_per_sample = 1;
-  float* stats = nullptr;   // BN partials [row_tile][N][2] = (mean, M2)
+  float* stats = nullptr;   // BN partials [64-row tile][N][2] = (mean, M2)
   float* colsum = nullptr;  // atomic column sums of the final v
   // EPI_PATCH: m = token (b, py, px) of Hp x Wp, n = (ky*P + kx)*C + c
   int pP = 0, pC = 0, pHp = 0, pWp = 0, pH = 0, pW = 0;
 };
+
+// 4 adjacent output columns (n .. n+nv-1) of row m: store helpers and the
+// fused epilogue math.
+__device__ __forceinline__ void store4(void* p, long off, const f32x4& v, int nv, int dt) {
+  if (dt == HVIT_F32) {
+    float* q = (float*)p + off;
+    if (nv == 4 && (((uintptr_t)q) & 15) == 0) *(f32x4*)q = v;
+    else for (int e = 0; e < nv; ++e) q[e] = v[e];
+  } else {
+    bf16_t* q = (bf16_t*)p + off;
+    if (nv == 4 && (((uintptr_t)q) & 7) == 0) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *(uint2*)q = u;
+    } else {
+      for (int e = 0; e < nv; ++e) q[e] = f2bf(v[e]);
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 load4(const void* p, long off, int nv, int dt) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (dt == HVIT_F32) {
+    const float* q = (const float*)p + off;
+    if (nv == 4 && (((uintptr_t)q) & 15) == 0) return *(const f32x4*)q;
+    for (int e = 0; e < nv; ++e) v[e] = q[e];
+  } else {
+    const bf16_t* q = (const bf16_t*)p + off;
+    if (nv == 4 && (((uintptr_t)q) & 7) == 0) {
+      uint2 u = *(const uint2*)q;
+      v[0] = __uint_as_float(u.x << 16);
+      v[1] = __uint_as_float(u.x & 0xffff0000u);
+      v[2] = __uint_as_float(u.y << 16);
+      v[3] = __uint_as_float(u.y & 0xffff0000u);
+      return v;
+    }
+    for (int e = 0; e < nv; ++e) v[e] = bf2f(q[e]);
+  }
+  return v;
+}
+
+__device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, int N, f32x4& v) {
+  if (ep.bias) {
+    f32x4 b = load4(ep.bias, n, nv, HVIT_F32);
+    v += b;
+  }
+  if (ep.rowadd) v += load4(ep.rowadd, (long)(m % ep.rowadd_mod) * ep.rowadd_ld + n, nv, HVIT_F32);
+  float keep[4] = {1.f, 1.f, 1.f, 1.f};
+  if (ep.drop_thr) {
+    const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
+    if ((i0 & 3) == 0) {
+      uint64_t h = mix64(ep.seed ^ ((uint64_t)ep.site << 48) ^ ((i0 >> 2) * 0xD6E8FEB86659FD93ull));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) keep[e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= ep.drop_thr) ? ep.drop_scale : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) keep[e] = rng_keep(ep.seed, ep.site, i0 + e, ep.drop_thr) ? ep.drop_scale : 0.f;
+    }
+  } else if (ep.drop_scale != 1.f) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) keep[e] = ep.drop_scale;
+  }
+  if (ep.act == ACT_GELU_DUAL) {
+    store4(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
+    f32x4 g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[e] = gelu_f(v[e]) * keep[e];
+    store4(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
+    return;
+  }
+  if (ep.act == ACT_TANH) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] *= keep[e];
+  if (ep.act == ACT_GELU_BWD) {
+    f32x4 h = load4(ep.aux, (long)m * ep.ldaux + n, nv, ep.aux_dt);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(h[e]);
+  }
+  if (ep.resid) {
+    const float s = ep.rowscale ? ep.rowscale[m / ep.rows_per_sample] : 1.f;
+    f32x4 r = load4(ep.resid, (long)m * ep.ldr + n, nv, HVIT_F32);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = r[e] + s * v[e];
+  }
+  if (ep.mode == EPI_STORE) {
+    store4(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
+  } else if (ep.mode == EPI_SPLIT2) {
+    for (int e = 0; e < nv; ++e) {
+      if (n + e < ep.split_col) st_dt(ep.out, (long)m * ep.ldo + n + e, v[e], ep.out_dt);
+      else st_dt(ep.out2, (long)m * ep.ldo2 + (n + e - ep.split_col), v[e], ep.out2_dt);
+    }
+  } else {  // EPI_PATCH: m = token (b, py, px), n = (ky*P + kx)*C + c
+    const int hw = ep.pHp * ep.pWp;
+    const int b = m / hw, rem = m - b * hw;
+    const int py = rem / ep.pWp, px = rem - py * ep.pWp;
+    for (int e = 0; e < nv; ++e) {
+      const int nn = n + e;
+      const int tap = nn / ep.pC, c = nn - tap * ep.pC;
+      const int ky = tap / ep.pP, kx = tap - ky * ep.pP;
+      const long o = (((long)b * ep.pH + py * ep.pP + ky) * ep.pW + px * ep.pP + kx) * ep.pC + c;
+      st_dt(ep.out, o, v[e], ep.out_dt);
+    }
+  }
+}
 
 template <typename T, int BM, int BN, class LA, class LB>
 __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M, int N, int K,
@@ -161,7 +269,10 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M,
   constexpr int CB = BN * 4 / GEMM_THREADS;
   static_assert(CA >= 1 && CB >= 1, "tile too small");
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB];
+  // main loop: 2 stages of A/B tiles; epilogue: a 64-row f32 tile + reduction rows
+  constexpr int SM_LOOP = 2 * (BM + BN) * ROWB;
+  constexpr int SM_EPI = (64 * (BN + 4) + (GEMM_THREADS / (BN / 4)) * BN) * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI];
   char* As = smem;
   char* Bs = smem + 2 * BM * ROWB;
 
@@ -279,143 +390,137 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M,
   }
 
   // ------------------------------------------------------------- epilogue ---
-  // element (i, j, r): m = m0 + wm*WTM + i*16 + fq*4 + r ; n = n0 + wn*WTN + j*16 + frow
-  const int mb = m0 + wm * WTM + fq * 4;
-  const int nb = n0 + wn * WTN + frow;
-  if (ep.mode == EPI_SLAB) {
-    float* slab = (float*)ep.out + (long)blockIdx.z * M * ep.ldo;
+  // The accumulator tile is staged through LDS in 64-row halves (f32, padded
+  // rows) and then processed row-contiguously: each thread owns 4 adjacent
+  // columns, so bias / residual / aux loads and output stores are vectorised
+  // and coalesced, and every acc[][] index stays static (no scratch).
+  constexpr int CP = BN + 4;                 // LDS tile pitch (floats)
+  constexpr int HALVES = BM / 64;
+  constexpr int C4 = BN / 4;                 // 4-column chunks per row
+  constexpr int RSTEP = GEMM_THREADS / C4;   // rows advanced per sweep
+  static_assert((64 * CP + RSTEP * BN) * 4 <= (int)sizeof(smem), "epilogue tile exceeds LDS");
+  float* Cs = (float*)smem;
+  const int c4 = tid % C4;
+  const int r0 = tid / C4;
+  const int n = n0 + c4 * 4;
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int hh = 0; hh < HALVES; ++hh) {
+    if (hh > 0) __syncthreads();
+    // write this half's accumulators: wave rows wm*WTM + i*16 + fq*4 + r
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          int m = mb + i * 16 + r, n = nb + j * 16;
-          if (m < M && n < N) slab[(long)m * ep.ldo + n] = acc[i][j][r];
+          const int row = wm * WTM + i * 16 + fq * 4 + r - hh * 64;
+          if (row >= 0 && row < 64) Cs[row * CP + wn * WTN + j * 16 + frow] = acc[i][j][r];
         }
-    return;
-  }
+    __syncthreads();
+    const int mbase = m0 + hh * 64;
+    const int rows_here = min(64, M - mbase);
+    float st_sum[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int row = r0; row < 64; row += RSTEP) {
+      const int m = mbase + row;
+      if (m >= M || n >= N) continue;
+      f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
+      const bool full = n + 3 < N;
+      const int nv = full ? 4 : N - n;
+      if (ep.mode == EPI_SLAB) {
+        float* slab = (float*)ep.out + (long)blockIdx.z * M * ep.ldo + (long)m * ep.ldo + n;
+        if (full && (ep.ldo & 3) == 0) *(f32x4*)slab = v;
+        else for (int e = 0; e < nv; ++e) slab[e] = v[e];
+        continue;
+      }
+      epi_apply4(ep, m, n, nv, N, v);
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int m = mb + i * 16 + r, n = nb + j * 16;
-        if (m >= M || n >= N) continue;
-        float v = acc[i][j][r];
-        if (ep.bias) v += ep.bias[n];
-        if (ep.rowadd) v += ep.rowadd[(long)(m % ep.rowadd_mod) * ep.rowadd_ld + n];
-        uint64_t didx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-        if (ep.act == ACT_GELU_DUAL) {
-          st_dt(ep.out, (long)m * ep.ldo + n, v, ep.out_dt);
-          float g = gelu_f(v);
-          if (ep.drop_thr && !rng_keep(ep.seed, ep.site, didx, ep.drop_thr)) g = 0.f;
-          else g *= ep.drop_scale;
-          st_dt(ep.out2, (long)m * ep.ldo2 + n, g, ep.out2_dt);
-          acc[i][j][r] = v;
-          continue;
-        }
-        if (ep.act == ACT_TANH) v = tanhf(v);
-        if (ep.drop_thr) v = rng_keep(ep.seed, ep.site, didx, ep.drop_thr) ? v * ep.drop_scale : 0.f;
-        else if (ep.drop_scale != 1.f) v *= ep.drop_scale;
-        if (ep.act == ACT_GELU_BWD) v *= gelu_grad(ld_dt(ep.aux, (long)m * ep.ldaux + n, ep.aux_dt));
-        if (ep.resid) {
-          float s = ep.rowscale ? ep.rowscale[m / ep.rows_per_sample] : 1.f;
-          v = ep.resid[(long)m * ep.ldr + n] + s * v;
-        }
-        acc[i][j][r] = v;
-        if (ep.mode == EPI_STORE) {
-          st_dt(ep.out, (long)m * ep.ldo + n, v, ep.out_dt);
-        } else if (ep.mode == EPI_SPLIT2) {
-          if (n < ep.split_col) st_dt(ep.out, (long)m * ep.ldo + n, v, ep.out_dt);
-          else st_dt(ep.out2, (long)m * ep.ldo2 + (n - ep.split_col), v, ep.out2_dt);
-        } else {  // EPI_PATCH
-          int hw = ep.pHp * ep.pWp;
-          int b = m / hw, rem = m - b * hw;
-          int py = rem / ep.pWp, px = rem - py * ep.pWp;
-          int tap = n / ep.pC, c = n - tap * ep.pC;
-          int ky = tap / ep.pP, kx = tap - ky * ep.pP;
-          long o = (((long)b * ep.pH + py * ep.pP + ky) * ep.pW + px * ep.pP + kx) * ep.pC + c;
-          st_dt(ep.out, o, v, ep.out_dt);
+      for (int e = 0; e < 4; ++e) {
+        if (e < nv) {
+          csum[e] += v[e];
+          st_sum[e] += v[e];
         }
       }
-
-  if (ep.colsum) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (mb + i * 16 + r < M) s += acc[i][j][r];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      int n = nb + j * 16;
-      if (fq == 0 && n < N) atomicAdd(ep.colsum + n, s);
+      Cs[row * CP + c4 * 4 + 0] = v[0];
+      Cs[row * CP + c4 * 4 + 1] = v[1];
+      Cs[row * CP + c4 * 4 + 2] = v[2];
+      Cs[row * CP + c4 * 4 + 3] = v[3];
     }
-  }
-
-  if (ep.stats) {
-    // per-column (mean, M2) over this tile's valid rows, two passes on-chip
-    float* red = (float*)smem;  // [WM][BN]
-    const int rows_valid = min(BM, M - m0);
-    float colmean[FN];
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
+    if (ep.stats && rows_here > 0) {
+      // per-column (mean, M2) of this 64-row sub-tile: sums -> mean -> M2
+      float* red = Cs + 64 * CP;  // [RSTEP][BN] scratch after the tile
+      __syncthreads();
+      for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = st_sum[e];
+      __syncthreads();
+      float mean[4], q[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 4; ++e) {
         float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (mb + i * 16 + r < M) {
-              float v = acc[i][j][r];
-              if (pass == 0) s += v;
-              else { float d = v - colmean[j]; s += d * d; }
-            }
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        if (fq == 0) red[wm * BN + wn * WTN + j * 16 + frow] = s;
+        for (int k = 0; k < RSTEP; ++k) s += red[k * BN + c4 * 4 + e];
+        mean[e] = s / (float)rows_here;
       }
+      for (int row = r0; row < rows_here; row += RSTEP)
+        for (int e = 0; e < 4; ++e) {
+          float d = Cs[row * CP + c4 * 4 + e] - mean[e];
+          q[e] += d * d;
+        }
       __syncthreads();
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        int cl = wn * WTN + j * 16 + frow;
-        float tot = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) tot += red[w * BN + cl];
-        if (pass == 0) colmean[j] = tot / (float)rows_valid;
-        else if (wm == 0 && fq == 0 && n0 + cl < N) {
-          float* o = ep.stats + ((long)blockIdx.x * N + n0 + cl) * 2;
-          o[0] = colmean[j];
-          o[1] = tot;
+      for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = q[e];
+      __syncthreads();
+      if (r0 == 0) {
+        const long tile = (m0 / 64) + hh;
+        for (int e = 0; e < 4; ++e) {
+          if (n + e >= N) break;
+          float s = 0.f;
+          for (int k = 0; k < RSTEP; ++k) s += red[k * BN + c4 * 4 + e];
+          ep.stats[(tile * N + n + e) * 2] = mean[e];
+          ep.stats[(tile * N + n + e) * 2 + 1] = s;
         }
       }
-      __syncthreads();
     }
+  }
+  if (ep.colsum) {
+    float* red = Cs + 64 * CP;
+    __syncthreads();
+    for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = csum[e];
+    __syncthreads();
+    if (r0 == 0)
+      for (int e = 0; e < 4; ++e) {
+        if (n + e >= N) break;
+        float s = 0.f;
+        for (int k = 0; k < RSTEP; ++k) s += red[k * BN + c4 * 4 + e];
+        atomicAdd(ep.colsum + n + e, s);
+      }
   }
 }
 
+
 // host-side launcher --------------------------------------------------------
-template <typename T, class LA, class LB>
-int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep, hipStream_t st,
-                int force_tile = 0) {
-  if (M <= 0 || N <= 0) return HVIT_OK;
+// Effective split-K count after rounding each split to whole K-tiles (never
+// more than requested).  Callers that reduce slabs must use this count.
+template <typename T>
+inline int plan_splits(int K, int splits, int* kps_out = nullptr) {
   constexpr int BK = 64 / sizeof(T);
   if (splits < 1) splits = 1;
   int kps = (K + splits - 1) / splits;
   kps = ((kps + BK - 1) / BK) * BK;
-  splits = K > 0 ? (K + kps - 1) / kps : 1;
+  if (kps < BK) kps = BK;
+  if (kps_out) *kps_out = kps;
+  return K > 0 ? (K + kps - 1) / kps : 1;
+}
+
+template <typename T, class LA, class LB>
+int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep, hipStream_t st,
+                int force_tile = 0) {
+  if (M <= 0 || N <= 0) return HVIT_OK;
+  int kps = 0;
+  splits = plan_splits<T>(K, splits, &kps);
   if (splits > 1 && ep.mode != EPI_SLAB) {
     hvit_set_error("launch_gemm: split-K requires EPI_SLAB");
     return HVIT_ERR_ARG;
   }
   int big = force_tile ? (force_tile == 128)
                        : ((long)cdiv(M, 128) * cdiv(N, 128) * splits >= 160);
-  if (ep.stats) big = 1;  // stats partial layout is per 128-row tile
   if (big) {
     dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
     hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb,

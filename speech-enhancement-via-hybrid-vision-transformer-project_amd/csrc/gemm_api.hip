@@ -176,6 +176,9 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
   ep.ldo = K;
   DT_DISPATCH(dt, {
     HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_wgrad: N, K alignment");
+    splits = plan_splits<T>(M, splits);
+    ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
+    ep.out = splits > 1 ? (void*)ws : (void*)dw;
     int rc = launch_gemm<T>(dense<T, false>(dy, N, N, M), dense<T, false>(x, K, K, M), N, K, M, splits, ep, st,
                             splits > 1 ? 64 : 0);
     if (rc) return rc;
@@ -276,6 +279,7 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     const int M = g->Cout, N = la.Kt, K = la.P;
     int splits = wgrad_splits(M, N, K, 32);
     if ((long long)splits * M * N > ws_elems || !ws) splits = 1;
+    splits = plan_splits<T>(K, splits);
     Epi ep;
     ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
     ep.out = splits > 1 ? (void*)ws : (void*)dw_packed;

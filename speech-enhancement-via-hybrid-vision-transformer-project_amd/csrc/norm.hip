@@ -242,16 +242,21 @@ __device__ __forceinline__ void bn_act_grad(const BnAct& a, const void* dy, int 
   int oy = y / a.pool, ox = x / a.pool;
   if (oy >= Ho || ox >= Wo) return;
   if (a.pool > 1) {
-    // first maximum in window scan order wins (torch max_pool2d)
+    // first maximum in window scan order wins (torch max_pool2d): lose to any
+    // earlier element >= me or any later element > me
+    bool before = true;
     for (int dy2 = 0; dy2 < a.pool; ++dy2)
       for (int dx2 = 0; dx2 < a.pool; ++dx2) {
         int yy = oy * a.pool + dy2, xx = ox * a.pool + dx2;
-        if (yy == y && xx == x) goto mine;
+        if (yy == y && xx == x) {
+          before = false;
+          continue;
+        }
         long zi = (((long)n * a.H + yy) * a.W + xx) * a.C + c;
-        if (bn_relu(a, ld_dt(a.z, zi, a.dt), c) >= me) return;
+        float o = bn_relu(a, ld_dt(a.z, zi, a.dt), c);
+        if (before ? (o >= me) : (o > me)) return;
       }
   }
-mine:
   g = ld_dt(dy, (((long)n * Ho + oy) * Wo + ox) * a.C + c, dy_dt) * drop2d(a, n, c);
 }
 

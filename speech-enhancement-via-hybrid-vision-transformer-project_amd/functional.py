@@ -145,10 +145,10 @@ class ConvBNActFn(torch.autograd.Function):
         invstd = torch.empty_like(mean)
         if training:
             P = N * H * W
-            nt = (P + 127) // 128
+            nt = (P + 63) // 64  # BN partials per 64-row GEMM sub-tile
             part = torch.empty((nt, Cout, 2), dtype=torch.float32, device=dev)
             call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, part.data_ptr(), None, s)
-            call("hvit_bn_finalize", part.data_ptr(), nt, 128, P, Cout, mean.data_ptr(), invstd.data_ptr(),
+            call("hvit_bn_finalize", part.data_ptr(), nt, 64, P, Cout, mean.data_ptr(), invstd.data_ptr(),
                  ptr(rmean), ptr(rvar), ptr(nbt), momentum, eps, s)
         else:
             call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, None, None, s)
