@@ -137,7 +137,9 @@ int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* m
  * invstd from hvit_bn_finalize (which also updates running stats with
  * momentum and the unbiased variance, and increments num_batches_tracked);
  * eval: hvit_bn_eval_prep.  Backward: dz from dy = grad of the pooled output;
- * sums [2][C] receives (dbeta, dgamma). */
+ * sums (hvit_bn_act_bwd_sums_elems(C) floats: [2][C] result followed by
+ * per-slot partials) receives (dbeta, dgamma) in its first 2*C entries. */
+long long hvit_bn_act_bwd_sums_elems(int C);
 int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C, float* mean,
                      float* invstd, float* running_mean, float* running_var, long long* num_batches_tracked,
                      float momentum, float eps, void* stream);

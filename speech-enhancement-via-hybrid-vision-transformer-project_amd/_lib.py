@@ -68,7 +68,8 @@ _SIGS = {
     "hvit_bn_act_fwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, vp], i32),
     "hvit_bn_act_bwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, i32, vp,
                          i32, vp, vp], i32),
-    "hvit_bilinear_fwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp], i32),
+    "hvit_bn_act_bwd_sums_elems": ([i32], i64),
+    "hvit_bilinear_fwd":([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_bilinear_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "hvit_upsample_split_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp], i32),
     "hvit_cast": ([vp, i32, vp, i32, i64, vp], i32),

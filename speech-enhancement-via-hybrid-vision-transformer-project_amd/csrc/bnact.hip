@@ -1,0 +1,341 @@
+// BatchNorm2d -> ReLU -> Dropout2d -> MaxPool2d(pool) tail of ConvBlock /
+// TransposeConvBlock (components.py:67-85, :161-178 of the reference) on NHWC
+// activations, gfx950.
+//
+// One thread owns one pooling window x 16 bytes of channels (8 bf16 / 4 f32),
+// so every z / y / dy / dz access is a coalesced 16-byte vector and the window
+// is read once.  The backward recomputes relu(bn(z)) for the window, routes the
+// pooled gradient to the first maximum in scan order (torch's max_pool2d tie
+// rule; positions outside full windows get zero), applies the per-(sample,
+// channel) dropout mask and relu', then
+//   reduce pass: sums[0][c] = sum g, sums[1][c] = sum g * xhat  (dbeta, dgamma)
+//   apply pass : dz = gamma * invstd * (g - sum g / M - xhat * sum g*xhat / M)
+// Window / pixel indices stay in 32 bits.
+#include "common.h"
+
+namespace hvit {
+
+constexpr int BN_SLOTS = 32;  // atomic spreading slots for the backward sums
+
+template <typename T>
+struct V16 {  // 16 bytes of T as floats
+  static constexpr int N = 16 / sizeof(T);
+  __device__ __forceinline__ static void load(const T* p, float* f) {
+    u32x4 u = *(const u32x4*)p;
+    const T* e = (const T*)&u;
+#pragma unroll
+    for (int i = 0; i < N; ++i) f[i] = Elem<T>::to_f(e[i]);
+  }
+  __device__ __forceinline__ static void store(T* p, const float* f) {
+    T e[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = Elem<T>::from_f(f[i]);
+    *(u32x4*)p = *(const u32x4*)e;
+  }
+};
+
+struct BnArgs {
+  int N, H, W, C, pool;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  uint32_t thr;
+  float dscale;
+  unsigned long long seed;
+  uint32_t site;
+};
+
+template <int CV>
+__device__ __forceinline__ void drop_mask(const BnArgs& a, int n, int c, float* m) {
+#pragma unroll
+  for (int e = 0; e < CV; ++e)
+    m[e] = a.thr ? (rng_keep(a.seed, a.site, (uint64_t)n * a.C + c + e, a.thr) ? a.dscale : 0.f) : 1.f;
+}
+
+// forward: y[n, oy, ox, c..] over full windows
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z, TO* __restrict__ y, BnArgs a) {
+  constexpr int CV = V16<T>::N;
+  const int G = a.C / CV;
+  const int Ho = a.H / a.pool, Wo = a.W / a.pool;
+  const int total = a.N * Ho * Wo * G;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % G;
+    int t = i / G;
+    const int ox = t % Wo;
+    t /= Wo;
+    const int oy = t % Ho;
+    const int n = t / Ho;
+    const int c = cg * CV;
+    float sc[CV], sh[CV], best[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      sc[e] = a.invstd[c + e] * a.gamma[c + e];
+      sh[e] = a.beta[c + e] - a.mean[c + e] * sc[e];
+      best[e] = 0.f;  // relu output >= 0
+    }
+    for (int dy = 0; dy < a.pool; ++dy)
+      for (int dx = 0; dx < a.pool; ++dx) {
+        float v[CV];
+        V16<T>::load(z + ((size_t)(n * a.H + oy * a.pool + dy) * a.W + ox * a.pool + dx) * a.C + c, v);
+#pragma unroll
+        for (int e = 0; e < CV; ++e) best[e] = fmaxf(best[e], v[e] * sc[e] + sh[e]);
+      }
+    float m[CV];
+    drop_mask<CV>(a, n, c, m);
+    float o[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) o[e] = best[e] * m[e];
+    TO* dst = y + ((size_t)(n * Ho + oy) * Wo + ox) * a.C + c;
+    if constexpr (sizeof(TO) == sizeof(T)) {
+      V16<TO>::store(dst, o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < CV; ++e) dst[e] = Elem<TO>::from_f(o[e]);
+    }
+  }
+}
+
+// backward: APPLY = false -> per-channel sums; APPLY = true -> dz
+template <typename T, typename TD, bool APPLY>
+__global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z, const TD* __restrict__ dy,
+                                                       BnArgs a, float* __restrict__ sums, int training,
+                                                       T* __restrict__ dz) {
+  constexpr int CV = V16<T>::N;
+  constexpr int MAXW = 4;  // pool <= 2
+  __shared__ float red[2][256][CV];
+  const int G = a.C / CV;
+  const int P = a.pool;
+  const int Ho = a.H / P, Wo = a.W / P;
+  const int Hw = (a.H + P - 1) / P, Ww = (a.W + P - 1) / P;
+  const int total = a.N * Hw * Ww * G;
+  const float invM = 1.f / (float)(a.N * a.H * a.W);
+  float acc1[CV], acc2[CV];
+#pragma unroll
+  for (int e = 0; e < CV; ++e) acc1[e] = acc2[e] = 0.f;
+  int cg_fixed = -1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % G;
+    cg_fixed = cg;
+    int t = i / G;
+    const int wx = t % Ww;
+    t /= Ww;
+    const int wy = t % Hw;
+    const int n = t / Hw;
+    const int c = cg * CV;
+    float sc[CV], sh[CV], mu[CV], is[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      mu[e] = a.mean[c + e];
+      is[e] = a.invstd[c + e];
+      sc[e] = is[e] * a.gamma[c + e];
+      sh[e] = a.beta[c + e] - mu[e] * sc[e];
+    }
+    // window values
+    float zv[MAXW][CV];
+    bool inb[MAXW];
+#pragma unroll
+    for (int q = 0; q < MAXW; ++q) {
+      const int y = wy * P + (q >> 1), x = wx * P + (q & 1);
+      inb[q] = (q < P * P) && (P == 2 || q == 0) && y < a.H && x < a.W;
+      if (inb[q]) V16<T>::load(z + ((size_t)(n * a.H + y) * a.W + x) * a.C + c, zv[q]);
+    }
+    const bool full = wy < Ho && wx < Wo;
+    float g[MAXW][CV];
+#pragma unroll
+    for (int q = 0; q < MAXW; ++q)
+#pragma unroll
+      for (int e = 0; e < CV; ++e) g[q][e] = 0.f;
+    if (full) {
+      float d[CV], m[CV];
+      const TD* dp = dy + ((size_t)(n * Ho + wy) * Wo + wx) * a.C + c;
+      if constexpr (sizeof(TD) == sizeof(T)) {
+        V16<TD>::load(dp, d);
+      } else {
+#pragma unroll
+        for (int e = 0; e < CV; ++e) d[e] = Elem<TD>::to_f(dp[e]);
+      }
+      drop_mask<CV>(a, n, c, m);
+#pragma unroll
+      for (int e = 0; e < CV; ++e) {
+        // first maximum of relu(bn(z)) over the window
+        int arg = 0;
+        float best = fmaxf(zv[0][e] * sc[e] + sh[e], 0.f);
+#pragma unroll
+        for (int q = 1; q < MAXW; ++q) {
+          if (!inb[q]) continue;
+          const float v = fmaxf(zv[q][e] * sc[e] + sh[e], 0.f);
+          if (v > best) {
+            best = v;
+            arg = q;
+          }
+        }
+        const float gv = best > 0.f ? d[e] * m[e] : 0.f;
+#pragma unroll
+        for (int q = 0; q < MAXW; ++q)
+          if (q == arg) g[q][e] = gv;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < MAXW; ++q) {
+      if (!inb[q]) continue;
+      if (!APPLY) {
+        if (full)
+#pragma unroll
+          for (int e = 0; e < CV; ++e) {
+            const float xh = (zv[q][e] - mu[e]) * is[e];
+            acc1[e] += g[q][e];
+            acc2[e] += g[q][e] * xh;
+          }
+      } else {
+        float o[CV];
+#pragma unroll
+        for (int e = 0; e < CV; ++e) {
+          const float k = sc[e];
+          if (training) {
+            const float xh = (zv[q][e] - mu[e]) * is[e];
+            o[e] = k * (g[q][e] - sums[c + e] * invM - xh * sums[a.C + c + e] * invM);
+          } else {
+            o[e] = k * g[q][e];
+          }
+        }
+        const int y = wy * P + (q >> 1), x = wx * P + (q & 1);
+        V16<T>::store(dz + ((size_t)(n * a.H + y) * a.W + x) * a.C + c, o);
+      }
+    }
+  }
+  if (!APPLY) {
+    // every thread of a block keeps one channel group (256 % G == 0 and the
+    // grid stride is a multiple of G); reduce across the block, one atomic each
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      red[0][threadIdx.x][e] = acc1[e];
+      red[1][threadIdx.x][e] = acc2[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < G) {
+      float t1[CV], t2[CV];
+#pragma unroll
+      for (int e = 0; e < CV; ++e) t1[e] = t2[e] = 0.f;
+      for (int k = threadIdx.x; k < 256; k += G)
+#pragma unroll
+        for (int e = 0; e < CV; ++e) {
+          t1[e] += red[0][k][e];
+          t2[e] += red[1][k][e];
+        }
+      // spread the per-block partials over BN_SLOTS copies so that few blocks
+      // add to the same address (same-address atomics serialise)
+      float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+      const int c = threadIdx.x * CV;
+#pragma unroll
+      for (int e = 0; e < CV; ++e) {
+        atomicAdd(slot + c + e, t1[e]);
+        atomicAdd(slot + a.C + c + e, t2[e]);
+      }
+    }
+    (void)cg_fixed;
+  }
+}
+
+// sums[0 .. 2C) = sum over the BN_SLOTS slot copies that follow it
+__global__ void bn_slots_reduce_kernel(float* sums, int n2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n2) return;
+  float s = 0.f;
+  for (int k = 1; k <= BN_SLOTS; ++k) s += sums[(size_t)k * n2 + i];
+  sums[i] = s;
+}
+
+static int grid_for(long n) {
+  long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, const hvit_dropout_t* dr, int cv) {
+  HVIT_CHECK(mean && invstd && gamma && beta, "bn_act: null statistics / affine pointer");
+  HVIT_CHECK(pool == 1 || pool == 2, "bn_act: pool must be 1 or 2");
+  HVIT_CHECK(C > 0 && C % cv == 0 && (C / cv) <= 256 && (256 % (C / cv)) == 0,
+             "bn_act: C=%d must be a multiple of %d with C/%d dividing 256", C, cv, cv);
+  HVIT_CHECK((long)N * H * W * C < (1L << 31), "bn_act: tensor too large for 32-bit indexing");
+  a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
+  a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.beta = beta;
+  a.thr = dr ? drop_threshold(dr->p) : 0;
+  a.dscale = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
+  a.seed = dr ? dr->seed : 0;
+  a.site = dr ? dr->site : 0;
+  return HVIT_OK;
+}
+
+}  // namespace hvit
+
+using namespace hvit;
+
+extern "C" int hvit_bn_act_fwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               const hvit_dropout_t* dropout2d, int pool, void* y, int y_dt, void* stream) {
+  HVIT_CHECK(z && y, "hvit_bn_act_fwd: null pointer");
+  HVIT_CHECK(aligned16(z) && aligned16(y), "hvit_bn_act_fwd: alignment");
+  BnArgs a;
+  const int cv = dt == HVIT_BF16 ? 8 : 4;
+  if (int rc = make_args(a, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d, cv)) return rc;
+  const long total = (long)N * (H / pool) * (W / pool) * (C / cv);
+  if (total <= 0) return HVIT_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(grid_for(total));
+  if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
+    hipLaunchKernelGGL((bnact_fwd_kernel<bf16_t, bf16_t>), g, dim3(256), 0, st, (const bf16_t*)z, (bf16_t*)y, a);
+  else if (dt == HVIT_BF16)
+    hipLaunchKernelGGL((bnact_fwd_kernel<bf16_t, float>), g, dim3(256), 0, st, (const bf16_t*)z, (float*)y, a);
+  else if (y_dt == HVIT_F32)
+    hipLaunchKernelGGL((bnact_fwd_kernel<float, float>), g, dim3(256), 0, st, (const float*)z, (float*)y, a);
+  else
+    hipLaunchKernelGGL((bnact_fwd_kernel<float, bf16_t>), g, dim3(256), 0, st, (const float*)z, (bf16_t*)y, a);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+template <typename T, typename TD>
+static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* sums, int training, void* dz,
+                       hipStream_t st) {
+  const int cv = 16 / sizeof(T);
+  const int P = a.pool;
+  const long total = (long)a.N * ((a.H + P - 1) / P) * ((a.W + P - 1) / P) * (a.C / cv);
+  if (total <= 0) return HVIT_OK;
+  dim3 g(grid_for(total));
+  if (training) {
+    hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, false>), g, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
+                       training, (T*)dz);
+    HVIT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(bn_slots_reduce_kernel, dim3(cdiv(2 * a.C, 256)), dim3(256), 0, st, sums, 2 * a.C);
+    HVIT_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, true>), g, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
+                     training, (T*)dz);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" long long hvit_bn_act_bwd_sums_elems(int C) { return 2LL * C * (1 + BN_SLOTS); }
+
+extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               const hvit_dropout_t* dropout2d, int pool, const void* dy, int dy_dt,
+                               int training, void* dz, int dz_dt, float* sums, void* stream) {
+  HVIT_CHECK(z && dy && dz && sums, "hvit_bn_act_bwd: null pointer");
+  HVIT_CHECK(dz_dt == dt, "hvit_bn_act_bwd: dz dtype must equal z dtype");
+  HVIT_CHECK(aligned16(z) && aligned16(dz) && aligned16(dy), "hvit_bn_act_bwd: alignment");
+  BnArgs a;
+  const int cv = dt == HVIT_BF16 ? 8 : 4;
+  if (int rc = make_args(a, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d, cv)) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * (1 + BN_SLOTS), st);
+  if (dt == HVIT_BF16)
+    return dy_dt == HVIT_BF16 ? bnact_bwd_t<bf16_t, bf16_t>(z, dy, a, sums, training, dz, st)
+                              : bnact_bwd_t<bf16_t, float>(z, dy, a, sums, training, dz, st);
+  return dy_dt == HVIT_BF16 ? bnact_bwd_t<float, bf16_t>(z, dy, a, sums, training, dz, st)
+                            : bnact_bwd_t<float, float>(z, dy, a, sums, training, dz, st);
+}

@@ -2,29 +2,41 @@
 //
 //   C[m][n] = sum_k A(m, k) * B(n, k)         (both operands "row x reduction")
 //
-// Operands are staged global -> registers -> LDS as [rows][64 bytes of k] tiles
-// (k contiguous, 16-byte row pad).  Each lane reads one 16-byte fragment per
-// 16x16 sub-tile and issues
+// Structure: 256 threads (4 waves, 2x2), BM x BN output tile, 128 bytes of K
+// per stage (64 bf16 / 32 f32), two LDS stages, register-staged global loads
+// issued one stage ahead of the MFMAs.  Per 64-byte k-step each lane feeds one
+// 16-byte fragment per 16x16 sub-tile:
 //   bf16: one  v_mfma_f32_16x16x32_bf16 (8 k per lane)
 //   f32 : four v_mfma_f32_16x16x4_f32   (4 k per lane; the k-slots of the four
 //         MFMAs are a permutation of the 16 k's, identical for A and B)
-// so both precisions share the tile/LDS/fragment code.  Loaders either read k
-// contiguously (16-byte vectors straight into the LDS row) or read the row
-// dimension contiguously and scatter-transpose into LDS (wgrad / dgrad roles).
+// Operand layouts in LDS:
+//   KC (reduction dim contiguous in memory): [rows][128 B] + 16 B pad, read
+//     with ds_read_b128;
+//   MN (rows contiguous in memory: wgrad/dgrad operands), bf16: copied as is,
+//     [k][rows] (+32 B pad, 128-B XOR swizzle on k bit 3), and read with
+//     ds_read_b64_tr_b16 (hardware transpose) -- no scalar LDS scatter;
+//   MN, f32 (parity path): scatter-transposed into the KC layout.
 // Implicit-GEMM loaders gather conv taps from NHWC activations on the fly
 // (3x3 same conv with optional nearest x2 upsample and two concatenated
-// sources; the 4x4/stride-4 patch embedding), so no im2col buffer exists.
+// sources; the 4x4/stride-4 patch embedding); each thread keeps a cursor per
+// 16-byte chunk (its pixel / tap decomposition) that advances incrementally.
 #pragma once
 #include "common.h"
 
 namespace hvit {
 
 constexpr int GEMM_THREADS = 256;
-constexpr int ROWB = 80;  // LDS row pitch in bytes (64 data + 16 pad)
+constexpr int KSTAGE = 128;          // bytes of K per stage
+constexpr int PK = KSTAGE + 16;      // LDS pitch of KC tiles (bytes)
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 // ------------------------------------------------------------ loaders --------
-// vec(a, b): KC  -> 16 bytes of elements (row a, k = b .. b+E-1)
-//            !KC -> 16 bytes of elements (rows a .. a+E-1, k = b)
+// Roles: a = row index of the operand (m for A, n for B), b = reduction index.
+// KC loaders return 16 bytes = E elements (a, b..b+E-1); MN loaders return
+// E elements (a..a+E-1, b).  init() builds a cursor for (a, b); fetch(cur)
+// reads the current chunk; step(cur, BK) moves it BK along the reduction.
 template <typename T, bool KC_>
 struct LdDense {
   static constexpr bool KC = KC_;
@@ -34,7 +46,13 @@ struct LdDense {
   int rows;    // row extent
   int K;       // reduction extent
   bool vok;    // base 16-byte aligned and ld % E == 0 (vector loads legal)
-  __device__ __forceinline__ u32x4 vec(int a, int b) const {
+  struct Cur {
+    int a, b;
+  };
+  __device__ __forceinline__ void init(Cur& c, int a, int b) const { c.a = a; c.b = b; }
+  __device__ __forceinline__ void step(Cur& c, int bk) const { c.b += bk; }
+  __device__ __forceinline__ u32x4 fetch(const Cur& c) const {
+    const int a = c.a, b = c.b;
     u32x4 r = {0u, 0u, 0u, 0u};
     if (KC) {
       if (a >= rows || b >= K) return r;
@@ -56,9 +74,11 @@ struct LdDense {
   }
 };
 
-// Implicit im2col over NHWC sources.  Row index = output pixel (n, oy, ox) of a
-// Ho x Wo grid; reduction index = (ky*KS + kx)*Ctot + c.  The conv input image
-// is concat(src1[C1], src2[C2]) upsampled (nearest) by U from Hs x Ws.
+// Implicit im2col over NHWC sources.  Pixel index p = output pixel (n, oy, ox)
+// of a Ho x Wo grid; im2col index k = (ky*KS + kx)*Ctot + c.  The conv input is
+// concat(src1[C1], src2[C2]) upsampled (nearest) by U from Hs x Ws.
+// KC (fwd / dgrad A operand): a = pixel (fixed per cursor), b = k (advances).
+// !KC (wgrad B operand):     a = k (fixed per cursor),     b = pixel (advances).
 template <typename T, bool KC_>
 struct LdConv {
   static constexpr bool KC = KC_;
@@ -71,7 +91,7 @@ struct LdConv {
   int Ho, Wo;             // output grid
   int P;                  // number of output pixels (N*Ho*Wo)
   int Kt;                 // KS*KS*Ctot
-  bool vec_ok;            // C1 % E == 0 && C2 % E == 0
+  bool vec_ok;            // C1 % E == 0 && C2 % E == 0 (16-byte gathers)
 
   __device__ __forceinline__ float elem_f(int p, int k) const {
     if (p >= P || k >= Kt) return 0.f;
@@ -86,31 +106,66 @@ struct LdConv {
     long pix = ((long)n * Hs + sy) * Ws + sx;
     return c < C1 ? Elem<T>::to_f(src1[pix * C1 + c]) : Elem<T>::to_f(src2[pix * C2 + (c - C1)]);
   }
-  // E consecutive reduction indices k..k+E-1 at pixel p
-  __device__ __forceinline__ u32x4 gather(int p, int k) const {
+
+  // cursor: pixel part (n, oy, ox) and tap part (ky, kx, c) of (p, k)
+  struct Cur {
+    int p, k;       // current pixel / im2col index (scalar-path fallback)
+    int n, oy, ox;  // decomposition of p
+    int c, kx, ky;  // decomposition of k
+  };
+  __device__ __forceinline__ void init(Cur& cu, int a, int b) const {
+    const int p = KC ? a : b, k = KC ? b : a;
+    cu.p = p;
+    cu.k = k;
+    const int hw = Ho * Wo;
+    cu.n = p / hw;
+    const int rem = p - cu.n * hw;
+    cu.oy = rem / Wo;
+    cu.ox = rem - cu.oy * Wo;
+    const int tap = k / Ctot;
+    cu.c = k - tap * Ctot;
+    cu.ky = tap / KS;
+    cu.kx = tap - cu.ky * KS;
+  }
+  __device__ __forceinline__ void step(Cur& cu, int bk) const {
+    if (KC) {  // advance k
+      cu.k += bk;
+      cu.c += bk;
+      while (cu.c >= Ctot) {
+        cu.c -= Ctot;
+        if (++cu.kx == KS) {
+          cu.kx = 0;
+          ++cu.ky;
+        }
+      }
+    } else {  // advance pixel
+      cu.p += bk;
+      cu.ox += bk;
+      while (cu.ox >= Wo) {
+        cu.ox -= Wo;
+        if (++cu.oy == Ho) {
+          cu.oy = 0;
+          ++cu.n;
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ u32x4 fetch(const Cur& cu) const {
     u32x4 r = {0u, 0u, 0u, 0u};
     if (vec_ok) {
-      if (p >= P || k >= Kt) return r;
-      int hw = Ho * Wo;
-      int n = p / hw, rem = p - n * hw;
-      int oy = rem / Wo, ox = rem - oy * Wo;
-      int tap = k / Ctot, c = k - tap * Ctot;
-      int ky = tap / KS, kx = tap - ky * KS;
-      int iy = oy * S - Pd + ky, ix = ox * S - Pd + kx;
+      if (cu.p >= P || cu.k >= Kt) return r;
+      const int iy = cu.oy * S - Pd + cu.ky, ix = cu.ox * S - Pd + cu.kx;
       if (iy < 0 || ix < 0 || iy >= Hi || ix >= Wi) return r;
-      int sy = iy / U, sx = ix / U;
-      long pix = ((long)n * Hs + sy) * Ws + sx;
-      const T* q = c < C1 ? src1 + pix * C1 + c : src2 + pix * C2 + (c - C1);
+      const int sy = U == 2 ? (iy >> 1) : iy, sx = U == 2 ? (ix >> 1) : ix;
+      const long pix = ((long)cu.n * Hs + sy) * Ws + sx;
+      const T* q = cu.c < C1 ? src1 + pix * C1 + cu.c : src2 + pix * C2 + (cu.c - C1);
       return *(const u32x4*)q;
     }
     T tmp[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) tmp[e] = Elem<T>::from_f(elem_f(p, k + e));
+    for (int e = 0; e < E; ++e)
+      tmp[e] = Elem<T>::from_f(KC ? elem_f(cu.p, cu.k + e) : elem_f(cu.p, cu.k + e));
     return *(u32x4*)tmp;
-  }
-  // role A (KC): a = pixel, b = k.   role B (!KC, wgrad): a = im2col k, b = pixel
-  __device__ __forceinline__ u32x4 vec(int a, int b) const {
-    return KC ? gather(a, b) : gather(b, a);
   }
 };
 
@@ -257,24 +312,91 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, 
   }
 }
 
+// k-major ("MN") bf16 tile: element (k, r) at k*PM + swizzled byte column.
+// The 128-byte XOR on k bit 3 (tiles with >= 128 rows) puts the two 16-lane
+// groups of a transposed read on disjoint bank halves.
+template <int R>
+struct MnTile {
+  static constexpr int PM = R * 2 + 32;
+  __device__ __forceinline__ static int off(int k, int colbyte) {
+    return k * PM + (R >= 128 ? (colbyte ^ (((k >> 3) & 1) << 7)) : colbyte);
+  }
+};
+
+// 16x16x32 bf16 operand fragment from a k-major tile via two transposed reads:
+// lane (g = l>>4, i = l&15) receives rows rb+i, k = 32s + 8g + 0..7.
+template <int R>
+__device__ __forceinline__ u32x4 frag_tr(const char* tile, int rb, int s, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int k0 = 32 * s + 8 * g + q;
+  const int cb = (rb + 4 * p) * 2;
+  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + MnTile<R>::off(k0, cb)));
+  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + MnTile<R>::off(k0 + 4, cb)));
+  u32x4 r;
+  r[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+  r[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+  r[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+  r[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+  return r;
+}
+
+template <typename T, int R, bool KC>
+struct TileCfg {
+  static constexpr int E = Elem<T>::PER16;
+  static constexpr int BK = KSTAGE / sizeof(T);
+  static constexpr bool TR = !KC && sizeof(T) == 2;
+  static constexpr int BYTES = TR ? BK * MnTile<R>::PM : R * PK;  // per stage
+  static constexpr int CH = R * KSTAGE / 16 / GEMM_THREADS;        // chunks per thread
+  // chunk ch -> (row, k) offsets within the stage
+  __device__ __forceinline__ static void map(int ch, int& row, int& k) {
+    if (KC) {
+      row = ch / (KSTAGE / 16);
+      k = (ch % (KSTAGE / 16)) * E;
+    } else {
+      k = ch / (R / E);
+      row = (ch % (R / E)) * E;
+    }
+  }
+  __device__ __forceinline__ static void store(char* tile, int ch, const u32x4& v) {
+    int row, k;
+    map(ch, row, k);
+    if (KC) {
+      *(u32x4*)(tile + row * PK + (k / E) * 16) = v;
+    } else if (TR) {
+      *(u32x4*)(tile + MnTile<R>::off(k, row * 2)) = v;
+    } else {  // f32 scatter-transpose
+      const T* e = (const T*)&v;
+#pragma unroll
+      for (int i = 0; i < E; ++i) *(T*)(tile + (row + i) * PK + k * sizeof(T)) = e[i];
+    }
+  }
+  __device__ __forceinline__ static u32x4 frag(const char* tile, int rb, int s, int lane) {
+    if constexpr (TR) {
+      return frag_tr<R>(tile, rb, s, lane);
+    } else {
+      return *(const u32x4*)(tile + (rb + (lane & 15)) * PK + (4 * s + (lane >> 4)) * 16);
+    }
+  }
+};
+
 template <typename T, int BM, int BN, class LA, class LB>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M, int N, int K,
-                                                            int kps, Epi ep) {
-  constexpr int E = Elem<T>::PER16;
-  constexpr int BK = 64 / sizeof(T);
+__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_kernel(LA la, LB lb, int M, int N, int K,
+                                                               int kps, Epi ep) {
+  using TA = TileCfg<T, BM, LA::KC>;
+  using TB = TileCfg<T, BN, LB::KC>;
+  constexpr int BK = TA::BK;
   constexpr int WM = 2, WN = 2;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int CA = BM * 4 / GEMM_THREADS;  // 16-byte chunks per thread
-  constexpr int CB = BN * 4 / GEMM_THREADS;
+  constexpr int CA = TA::CH, CB = TB::CH;
+  constexpr int STEPS = KSTAGE / 64;
   static_assert(CA >= 1 && CB >= 1, "tile too small");
 
-  // main loop: 2 stages of A/B tiles; epilogue: a 64-row f32 tile + reduction rows
-  constexpr int SM_LOOP = 2 * (BM + BN) * ROWB;
+  constexpr int SM_LOOP = 2 * (TA::BYTES + TB::BYTES);
   constexpr int SM_EPI = (64 * (BN + 4) + (GEMM_THREADS / (BN / 4)) * BN) * 4;
   __shared__ __attribute__((aligned(16))) char smem[SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI];
   char* As = smem;
-  char* Bs = smem + 2 * BM * ROWB;
+  char* Bs = smem + 2 * TA::BYTES;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -292,65 +414,43 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  typename LA::Cur ca[CA];
+  typename LB::Cur cb[CB];
+  int kofa[CA], kofb[CB];
+#pragma unroll
+  for (int c = 0; c < CA; ++c) {
+    int row, k;
+    TA::map(tid + c * GEMM_THREADS, row, k);
+    kofa[c] = k;
+    la.init(ca[c], m0 + row, kbeg + k);
+  }
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    int row, k;
+    TB::map(tid + c * GEMM_THREADS, row, k);
+    kofb[c] = k;
+    lb.init(cb[c], n0 + row, kbeg + k);
+  }
   u32x4 ra[CA], rb[CB];
-
   auto fetch = [&](int k0) {
 #pragma unroll
-    for (int c = 0; c < CA; ++c) {
-      int ch = tid + c * GEMM_THREADS;
-      if (LA::KC) {
-        int r = ch >> 2, kc = ch & 3;
-        int kk = k0 + kc * E;
-        ra[c] = (kk < kend) ? la.vec(m0 + r, kk) : (u32x4){0u, 0u, 0u, 0u};
-      } else {
-        int kr = ch / (BM / E), mc = ch % (BM / E);
-        int kk = k0 + kr;
-        ra[c] = (kk < kend) ? la.vec(m0 + mc * E, kk) : (u32x4){0u, 0u, 0u, 0u};
-      }
-    }
+    for (int c = 0; c < CA; ++c)
+      ra[c] = (k0 + kofa[c] < kend) ? la.fetch(ca[c]) : (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      int ch = tid + c * GEMM_THREADS;
-      if (LB::KC) {
-        int r = ch >> 2, kc = ch & 3;
-        int kk = k0 + kc * E;
-        rb[c] = (kk < kend) ? lb.vec(n0 + r, kk) : (u32x4){0u, 0u, 0u, 0u};
-      } else {
-        int kr = ch / (BN / E), nc = ch % (BN / E);
-        int kk = k0 + kr;
-        rb[c] = (kk < kend) ? lb.vec(n0 + nc * E, kk) : (u32x4){0u, 0u, 0u, 0u};
-      }
-    }
+    for (int c = 0; c < CB; ++c)
+      rb[c] = (k0 + kofb[c] < kend) ? lb.fetch(cb[c]) : (u32x4){0u, 0u, 0u, 0u};
+  };
+  auto advance = [&]() {
+#pragma unroll
+    for (int c = 0; c < CA; ++c) la.step(ca[c], BK);
+#pragma unroll
+    for (int c = 0; c < CB; ++c) lb.step(cb[c], BK);
   };
   auto stash = [&](int buf) {
-    char* a = As + buf * BM * ROWB;
-    char* b = Bs + buf * BN * ROWB;
 #pragma unroll
-    for (int c = 0; c < CA; ++c) {
-      int ch = tid + c * GEMM_THREADS;
-      if (LA::KC) {
-        int r = ch >> 2, kc = ch & 3;
-        *(u32x4*)(a + r * ROWB + kc * 16) = ra[c];
-      } else {
-        int kr = ch / (BM / E), mc = ch % (BM / E);
-        const T* v = (const T*)&ra[c];
+    for (int c = 0; c < CA; ++c) TA::store(As + buf * TA::BYTES, tid + c * GEMM_THREADS, ra[c]);
 #pragma unroll
-        for (int e = 0; e < E; ++e) *(T*)(a + (mc * E + e) * ROWB + kr * sizeof(T)) = v[e];
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      int ch = tid + c * GEMM_THREADS;
-      if (LB::KC) {
-        int r = ch >> 2, kc = ch & 3;
-        *(u32x4*)(b + r * ROWB + kc * 16) = rb[c];
-      } else {
-        int kr = ch / (BN / E), nc = ch % (BN / E);
-        const T* v = (const T*)&rb[c];
-#pragma unroll
-        for (int e = 0; e < E; ++e) *(T*)(b + (nc * E + e) * ROWB + kr * sizeof(T)) = v[e];
-      }
-    }
+    for (int c = 0; c < CB; ++c) TB::store(Bs + buf * TB::BYTES, tid + c * GEMM_THREADS, rb[c]);
   };
 
   if (nk > 0) {
@@ -361,33 +461,41 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M,
   const int frow = lane & 15, fq = lane >> 4;
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
-    if (t + 1 < nk) fetch(kbeg + (t + 1) * BK);
-    const char* a = As + buf * BM * ROWB + (wm * WTM + frow) * ROWB + fq * 16;
-    const char* b = Bs + buf * BN * ROWB + (wn * WTN + frow) * ROWB + fq * 16;
-    u32x4 fa[FM], fb[FN];
+    if (t + 1 < nk) {
+      advance();
+      fetch(kbeg + (t + 1) * BK);
+    }
+    const char* at = As + buf * TA::BYTES;
+    const char* bt = Bs + buf * TB::BYTES;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) fa[i] = *(const u32x4*)(a + i * 16 * ROWB);
+    for (int s = 0; s < STEPS; ++s) {
+      u32x4 fa[FM], fb[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j] = *(const u32x4*)(b + j * 16 * ROWB);
+      for (int i = 0; i < FM; ++i) fa[i] = TA::frag(at, wm * WTM + i * 16, s, lane);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j) fb[j] = TB::frag(bt, wn * WTN + j * 16, s, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if constexpr (sizeof(T) == 2) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(s16x8, fa[i]), __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
-        } else {
-          f32x4 va = __builtin_bit_cast(f32x4, fa[i]);
-          f32x4 vb = __builtin_bit_cast(f32x4, fb[j]);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[0], vb[0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[1], vb[1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[2], vb[2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[3], vb[3], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (sizeof(T) == 2) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(s16x8, fa[i]), __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+          } else {
+            f32x4 va = __builtin_bit_cast(f32x4, fa[i]);
+            f32x4 vb = __builtin_bit_cast(f32x4, fb[j]);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[0], vb[0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[1], vb[1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[2], vb[2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[3], vb[3], acc[i][j], 0, 0, 0);
+          }
         }
-      }
+    }
     if (t + 1 < nk) stash(buf ^ 1);
     __syncthreads();
   }
+  (void)frow;
+  (void)fq;
 
   // ------------------------------------------------------------- epilogue ---
   // The accumulator tile is staged through LDS in 64-row halves (f32, padded
@@ -493,6 +601,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_kernel(LA la, LB lb, int M,
       }
   }
 }
+
 
 
 // host-side launcher --------------------------------------------------------

@@ -108,7 +108,27 @@ int check_geom(const hvit_conv_geom_t* g) {
   return HVIT_OK;
 }
 
+// thin-channel stencil kernels (thinconv.hip)
+bool thin_c1(const hvit_conv_geom_t* g) {
+  return g->C1 == 1 && g->C2 == 0 && g->U == 1 && g->KS == 3 && g->stride == 1 && g->pad == 1 &&
+         g->Cout % 8 == 0 && g->Cout <= 256 && 256 % g->Cout == 0;
+}
+bool thin_o1(const hvit_conv_geom_t* g) {
+  return g->Cout == 1 && g->C2 == 0 && g->KS == 3 && g->stride == 1 && g->pad == 1 && g->C1 % 8 == 0 &&
+         g->C1 / 8 <= 64 && 64 % (g->C1 / 8) == 0 && aligned16(g->src1);
+}
+
 }  // namespace
+
+int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats, hipStream_t st);
+long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g);
+int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
+                       hipStream_t st);
+int hvit_thin_o1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, int act_tanh, hipStream_t st);
+int hvit_thin_o1_dgrad(int dt, const hvit_conv_geom_t* g, const void* dz, const void* w, void* du, hipStream_t st);
+long long hvit_thin_o1_wgrad_ws(const hvit_conv_geom_t* g);
+int hvit_thin_o1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
+                       hipStream_t st);
 
 #define DT_DISPATCH(dt, ...)                   \
   if ((dt) == HVIT_BF16) {                     \
@@ -196,6 +216,11 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
              "hvit_conv_fwd: act must be NONE or TANH");
   HVIT_CHECK(!epi || !epi->resid, "hvit_conv_fwd: residual epilogue unsupported");
   HVIT_CHECK(aligned16(w_packed), "hvit_conv_fwd: weight alignment");
+  const bool plain_epi = !epi || (epi->dropout.p == 0.f && !epi->rowadd && !epi->colsum);
+  if (thin_c1(g) && plain_epi && !bias && (!epi || epi->act == HVIT_ACT_NONE) && aligned16(y))
+    return hvit_thin_c1_fwd(dt, g, w_packed, y, y_dt, bn_partials, (hipStream_t)stream);
+  if (thin_o1(g) && plain_epi && !bias && !bn_partials)
+    return hvit_thin_o1_fwd(dt, g, w_packed, y, y_dt, epi && epi->act == HVIT_ACT_TANH, (hipStream_t)stream);
   Epi ep = to_epi(epi, y, y_dt, g->Cout);
   ep.bias = bias;
   ep.stats = bn_partials;
@@ -243,6 +268,7 @@ extern "C" int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     });
   }
   HVIT_CHECK(g->stride == 1 && g->pad == g->KS / 2 && (g->KS & 1), "hvit_conv_dgrad: only odd same-convs");
+  if (thin_o1(g) && dx_dt == dt && aligned16(dx)) return hvit_thin_o1_dgrad(dt, g, dy, w, dx, st);
   Epi ep;
   ep.out = dx;
   ep.out_dt = dx_dt;
@@ -257,6 +283,8 @@ extern "C" int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy
 
 extern "C" long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g) {
   if (!g) return 0;
+  if (thin_c1(g)) return hvit_thin_c1_wgrad_ws(g);
+  if (thin_o1(g)) return hvit_thin_o1_wgrad_ws(g);
   const int Hi = g->Hs * g->U, Wi = g->Ws * g->U;
   const long Ho = (Hi + 2 * g->pad - g->KS) / g->stride + 1;
   const long Wo = (Wi + 2 * g->pad - g->KS) / g->stride + 1;
@@ -271,6 +299,8 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
   HVIT_CHECK(dy && dw_packed, "hvit_conv_wgrad: null pointer");
   HVIT_CHECK(aligned16(dy), "hvit_conv_wgrad: alignment");
   hipStream_t st = (hipStream_t)stream;
+  if (thin_c1(g)) return hvit_thin_c1_wgrad(dt, g, dy, dw_packed, ws, ws_elems, st);
+  if (thin_o1(g)) return hvit_thin_o1_wgrad(dt, g, dy, dw_packed, ws, ws_elems, st);
   DT_DISPATCH(dt, {
     auto la = conv_a<T>(g, g->src1, g->C1, g->src2, g->C2, g->Hs, g->Ws, g->U, g->KS, g->stride, g->pad);
     LdConv<T, false> lb;

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 }
 
 // rows per workgroup for the backward (4 waves x 16 rows)
-constexpr int LNB_ROWS = 64;
+constexpr int LNB_ROWS = 16;
 
 template <typename TD, int MAXV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, const float* __restrict__ x,
@@ -185,125 +185,6 @@ __global__ void bn_eval_prep_kernel(const float* rmean, const float* rvar, int C
   }
 }
 
-struct BnAct {
-  const void* z; int dt;      // pre-BN conv output, NHWC [N, H, W, C]
-  int N, H, W, C, pool;       // pool: 1 or 2
-  const float* mean; const float* invstd; const float* gamma; const float* beta;
-  uint32_t thr; float dscale; unsigned long long seed; uint32_t site;  // dropout2d
-};
-
-__device__ __forceinline__ float bn_relu(const BnAct& a, float z, int c) {
-  float v = (z - a.mean[c]) * a.invstd[c] * a.gamma[c] + a.beta[c];
-  return v > 0.f ? v : 0.f;
-}
-__device__ __forceinline__ float drop2d(const BnAct& a, int n, int c) {
-  if (!a.thr) return 1.f;
-  return rng_keep(a.seed, a.site, (uint64_t)n * a.C + c, a.thr) ? a.dscale : 0.f;
-}
-
-// y[n, oy, ox, c] = max over window of drop2d(relu(bn(z)))
-__global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnAct a, void* y, int y_dt) {
-  int Ho = a.H / a.pool, Wo = a.W / a.pool;
-  long total = (long)a.N * Ho * Wo * a.C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = i % a.C;
-    long p = i / a.C;
-    int ox = p % Wo;
-    long t = p / Wo;
-    int oy = t % Ho;
-    int n = t / Ho;
-    float best = -INFINITY;
-    for (int dy = 0; dy < a.pool; ++dy)
-      for (int dx = 0; dx < a.pool; ++dx) {
-        long zi = (((long)n * a.H + oy * a.pool + dy) * a.W + ox * a.pool + dx) * a.C + c;
-        float v = bn_relu(a, ld_dt(a.z, zi, a.dt), c);
-        best = fmaxf(best, v);
-      }
-    st_dt(y, i, best * drop2d(a, n, c), y_dt);
-  }
-}
-
-// gradient wrt the pre-BN activation's BN output (g) at full-res element i,
-// and xhat; dy is the gradient of the pooled block output.
-__device__ __forceinline__ void bn_act_grad(const BnAct& a, const void* dy, int dy_dt, long i, float& g,
-                                            float& xhat) {
-  int c = i % a.C;
-  long p = i / a.C;
-  int x = p % a.W;
-  long t = p / a.W;
-  int y = t % a.H;
-  int n = t / a.H;
-  float z = ld_dt(a.z, i, a.dt);
-  xhat = (z - a.mean[c]) * a.invstd[c];
-  g = 0.f;
-  float me = bn_relu(a, z, c);
-  if (me <= 0.f) return;  // relu'(0) = 0
-  int Ho = a.H / a.pool, Wo = a.W / a.pool;
-  int oy = y / a.pool, ox = x / a.pool;
-  if (oy >= Ho || ox >= Wo) return;
-  if (a.pool > 1) {
-    // first maximum in window scan order wins (torch max_pool2d): lose to any
-    // earlier element >= me or any later element > me
-    bool before = true;
-    for (int dy2 = 0; dy2 < a.pool; ++dy2)
-      for (int dx2 = 0; dx2 < a.pool; ++dx2) {
-        int yy = oy * a.pool + dy2, xx = ox * a.pool + dx2;
-        if (yy == y && xx == x) {
-          before = false;
-          continue;
-        }
-        long zi = (((long)n * a.H + yy) * a.W + xx) * a.C + c;
-        float o = bn_relu(a, ld_dt(a.z, zi, a.dt), c);
-        if (before ? (o >= me) : (o > me)) return;
-      }
-  }
-  g = ld_dt(dy, (((long)n * Ho + oy) * Wo + ox) * a.C + c, dy_dt) * drop2d(a, n, c);
-}
-
-// sums[0][c] = sum g ; sums[1][c] = sum g*xhat   (atomic, caller zeroes)
-__global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnAct a, const void* dy, int dy_dt,
-                                                               float* __restrict__ sums) {
-  __shared__ float s1[256], s2[256];
-  long total = (long)a.N * a.H * a.W * a.C;
-  // each thread keeps a fixed channel: stride is a multiple of C
-  int per = 256 / a.C;  // pixels per block-iteration (C <= 256, power of two)
-  int c = threadIdx.x % a.C;
-  int pofs = threadIdx.x / a.C;
-  float acc1 = 0.f, acc2 = 0.f;
-  if (pofs < per) {
-    long npix = total / a.C;
-    for (long p = (long)blockIdx.x * per + pofs; p < npix; p += (long)gridDim.x * per) {
-      float g, xh;
-      bn_act_grad(a, dy, dy_dt, p * a.C + c, g, xh);
-      acc1 += g;
-      acc2 += g * xh;
-    }
-  }
-  s1[threadIdx.x] = acc1;
-  s2[threadIdx.x] = acc2;
-  __syncthreads();
-  if (threadIdx.x < a.C) {
-    float t1 = 0.f, t2 = 0.f;
-    for (int k = threadIdx.x; k < per * a.C; k += a.C) { t1 += s1[k]; t2 += s2[k]; }
-    atomicAdd(sums + threadIdx.x, t1);
-    atomicAdd(sums + a.C + threadIdx.x, t2);
-  }
-}
-
-__global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnAct a, const void* dy, int dy_dt,
-                                                              const float* __restrict__ sums, int training,
-                                                              void* dz, int dz_dt) {
-  long total = (long)a.N * a.H * a.W * a.C;
-  float invM = 1.f / (float)(total / a.C);
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = i % a.C;
-    float g, xh;
-    bn_act_grad(a, dy, dy_dt, i, g, xh);
-    float k = a.gamma[c] * a.invstd[c];
-    float v = training ? k * (g - sums[c] * invM - xh * sums[a.C + c] * invM) : k * g;
-    st_dt(dz, i, v, dz_dt);
-  }
-}
 
 static int grid_for(long n) {
   long g = (n + 255) / 256;
@@ -373,54 +254,3 @@ extern "C" int hvit_bn_eval_prep(const float* running_mean, const float* running
   return HVIT_OK;
 }
 
-static int make_bnact(BnAct& a, int dt, const void* z, int N, int H, int W, int C, int pool,
-                      const float* mean, const float* invstd, const float* gamma, const float* beta,
-                      const hvit_dropout_t* dr) {
-  HVIT_CHECK(z && mean && invstd && gamma && beta, "bn_act: null pointer");
-  HVIT_CHECK(pool == 1 || pool == 2, "bn_act: pool must be 1 or 2");
-  HVIT_CHECK(C > 0 && C <= 256 && (C & (C - 1)) == 0, "bn_act: C=%d must be a power of two <= 256", C);
-  a.z = z; a.dt = dt; a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
-  a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.beta = beta;
-  a.thr = dr ? drop_threshold(dr->p) : 0;
-  a.dscale = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-  a.seed = dr ? dr->seed : 0;
-  a.site = dr ? dr->site : 0;
-  return HVIT_OK;
-}
-
-extern "C" int hvit_bn_act_fwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
-                               const float* invstd, const float* gamma, const float* beta,
-                               const hvit_dropout_t* dropout2d, int pool, void* y, int y_dt, void* stream) {
-  BnAct a;
-  int rc = make_bnact(a, dt, z, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d);
-  if (rc) return rc;
-  HVIT_CHECK(y, "hvit_bn_act_fwd: null y");
-  long total = (long)N * (H / pool) * (W / pool) * C;
-  if (total <= 0) return HVIT_OK;
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a, y, y_dt);
-  HVIT_LAUNCH_CHECK();
-  return HVIT_OK;
-}
-
-extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
-                               const float* invstd, const float* gamma, const float* beta,
-                               const hvit_dropout_t* dropout2d, int pool, const void* dy, int dy_dt,
-                               int training, void* dz, int dz_dt, float* sums, void* stream) {
-  BnAct a;
-  int rc = make_bnact(a, dt, z, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d);
-  if (rc) return rc;
-  HVIT_CHECK(dy && dz && sums, "hvit_bn_act_bwd: null pointer");
-  hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st);
-  long total = (long)N * H * W * C;
-  if (total <= 0) return HVIT_OK;
-  long npix = total / C;
-  int per = 256 / C;
-  hipLaunchKernelGGL(bn_act_bwd_reduce_kernel, dim3(grid_for(npix * 256 / per / 16 + 1)), dim3(256), 0, st, a,
-                     dy, dy_dt, sums);
-  HVIT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_act_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, st, a, dy, dy_dt,
-                     (const float*)sums, training, dz, dz_dt);
-  HVIT_LAUNCH_CHECK();
-  return HVIT_OK;
-}

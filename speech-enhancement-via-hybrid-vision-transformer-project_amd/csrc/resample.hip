@@ -32,16 +32,16 @@ __device__ __forceinline__ LinIdx lin_idx(int o, int in, float scale) {
 __global__ __launch_bounds__(256) void bilinear_fwd_kernel(const void* x, int x_dt, void* y, int y_dt, int N,
                                                           int Hi, int Wi, int C, int Ho, int Wo, float sh,
                                                           float sw) {
-  long total = (long)N * Ho * Wo * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = i % C;
-    long p = i / C;
-    int ox = p % Wo;
-    long t = p / Wo;
-    int oy = t % Ho;
-    int n = t / Ho;
+  const int total = N * Ho * Wo * C;  // < 2^31 (checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % C;
+    const int p = i / C;
+    const int ox = p % Wo;
+    const int t = p / Wo;
+    const int oy = t % Ho;
+    const int n = t / Ho;
     LinIdx ly = lin_idx(oy, Hi, sh), lx = lin_idx(ox, Wi, sw);
-    long b = (long)n * Hi;
+    const int b = n * Hi;
     float v00 = ld_dt(x, ((b + ly.i0) * Wi + lx.i0) * C + c, x_dt);
     float v01 = ld_dt(x, ((b + ly.i0) * Wi + lx.i1) * C + c, x_dt);
     float v10 = ld_dt(x, ((b + ly.i1) * Wi + lx.i0) * C + c, x_dt);
@@ -71,26 +71,26 @@ __device__ __forceinline__ void out_range(int i, int in, int out, float scale, i
 __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const void* dy, int dy_dt, void* dx, int dx_dt, int N,
                                                           int Hi, int Wi, int C, int Ho, int Wo, float sh,
                                                           float sw, int accumulate) {
-  long total = (long)N * Hi * Wi * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = i % C;
-    long p = i / C;
-    int ix = p % Wi;
-    long t = p / Wi;
-    int iy = t % Hi;
-    int n = t / Hi;
+  const int total = N * Hi * Wi * C;  // < 2^31 (checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % C;
+    const int p = i / C;
+    const int ix = p % Wi;
+    const int t = p / Wi;
+    const int iy = t % Hi;
+    const int n = t / Hi;
     int ylo, yhi, xlo, xhi;
     out_range(iy, Hi, Ho, sh, ylo, yhi);
     out_range(ix, Wi, Wo, sw, xlo, xhi);
     float acc = 0.f;
     for (int oy = ylo; oy <= yhi; ++oy) {
-      float wy = lin_w(oy, iy, Hi, sh);
+      const float wy = lin_w(oy, iy, Hi, sh);
       if (wy == 0.f) continue;
       float row = 0.f;
+      const int base = (n * Ho + oy) * Wo;
       for (int ox = xlo; ox <= xhi; ++ox) {
-        float wx = lin_w(ox, ix, Wi, sw);
-        if (wx == 0.f) continue;
-        row += wx * ld_dt(dy, (((long)n * Ho + oy) * Wo + ox) * C + c, dy_dt);
+        const float wx = lin_w(ox, ix, Wi, sw);
+        if (wx != 0.f) row += wx * ld_dt(dy, (base + ox) * C + c, dy_dt);
       }
       acc += wy * row;
     }
@@ -103,19 +103,19 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const void* dy, int d
 __global__ __launch_bounds__(256) void up_split_bwd_kernel(const void* du, int du_dt, int N, int H, int W, int U,
                                                           int C1, int C2, void* dx1, int dx1_dt, void* dx2,
                                                           int dx2_dt) {
-  int Ct = C1 + C2;
-  long total = (long)N * H * W * Ct;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = i % Ct;
-    long p = i / Ct;
-    int x = p % W;
-    long t = p / W;
-    int y = t % H;
-    int n = t / H;
+  const int Ct = C1 + C2;
+  const int total = N * H * W * Ct;  // < 2^31 (checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % Ct;
+    const int p = i / Ct;
+    const int x = p % W;
+    const int t = p / W;
+    const int y = t % H;
+    const int n = t / H;
     float s = 0.f;
     for (int a = 0; a < U; ++a)
       for (int b = 0; b < U; ++b)
-        s += ld_dt(du, (((long)n * H * U + y * U + a) * (W * U) + x * U + b) * Ct + c, du_dt);
+        s += ld_dt(du, ((long)((n * H + y) * U + a) * (W * U) + x * U + b) * Ct + c, du_dt);
     if (c < C1) st_dt(dx1, p * C1 + c, s, dx1_dt);
     else st_dt(dx2, p * C2 + (c - C1), s, dx2_dt);
   }
@@ -138,6 +138,7 @@ extern "C" int hvit_bilinear_fwd(const void* x, int x_dt, int N, int Hi, int Wi,
   HVIT_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0, "hvit_bilinear_fwd: bad sizes");
   long total = (long)N * Ho * Wo * C;
   if (total <= 0) return HVIT_OK;
+  HVIT_CHECK(total < (1L << 31) && (long)N * Hi * Wi * C < (1L << 31), "resample: tensor too large");
   float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
   hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, x_dt,
                      y, y_dt, N, Hi, Wi, C, Ho, Wo, sh, sw);
@@ -151,6 +152,7 @@ extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int W
   HVIT_CHECK(Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0, "hvit_bilinear_bwd: bad sizes");
   long total = (long)N * Hi * Wi * C;
   if (total <= 0) return HVIT_OK;
+  HVIT_CHECK(total < (1L << 31) && (long)N * Ho * Wo * C < (1L << 31), "resample: tensor too large");
   float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
   hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dy, dy_dt,
                      dx, dx_dt, N, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
@@ -164,6 +166,7 @@ extern "C" int hvit_upsample_split_bwd(const void* du, int du_dt, int N, int H, 
   HVIT_CHECK(U >= 1 && C1 > 0 && C2 >= 0, "hvit_upsample_split_bwd: bad sizes");
   long total = (long)N * H * W * (C1 + C2);
   if (total <= 0) return HVIT_OK;
+  HVIT_CHECK(total * U * U < (1L << 31), "resample: tensor too large");
   hipLaunchKernelGGL(up_split_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, du, du_dt,
                      N, H, W, U, C1, C2, dx1, dx1_dt, dx2, dx2_dt);
   HVIT_LAUNCH_CHECK();

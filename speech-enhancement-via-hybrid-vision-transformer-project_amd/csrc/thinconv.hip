@@ -1,0 +1,390 @@
+// Thin-channel 3x3 convolutions (gfx950) where an MFMA tile would be mostly
+// padding:
+//   * Cin = 1  : the first encoder conv (ConvBlock 0, components.py:55-62) on
+//                the magnitude spectrogram -- fwd with fused BatchNorm partials,
+//                and wgrad (a 2M-pixel reduction into 9*Cout weights);
+//   * Cout = 1 : the final decoder conv + tanh (TransposeConvBlock final,
+//                components.py:149-167) -- fwd, dgrad and wgrad.
+// All are HBM-bound stencils on NHWC data: 16-byte channel vectors, one pass
+// over the large tensor, weights in LDS.  Called from the hvit_conv_* entry
+// points when the geometry matches (3x3, stride 1, pad 1).
+#include <algorithm>
+
+#include "common.h"
+
+namespace hvit {
+
+template <typename T>
+struct Vec8 {  // 8 consecutive elements as floats (16 B for bf16, 32 B for f32)
+  __device__ __forceinline__ static void load(const T* p, float* f) {
+    if constexpr (sizeof(T) == 2) {
+      u32x4 u = *(const u32x4*)p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[2 * i] = __uint_as_float(u[i] << 16);
+        f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+      }
+    } else {
+      f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[i] = a[i];
+        f[4 + i] = b[i];
+      }
+    }
+  }
+  __device__ __forceinline__ static void store(T* p, const float* f) {
+    if constexpr (sizeof(T) == 2) {
+      u32x4 u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+      *(u32x4*)p = u;
+    } else {
+      *(f32x4*)p = (f32x4){f[0], f[1], f[2], f[3]};
+      *(f32x4*)(p + 4) = (f32x4){f[4], f[5], f[6], f[7]};
+    }
+  }
+};
+
+constexpr int TC_PIX = 64;   // pixels per stats tile (= BN partial tile rows)
+constexpr int TC_TILES = 4;  // tiles per block
+
+// ---------------------------------------------------------------- Cin = 1 ---
+// z[p][co] = sum_tap x[p + tap] * w[co][tap]; BN partials per 64-pixel tile.
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, TO* __restrict__ z,
+                                                     float* __restrict__ stats, int N, int H, int W, int Cout) {
+  // Each thread owns one 8-channel group cc (fixed: 256 % CC == 0) with its 72
+  // weights in registers and walks TC_TILES 64-pixel tiles; per tile the
+  // values go through an LDS tile for the (mean, M2) BN partials, reduced by
+  // all 256 threads.
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int CP = Cout + 1;
+  float* tile = sm;               // [64][Cout + 1]
+  float* red = sm + TC_PIX * CP;  // [256]
+  const int CC = Cout / 8;
+  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC, lanes = 256 / CC;
+  float wr[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wr[t][e] = Elem<T>::to_f(w[(cc * 8 + e) * 9 + t]);
+  const int P = N * H * W;
+  const int HW = H * W;
+  const int c_red = threadIdx.x % Cout, rg = threadIdx.x / Cout, groups = 256 / Cout;
+  for (int tt = 0; tt < TC_TILES; ++tt) {
+    const int tile_id = blockIdx.x * TC_TILES + tt;
+    const int p0 = tile_id * TC_PIX;
+    if (p0 >= P) break;
+    for (int px = pl; px < TC_PIX; px += lanes) {
+      const int p = p0 + px;
+      if (p >= P) break;
+      const int n = p / HW, rem = p - n * HW, y = rem / W, xx = rem - y * W;
+      const T* xb = x + n * HW;
+      float xv[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
+        xv[t] = (iy >= 0 && ix >= 0 && iy < H && ix < W) ? Elem<T>::to_f(xb[iy * W + ix]) : 0.f;
+      }
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float s = 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s += xv[t] * wr[t][e];
+        o[e] = s;
+      }
+      Vec8<TO>::store(z + (size_t)p * Cout + cc * 8, o);
+      if (stats) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tile[px * CP + cc * 8 + e] = o[e];
+      }
+    }
+    if (!stats) continue;
+    __syncthreads();
+    const int rows = min(TC_PIX, P - p0);
+    float s = 0.f;
+    for (int r = rg; r < rows; r += groups) s += tile[r * CP + c_red];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    float tot = 0.f;
+    for (int g = 0; g < groups; ++g) tot += red[g * Cout + c_red];
+    const float mean = tot / (float)rows;
+    float q = 0.f;
+    for (int r = rg; r < rows; r += groups) {
+      const float d = tile[r * CP + c_red] - mean;
+      q += d * d;
+    }
+    __syncthreads();
+    red[threadIdx.x] = q;
+    __syncthreads();
+    if (rg == 0) {
+      float qt = 0.f;
+      for (int g = 0; g < groups; ++g) qt += red[g * Cout + c_red];
+      stats[((size_t)tile_id * Cout + c_red) * 2] = mean;
+      stats[((size_t)tile_id * Cout + c_red) * 2 + 1] = qt;
+    }
+    __syncthreads();
+  }
+}
+
+// partial[blk][co][tap] = sum over the block's pixels of dz[p][co] * x[p + tap]
+constexpr int WG_PIX = 2048;
+template <typename T>
+__global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
+                                                       float* __restrict__ part, int N, int H, int W, int Cout) {
+  // thread = (8-channel group cc, pixel lane); 72 accumulators in registers;
+  // wave-level shuffles then LDS across the 4 waves.
+  __shared__ float red[4][256 * 9];
+  const int CC = Cout / 8;  // power of two, <= 32
+  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC, lanes = 256 / CC;
+  const int P = N * H * W;
+  const int HW = H * W;
+  const int pbeg = blockIdx.x * WG_PIX, pend = min(P, pbeg + WG_PIX);
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
+#pragma unroll 2
+  for (int p = pbeg + pl; p < pend; p += lanes) {
+    float d[8];
+    Vec8<T>::load(dz + (size_t)p * Cout + cc * 8, d);
+    const int n = p / HW, rem = p - n * HW, y = rem / W, xx = rem - y * W;
+    const T* xb = x + n * HW;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
+      const float xv = (iy >= 0 && ix >= 0 && iy < H && ix < W) ? Elem<T>::to_f(xb[iy * W + ix]) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t][e] += d[e] * xv;
+    }
+  }
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = acc[t][e];
+      for (int o = CC; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (ln < CC) red[wv][(cc * 8 + e) * 9 + t] = v;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < Cout * 9; i += 256)
+    part[(size_t)blockIdx.x * Cout * 9 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+}
+
+// --------------------------------------------------------------- Cout = 1 ---
+// y[p] = act(sum_{tap, ci} in[p + tap][ci] * w[tap][ci]); in = src upsampled by U
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void o1_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, TO* __restrict__ y,
+                                                     int N, int Hs, int Ws, int U, int C, int act_tanh) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  for (int i = threadIdx.x; i < 9 * C; i += 256) sm[i] = Elem<T>::to_f(w[i]);  // packed [tap][ci]
+  __syncthreads();
+  const int H = Hs * U, W = Ws * U;
+  const int P = N * H * W;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < P; p += gridDim.x * 256) {
+    const int n = p / (H * W), rem = p - n * H * W, yy = rem / W, xx = rem - yy * W;
+    float s = 0.f;
+    for (int t = 0; t < 9; ++t) {
+      const int iy = yy + t / 3 - 1, ix = xx + t % 3 - 1;
+      if (iy < 0 || ix < 0 || iy >= H || ix >= W) continue;
+      const T* src = x + ((size_t)(n * Hs + iy / U) * Ws + ix / U) * C;
+      const float* wt = sm + t * C;
+      for (int c = 0; c < C; c += 8) {
+        float v[8];
+        Vec8<T>::load(src + c, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[e] * wt[c + e];
+      }
+    }
+    if (act_tanh) s = tanhf(s);
+    y[p] = Elem<TO>::from_f(s);
+  }
+}
+
+// du[q][ci] = sum_tap dz[q - (tap - 1)] * w[tap][ci]   (q over the conv-input grid)
+template <typename T, typename TD>
+__global__ __launch_bounds__(256) void o1_dgrad_kernel(const TD* __restrict__ dz, const T* __restrict__ w,
+                                                       T* __restrict__ du, int N, int H, int W, int C) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  // w is the dgrad (mode-1, flipped) packing [ci][ky'][kx'][co=1]:
+  // sm[tap][ci] = w_fwd[0][ci][tap] = w[ci*9 + 8 - tap]
+  for (int i = threadIdx.x; i < 9 * C; i += 256) sm[i] = Elem<T>::to_f(w[(i % C) * 9 + 8 - i / C]);
+  __syncthreads();
+  const int CC = C / 8;
+  const long total = (long)N * H * W * CC;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int cc = i % CC;
+    const int q = i / CC;
+    const int n = q / (H * W), rem = q - n * H * W, yy = rem / W, xx = rem - yy * W;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int py = yy - (t / 3 - 1), px = xx - (t % 3 - 1);
+      if (py < 0 || px < 0 || py >= H || px >= W) continue;
+      const float d = Elem<TD>::to_f(dz[(n * H + py) * W + px]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += d * sm[t * C + cc * 8 + e];
+    }
+    Vec8<T>::store(du + (size_t)q * C + cc * 8, o);
+  }
+}
+
+// part[blk][tap][ci] = sum_p dz[p] * in[p + tap][ci]
+template <typename T, typename TD>
+__global__ __launch_bounds__(256) void o1_wgrad_kernel(const T* __restrict__ x, const TD* __restrict__ dz,
+                                                       float* __restrict__ part, int N, int Hs, int Ws, int U, int C) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][9*C]
+  const int CC = C / 8;  // power of two dividing 64
+  const int G = 256 / CC;
+  const int cc = threadIdx.x % CC, lg = threadIdx.x / CC;
+  const int H = Hs * U, W = Ws * U;
+  const int P = N * H * W;
+  const int pbeg = blockIdx.x * WG_PIX, pend = min(P, pbeg + WG_PIX);
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
+  for (int p = pbeg + lg; p < pend; p += G) {
+    const float d = Elem<TD>::to_f(dz[p]);
+    const int n = p / (H * W), rem = p - n * H * W, yy = rem / W, xx = rem - yy * W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = yy + t / 3 - 1, ix = xx + t % 3 - 1;
+      if (iy < 0 || ix < 0 || iy >= H || ix >= W) continue;
+      float v[8];
+      Vec8<T>::load(x + ((size_t)(n * Hs + iy / U) * Ws + ix / U) * C + cc * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t][e] += d * v[e];
+    }
+  }
+  // lanes of a wave with the same cc differ by multiples of CC
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = acc[t][e];
+      for (int o = CC; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (ln < CC) red[wv * 9 * C + t * C + cc * 8 + e] = v;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 9 * C; i += 256)
+    part[(size_t)blockIdx.x * 9 * C + i] = red[i] + red[9 * C + i] + red[18 * C + i] + red[27 * C + i];
+}
+
+}  // namespace hvit
+
+using namespace hvit;
+
+// host dispatchers (called from gemm_api.hip) -----------------------------------
+int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats,
+                     hipStream_t st) {
+  HVIT_CHECK(g->Cout % 8 == 0 && g->Cout <= 256, "thin conv: Cout=%d must be a multiple of 8 <= 256", g->Cout);
+  const int P = g->N * g->Hs * g->Ws;
+  const size_t smem = (TC_PIX * (g->Cout + 1) + 256) * sizeof(float);
+  dim3 grid(cdiv(cdiv(P, TC_PIX), TC_TILES));
+  if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
+    hipLaunchKernelGGL((c1_fwd_kernel<bf16_t, bf16_t>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
+                       (const bf16_t*)w, (bf16_t*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+  else if (dt == HVIT_BF16)
+    hipLaunchKernelGGL((c1_fwd_kernel<bf16_t, float>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
+                       (const bf16_t*)w, (float*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+  else if (y_dt == HVIT_F32)
+    hipLaunchKernelGGL((c1_fwd_kernel<float, float>), grid, dim3(256), smem, st, (const float*)g->src1,
+                       (const float*)w, (float*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+  else
+    hipLaunchKernelGGL((c1_fwd_kernel<float, bf16_t>), grid, dim3(256), smem, st, (const float*)g->src1,
+                       (const float*)w, (bf16_t*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g) {
+  const long P = (long)g->N * g->Hs * g->Ws;
+  return (long long)((P + WG_PIX - 1) / WG_PIX) * g->Cout * 9;
+}
+
+int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
+                       hipStream_t st) {
+  HVIT_CHECK(g->Cout <= 256 && 256 % g->Cout == 0, "thin conv wgrad: Cout=%d must divide 256", g->Cout);
+  const long P = (long)g->N * g->Hs * g->Ws;
+  const int nb = (int)((P + WG_PIX - 1) / WG_PIX);
+  HVIT_CHECK(ws && ws_elems >= (long long)nb * g->Cout * 9, "thin conv wgrad: workspace too small");
+  if (dt == HVIT_BF16)
+    hipLaunchKernelGGL((c1_wgrad_kernel<bf16_t>), dim3(nb), dim3(256), 0, st, (const bf16_t*)g->src1,
+                       (const bf16_t*)dz, ws, g->N, g->Hs, g->Ws, g->Cout);
+  else
+    hipLaunchKernelGGL((c1_wgrad_kernel<float>), dim3(nb), dim3(256), 0, st, (const float*)g->src1,
+                       (const float*)dz, ws, g->N, g->Hs, g->Ws, g->Cout);
+  HVIT_LAUNCH_CHECK();
+  return hvit_sum_slabs(ws, nb, (long long)g->Cout * 9, dw, st);
+}
+
+int hvit_thin_o1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, int act_tanh,
+                     hipStream_t st) {
+  const int C = g->C1;
+  HVIT_CHECK(C % 8 == 0, "thin conv: Cin=%d must be a multiple of 8", C);
+  const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
+  const size_t smem = 9 * C * sizeof(float);
+  dim3 grid((unsigned)std::min<long>((P + 255) / 256, 8192));
+  if (dt == HVIT_BF16 && y_dt == HVIT_F32)
+    hipLaunchKernelGGL((o1_fwd_kernel<bf16_t, float>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
+                       (const bf16_t*)w, (float*)y, g->N, g->Hs, g->Ws, g->U, C, act_tanh);
+  else if (dt == HVIT_BF16)
+    hipLaunchKernelGGL((o1_fwd_kernel<bf16_t, bf16_t>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
+                       (const bf16_t*)w, (bf16_t*)y, g->N, g->Hs, g->Ws, g->U, C, act_tanh);
+  else if (y_dt == HVIT_F32)
+    hipLaunchKernelGGL((o1_fwd_kernel<float, float>), grid, dim3(256), smem, st, (const float*)g->src1,
+                       (const float*)w, (float*)y, g->N, g->Hs, g->Ws, g->U, C, act_tanh);
+  else
+    hipLaunchKernelGGL((o1_fwd_kernel<float, bf16_t>), grid, dim3(256), smem, st, (const float*)g->src1,
+                       (const float*)w, (bf16_t*)y, g->N, g->Hs, g->Ws, g->U, C, act_tanh);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+// dz dtype = dt (the compute dtype); du at conv-input resolution [N, H, W, C]
+int hvit_thin_o1_dgrad(int dt, const hvit_conv_geom_t* g, const void* dz, const void* w, void* du, hipStream_t st) {
+  const int C = g->C1;
+  HVIT_CHECK(C % 8 == 0, "thin conv: Cin=%d must be a multiple of 8", C);
+  const int H = g->Hs * g->U, W = g->Ws * g->U;
+  const long total = (long)g->N * H * W * (C / 8);
+  const size_t smem = 9 * C * sizeof(float);
+  dim3 grid((unsigned)std::min<long>((total + 255) / 256, 16384));
+  if (dt == HVIT_BF16)
+    hipLaunchKernelGGL((o1_dgrad_kernel<bf16_t, bf16_t>), grid, dim3(256), smem, st, (const bf16_t*)dz,
+                       (const bf16_t*)w, (bf16_t*)du, g->N, H, W, C);
+  else
+    hipLaunchKernelGGL((o1_dgrad_kernel<float, float>), grid, dim3(256), smem, st, (const float*)dz,
+                       (const float*)w, (float*)du, g->N, H, W, C);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+long long hvit_thin_o1_wgrad_ws(const hvit_conv_geom_t* g) {
+  const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
+  return (long long)((P + WG_PIX - 1) / WG_PIX) * 9 * g->C1;
+}
+
+int hvit_thin_o1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
+                       hipStream_t st) {
+  const int C = g->C1;
+  HVIT_CHECK(C % 8 == 0 && C / 8 <= 64 && 64 % (C / 8) == 0, "thin conv wgrad: Cin=%d unsupported", C);
+  const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
+  const int nb = (int)((P + WG_PIX - 1) / WG_PIX);
+  HVIT_CHECK(ws && ws_elems >= (long long)nb * 9 * C, "thin conv wgrad: workspace too small");
+  const size_t smem = 4 * 9 * C * sizeof(float);
+  if (dt == HVIT_BF16)
+    hipLaunchKernelGGL((o1_wgrad_kernel<bf16_t, bf16_t>), dim3(nb), dim3(256), smem, st, (const bf16_t*)g->src1,
+                       (const bf16_t*)dz, ws, g->N, g->Hs, g->Ws, g->U, C);
+  else
+    hipLaunchKernelGGL((o1_wgrad_kernel<float, float>), dim3(nb), dim3(256), smem, st, (const float*)g->src1,
+                       (const float*)dz, ws, g->N, g->Hs, g->Ws, g->U, C);
+  HVIT_LAUNCH_CHECK();
+  return hvit_sum_slabs(ws, nb, 9LL * C, dw, st);
+}

@@ -176,11 +176,11 @@ class ConvBNActFn(torch.autograd.Function):
         s = stream_ptr()
         dy = dy.contiguous()
         dz = _empty(z.shape, dt, dev)
-        sums = torch.empty(2 * Cout, dtype=torch.float32, device=dev)
+        sums = torch.empty(L.lib().hvit_bn_act_bwd_sums_elems(Cout), dtype=torch.float32, device=dev)
         call("hvit_bn_act_bwd", dt, z.data_ptr(), N, H, W, Cout, ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
              gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
              dz.data_ptr(), dt, sums.data_ptr(), s)
-        dbeta, dgamma = sums[:Cout].clone(), sums[Cout:].clone()
+        dbeta, dgamma = sums[:Cout].clone(), sums[Cout:2 * Cout].clone()
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
         dw = conv_wgrad(dt, g, dz, w.shape)
         dx1 = dx2 = None
