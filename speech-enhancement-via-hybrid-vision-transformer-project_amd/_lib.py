@@ -17,7 +17,8 @@ F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhvit.so")
+# HVIT_LIB selects an alternative in-tree build (kernel A/B benchmarking only)
+LIB_PATH = os.path.join(_HERE, os.environ.get("HVIT_LIB", "libhvit.so"))
 
 vp = C.c_void_p
 i32 = C.c_int

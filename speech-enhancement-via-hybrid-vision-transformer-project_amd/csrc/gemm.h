@@ -3,15 +3,18 @@
 //   C[m][n] = sum_k A(m, k) * B(n, k)         (both operands "row x reduction")
 //
 // Structure: 256 threads (4 waves, 2x2), BM x BN output tile, 128 bytes of K
-// per stage (64 bf16 / 32 f32), two LDS stages, register-staged global loads
-// issued one stage ahead of the MFMAs.  Per 64-byte k-step each lane feeds one
-// 16-byte fragment per 16x16 sub-tile:
+// per stage (64 bf16 / 32 f32), two LDS stages and two register stages: the
+// global loads for stage t+2 are in flight while stage t runs on the MFMAs and
+// stage t+1 waits in registers, so HBM/L2 latency is covered by two stages of
+// math (counted vmcnt waits; interior tiles use branch-free loads so the
+// compiler can count them).  Per 64-byte k-step each lane feeds one 16-byte
+// fragment per 16x16 sub-tile:
 //   bf16: one  v_mfma_f32_16x16x32_bf16 (8 k per lane)
 //   f32 : four v_mfma_f32_16x16x4_f32   (4 k per lane; the k-slots of the four
 //         MFMAs are a permutation of the 16 k's, identical for A and B)
 // Operand layouts in LDS:
-//   KC (reduction dim contiguous in memory): [rows][128 B] + 16 B pad, read
-//     with ds_read_b128;
+//   KC (reduction dim contiguous in memory): [rows][128 B], 16-byte chunks
+//     XOR-swizzled by (row & 7) -> conflict-free ds_read_b128 / ds_write_b128;
 //   MN (rows contiguous in memory: wgrad/dgrad operands), bf16: copied as is,
 //     [k][rows] (+32 B pad, 128-B XOR swizzle on k bit 3), and read with
 //     ds_read_b64_tr_b16 (hardware transpose) -- no scalar LDS scatter;
@@ -26,17 +29,22 @@
 namespace hvit {
 
 constexpr int GEMM_THREADS = 256;
-constexpr int KSTAGE = 128;          // bytes of K per stage
-constexpr int PK = KSTAGE + 16;      // LDS pitch of KC tiles (bytes)
+constexpr int KSTAGE = 128;  // bytes of K per stage (= KC tile row pitch, no pad)
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
+__device__ __forceinline__ int kc_off(int row, int chunk) { return row * KSTAGE + ((chunk ^ (row & 7)) << 4); }
+
 // ------------------------------------------------------------ loaders --------
 // Roles: a = row index of the operand (m for A, n for B), b = reduction index.
 // KC loaders return 16 bytes = E elements (a, b..b+E-1); MN loaders return
-// E elements (a..a+E-1, b).  init() builds a cursor for (a, b); fetch(cur)
-// reads the current chunk; step(cur, BK) moves it BK along the reduction.
+// E elements (a..a+E-1, b).  A thread's chunks in one stage all share the same
+// b (KC) or the same a (MN) -- see TileCfg::map -- so a loader keeps that part
+// in one shared state `Sh` and only the varying part in a per-chunk cursor
+// `Cur` (keeps 128x128 tiles spill-free).  init() builds both for (a, b);
+// step() moves BK along the reduction; fetch<CHECK> reads the current chunk
+// (CHECK=false: interior tile, no bounds tests).
 template <typename T, bool KC_>
 struct LdDense {
   static constexpr bool KC = KC_;
@@ -46,29 +54,40 @@ struct LdDense {
   int rows;    // row extent
   int K;       // reduction extent
   bool vok;    // base 16-byte aligned and ld % E == 0 (vector loads legal)
+  struct Sh {};
   struct Cur {
+    const T* q;  // address of the current chunk
     int a, b;
   };
-  __device__ __forceinline__ void init(Cur& c, int a, int b) const { c.a = a; c.b = b; }
-  __device__ __forceinline__ void step(Cur& c, int bk) const { c.b += bk; }
-  __device__ __forceinline__ u32x4 fetch(const Cur& c) const {
+  __device__ __forceinline__ bool fast() const { return vok; }
+  __device__ __forceinline__ void init(Sh&, Cur& c, int a, int b) const {
+    c.a = a;
+    c.b = b;
+    c.q = KC ? p + (long)a * ld + b : p + (long)b * ld + a;
+  }
+  __device__ __forceinline__ void step_sh(Sh&, int) const {}
+  __device__ __forceinline__ void step(Cur& c, int bk) const {
+    c.b += bk;
+    c.q += KC ? (long)bk : (long)bk * ld;
+  }
+  template <bool CHECK>
+  __device__ __forceinline__ u32x4 fetch(const Sh&, const Cur& c) const {
+    if (!CHECK) return *(const u32x4*)c.q;
     const int a = c.a, b = c.b;
     u32x4 r = {0u, 0u, 0u, 0u};
     if (KC) {
       if (a >= rows || b >= K) return r;
-      const T* q = p + (long)a * ld + b;
-      if (vok && b + E <= K) return *(const u32x4*)q;
+      if (vok && b + E <= K) return *(const u32x4*)c.q;
       T tmp[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) tmp[e] = (b + e < K) ? q[e] : (T)0;
+      for (int e = 0; e < E; ++e) tmp[e] = (b + e < K) ? c.q[e] : (T)0;
       return *(u32x4*)tmp;
     } else {
       if (b >= K || a >= rows) return r;
-      const T* q = p + (long)b * ld + a;
-      if (vok && a + E <= rows) return *(const u32x4*)q;
+      if (vok && a + E <= rows) return *(const u32x4*)c.q;
       T tmp[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) tmp[e] = (a + e < rows) ? q[e] : (T)0;
+      for (int e = 0; e < E; ++e) tmp[e] = (a + e < rows) ? c.q[e] : (T)0;
       return *(u32x4*)tmp;
     }
   }
@@ -77,8 +96,8 @@ struct LdDense {
 // Implicit im2col over NHWC sources.  Pixel index p = output pixel (n, oy, ox)
 // of a Ho x Wo grid; im2col index k = (ky*KS + kx)*Ctot + c.  The conv input is
 // concat(src1[C1], src2[C2]) upsampled (nearest) by U from Hs x Ws.
-// KC (fwd / dgrad A operand): a = pixel (fixed per cursor), b = k (advances).
-// !KC (wgrad B operand):     a = k (fixed per cursor),     b = pixel (advances).
+// KC (fwd / dgrad A operand): a = pixel (per chunk), b = k (shared, advances).
+// !KC (wgrad B operand):     a = k (shared),         b = pixel (per chunk, advances).
 template <typename T, bool KC_>
 struct LdConv {
   static constexpr bool KC = KC_;
@@ -93,6 +112,7 @@ struct LdConv {
   int Kt;                 // KS*KS*Ctot
   bool vec_ok;            // C1 % E == 0 && C2 % E == 0 (16-byte gathers)
 
+  __device__ __forceinline__ bool fast() const { return vec_ok; }
   __device__ __forceinline__ float elem_f(int p, int k) const {
     if (p >= P || k >= Kt) return 0.f;
     int hw = Ho * Wo;
@@ -107,64 +127,68 @@ struct LdConv {
     return c < C1 ? Elem<T>::to_f(src1[pix * C1 + c]) : Elem<T>::to_f(src2[pix * C2 + (c - C1)]);
   }
 
-  // cursor: pixel part (n, oy, ox) and tap part (ky, kx, c) of (p, k)
-  struct Cur {
-    int p, k;       // current pixel / im2col index (scalar-path fallback)
-    int n, oy, ox;  // decomposition of p
-    int c, kx, ky;  // decomposition of k
+  struct Sh {  // tap part (ky, kx, c) of the im2col index k
+    int k, c, kx, ky;
   };
-  __device__ __forceinline__ void init(Cur& cu, int a, int b) const {
+  struct Cur {  // pixel part (n, oy, ox) of p
+    int p, n, oy, ox;
+  };
+  __device__ __forceinline__ void init(Sh& sh, Cur& cu, int a, int b) const {
     const int p = KC ? a : b, k = KC ? b : a;
     cu.p = p;
-    cu.k = k;
     const int hw = Ho * Wo;
     cu.n = p / hw;
     const int rem = p - cu.n * hw;
     cu.oy = rem / Wo;
     cu.ox = rem - cu.oy * Wo;
+    sh.k = k;
     const int tap = k / Ctot;
-    cu.c = k - tap * Ctot;
-    cu.ky = tap / KS;
-    cu.kx = tap - cu.ky * KS;
+    sh.c = k - tap * Ctot;
+    sh.ky = tap / KS;
+    sh.kx = tap - sh.ky * KS;
   }
-  __device__ __forceinline__ void step(Cur& cu, int bk) const {
-    if (KC) {  // advance k
-      cu.k += bk;
-      cu.c += bk;
-      while (cu.c >= Ctot) {
-        cu.c -= Ctot;
-        if (++cu.kx == KS) {
-          cu.kx = 0;
-          ++cu.ky;
-        }
-      }
-    } else {  // advance pixel
-      cu.p += bk;
-      cu.ox += bk;
-      while (cu.ox >= Wo) {
-        cu.ox -= Wo;
-        if (++cu.oy == Ho) {
-          cu.oy = 0;
-          ++cu.n;
-        }
+  __device__ __forceinline__ void step_sh(Sh& sh, int bk) const {
+    if (!KC) return;
+    sh.k += bk;
+    sh.c += bk;
+    while (sh.c >= Ctot) {
+      sh.c -= Ctot;
+      if (++sh.kx == KS) {
+        sh.kx = 0;
+        ++sh.ky;
       }
     }
   }
-  __device__ __forceinline__ u32x4 fetch(const Cur& cu) const {
-    u32x4 r = {0u, 0u, 0u, 0u};
-    if (vec_ok) {
-      if (cu.p >= P || cu.k >= Kt) return r;
-      const int iy = cu.oy * S - Pd + cu.ky, ix = cu.ox * S - Pd + cu.kx;
-      if (iy < 0 || ix < 0 || iy >= Hi || ix >= Wi) return r;
-      const int sy = U == 2 ? (iy >> 1) : iy, sx = U == 2 ? (ix >> 1) : ix;
-      const long pix = ((long)cu.n * Hs + sy) * Ws + sx;
-      const T* q = cu.c < C1 ? src1 + pix * C1 + cu.c : src2 + pix * C2 + (cu.c - C1);
-      return *(const u32x4*)q;
+  __device__ __forceinline__ void step(Cur& cu, int bk) const {
+    if (KC) return;
+    cu.p += bk;
+    cu.ox += bk;
+    while (cu.ox >= Wo) {
+      cu.ox -= Wo;
+      if (++cu.oy == Ho) {
+        cu.oy = 0;
+        ++cu.n;
+      }
+    }
+  }
+  template <bool CHECK>
+  __device__ __forceinline__ u32x4 fetch(const Sh& sh, const Cur& cu) const {
+    if (!CHECK || vec_ok) {
+      // padding taps read a valid address and are zeroed by a select
+      const int iy = cu.oy * S - Pd + sh.ky, ix = cu.ox * S - Pd + sh.kx;
+      bool ok = (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+      if (CHECK) ok = ok && cu.p < P && sh.k < Kt;
+      const int sy = ok ? (U == 2 ? (iy >> 1) : iy) : 0, sx = ok ? (U == 2 ? (ix >> 1) : ix) : 0;
+      const int pix = ((ok ? cu.n : 0) * Hs + sy) * Ws + sx;
+      const int c = ok ? sh.c : 0;
+      const T* q = c < C1 ? src1 + (long)pix * C1 + c : src2 + (long)pix * C2 + (c - C1);
+      const u32x4 v = *(const u32x4*)q;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      return ok ? v : z;
     }
     T tmp[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-      tmp[e] = Elem<T>::from_f(KC ? elem_f(cu.p, cu.k + e) : elem_f(cu.p, cu.k + e));
+    for (int e = 0; e < E; ++e) tmp[e] = Elem<T>::from_f(elem_f(cu.p, sh.k + e));
     return *(u32x4*)tmp;
   }
 };
@@ -345,8 +369,8 @@ struct TileCfg {
   static constexpr int E = Elem<T>::PER16;
   static constexpr int BK = KSTAGE / sizeof(T);
   static constexpr bool TR = !KC && sizeof(T) == 2;
-  static constexpr int BYTES = TR ? BK * MnTile<R>::PM : R * PK;  // per stage
-  static constexpr int CH = R * KSTAGE / 16 / GEMM_THREADS;        // chunks per thread
+  static constexpr int BYTES = TR ? BK * MnTile<R>::PM : R * KSTAGE;  // per stage
+  static constexpr int CH = R * KSTAGE / 16 / GEMM_THREADS;           // chunks per thread
   // chunk ch -> (row, k) offsets within the stage
   __device__ __forceinline__ static void map(int ch, int& row, int& k) {
     if (KC) {
@@ -361,42 +385,159 @@ struct TileCfg {
     int row, k;
     map(ch, row, k);
     if (KC) {
-      *(u32x4*)(tile + row * PK + (k / E) * 16) = v;
+      *(u32x4*)(tile + kc_off(row, k / E)) = v;
     } else if (TR) {
       *(u32x4*)(tile + MnTile<R>::off(k, row * 2)) = v;
-    } else {  // f32 scatter-transpose
+    } else {  // f32 scatter-transpose into the KC layout
       const T* e = (const T*)&v;
 #pragma unroll
-      for (int i = 0; i < E; ++i) *(T*)(tile + (row + i) * PK + k * sizeof(T)) = e[i];
+      for (int i = 0; i < E; ++i)
+        *(T*)(tile + kc_off(row + i, k / E) + (k % E) * sizeof(T)) = e[i];
     }
   }
   __device__ __forceinline__ static u32x4 frag(const char* tile, int rb, int s, int lane) {
     if constexpr (TR) {
       return frag_tr<R>(tile, rb, s, lane);
     } else {
-      return *(const u32x4*)(tile + (rb + (lane & 15)) * PK + (4 * s + (lane >> 4)) * 16);
+      return *(const u32x4*)(tile + kc_off(rb + (lane & 15), 4 * s + (lane >> 4)));
     }
   }
 };
 
 template <typename T, int BM, int BN, class LA, class LB>
-__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_kernel(LA la, LB lb, int M, int N, int K,
-                                                               int kps, Epi ep) {
+struct GemmCore {
   using TA = TileCfg<T, BM, LA::KC>;
   using TB = TileCfg<T, BN, LB::KC>;
-  constexpr int BK = TA::BK;
-  constexpr int WM = 2, WN = 2;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int CA = TA::CH, CB = TB::CH;
-  constexpr int STEPS = KSTAGE / 64;
-  static_assert(CA >= 1 && CB >= 1, "tile too small");
+  static constexpr int BK = TA::BK;
+  static constexpr int WM = 2, WN = 2;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int CA = TA::CH, CB = TB::CH;
+  static constexpr int STEPS = KSTAGE / 64;
+  static constexpr int SM_LOOP = 2 * (TA::BYTES + TB::BYTES);
 
-  constexpr int SM_LOOP = 2 * (TA::BYTES + TB::BYTES);
+  // the K loop: acc += A[m0.., kbeg..kend) * B[n0.., kbeg..kend)^T
+  template <bool CHECK>
+  __device__ __forceinline__ static void run(const LA& la, const LB& lb, char* smem, int m0, int n0, int kbeg,
+                                             int kend, f32x4 (&acc)[FM][FN]) {
+    char* As = smem;
+    char* Bs = smem + 2 * TA::BYTES;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    if (nk == 0) return;
+
+    typename LA::Sh sa;
+    typename LB::Sh sb;
+    typename LA::Cur ca[CA];
+    typename LB::Cur cb[CB];
+    int kofa[CA], kofb[CB];
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      int row, k;
+      TA::map(tid + c * GEMM_THREADS, row, k);
+      kofa[c] = k;
+      la.init(sa, ca[c], m0 + row, kbeg + k);
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      int row, k;
+      TB::map(tid + c * GEMM_THREADS, row, k);
+      kofb[c] = k;
+      lb.init(sb, cb[c], n0 + row, kbeg + k);
+    }
+    u32x4 ra0[CA], rb0[CB], ra1[CA], rb1[CB];
+    // stage s is fetched with the cursors at kbeg + s*BK; stages beyond the end
+    // re-read the last valid stage (keeps the load count static; never used)
+    int fetched = 0;
+    auto fetch = [&](u32x4(&ra)[CA], u32x4(&rb)[CB]) {
+      const int s = fetched;
+      if (s > 0 && s < nk) {
+        la.step_sh(sa, BK);
+        lb.step_sh(sb, BK);
+#pragma unroll
+        for (int c = 0; c < CA; ++c) la.step(ca[c], BK);
+#pragma unroll
+        for (int c = 0; c < CB; ++c) lb.step(cb[c], BK);
+      }
+      const int k0 = kbeg + min(s, nk - 1) * BK;
+#pragma unroll
+      for (int c = 0; c < CA; ++c)
+        ra[c] = (!CHECK || k0 + kofa[c] < kend) ? la.template fetch<CHECK>(sa, ca[c]) : (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+        rb[c] = (!CHECK || k0 + kofb[c] < kend) ? lb.template fetch<CHECK>(sb, cb[c]) : (u32x4){0u, 0u, 0u, 0u};
+      ++fetched;
+    };
+    auto stash = [&](const u32x4(&ra)[CA], const u32x4(&rb)[CB], int buf) {
+#pragma unroll
+      for (int c = 0; c < CA; ++c) TA::store(As + buf * TA::BYTES, tid + c * GEMM_THREADS, ra[c]);
+#pragma unroll
+      for (int c = 0; c < CB; ++c) TB::store(Bs + buf * TB::BYTES, tid + c * GEMM_THREADS, rb[c]);
+    };
+    auto compute = [&](int buf) {
+      const char* at = As + buf * TA::BYTES;
+      const char* bt = Bs + buf * TB::BYTES;
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) {
+        u32x4 fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = TA::frag(at, wm * WTM + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = TB::frag(bt, wn * WTN + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (sizeof(T) == 2) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(s16x8, fa[i]), __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+            } else {
+              f32x4 va = __builtin_bit_cast(f32x4, fa[i]);
+              f32x4 vb = __builtin_bit_cast(f32x4, fb[j]);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[0], vb[0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[1], vb[1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[2], vb[2], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[3], vb[3], acc[i][j], 0, 0, 0);
+            }
+          }
+      }
+    };
+
+    // prologue: stage 0 -> regs0 -> LDS0; stage 1 -> regs1 (in flight)
+    fetch(ra0, rb0);
+    fetch(ra1, rb1);
+    stash(ra0, rb0, 0);
+    __syncthreads();
+    for (int t = 0; t < nk; t += 2) {
+      // even stage t in LDS0; stage t+1 in regs1; prefetch stage t+2 -> regs0
+      fetch(ra0, rb0);
+      compute(0);
+      if (t + 1 < nk) stash(ra1, rb1, 1);
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      // odd stage t+1 in LDS1; stage t+2 in regs0; prefetch stage t+3 -> regs1
+      fetch(ra1, rb1);
+      compute(1);
+      if (t + 2 < nk) stash(ra0, rb0, 0);
+      __syncthreads();
+    }
+  }
+};
+
+#ifndef HVIT_BIG_OCC
+#define HVIT_BIG_OCC 2
+#endif
+template <typename T, int BM, int BN, class LA, class LB>
+__global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N, int K,
+                                                               int kps, Epi ep) {
+  using C = GemmCore<T, BM, BN, LA, LB>;
+  constexpr int WM = C::WM, WN = C::WN, WTM = C::WTM, WTN = C::WTN, FM = C::FM, FN = C::FN;
+  constexpr int SM_LOOP = C::SM_LOOP;
   constexpr int SM_EPI = (64 * (BN + 4) + (GEMM_THREADS / (BN / 4)) * BN) * 4;
   __shared__ __attribute__((aligned(16))) char smem[SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI];
-  char* As = smem;
-  char* Bs = smem + 2 * TA::BYTES;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -406,7 +547,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_kernel(LA la, LB lb, int
   const int n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * kps;
   const int kend = min(K, kbeg + kps);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int frow = lane & 15, fq = lane >> 4;
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -414,88 +555,9 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_kernel(LA la, LB lb, int
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  typename LA::Cur ca[CA];
-  typename LB::Cur cb[CB];
-  int kofa[CA], kofb[CB];
-#pragma unroll
-  for (int c = 0; c < CA; ++c) {
-    int row, k;
-    TA::map(tid + c * GEMM_THREADS, row, k);
-    kofa[c] = k;
-    la.init(ca[c], m0 + row, kbeg + k);
-  }
-#pragma unroll
-  for (int c = 0; c < CB; ++c) {
-    int row, k;
-    TB::map(tid + c * GEMM_THREADS, row, k);
-    kofb[c] = k;
-    lb.init(cb[c], n0 + row, kbeg + k);
-  }
-  u32x4 ra[CA], rb[CB];
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int c = 0; c < CA; ++c)
-      ra[c] = (k0 + kofa[c] < kend) ? la.fetch(ca[c]) : (u32x4){0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int c = 0; c < CB; ++c)
-      rb[c] = (k0 + kofb[c] < kend) ? lb.fetch(cb[c]) : (u32x4){0u, 0u, 0u, 0u};
-  };
-  auto advance = [&]() {
-#pragma unroll
-    for (int c = 0; c < CA; ++c) la.step(ca[c], BK);
-#pragma unroll
-    for (int c = 0; c < CB; ++c) lb.step(cb[c], BK);
-  };
-  auto stash = [&](int buf) {
-#pragma unroll
-    for (int c = 0; c < CA; ++c) TA::store(As + buf * TA::BYTES, tid + c * GEMM_THREADS, ra[c]);
-#pragma unroll
-    for (int c = 0; c < CB; ++c) TB::store(Bs + buf * TB::BYTES, tid + c * GEMM_THREADS, rb[c]);
-  };
-
-  if (nk > 0) {
-    fetch(kbeg);
-    stash(0);
-    __syncthreads();
-  }
-  const int frow = lane & 15, fq = lane >> 4;
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nk) {
-      advance();
-      fetch(kbeg + (t + 1) * BK);
-    }
-    const char* at = As + buf * TA::BYTES;
-    const char* bt = Bs + buf * TB::BYTES;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      u32x4 fa[FM], fb[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = TA::frag(at, wm * WTM + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = TB::frag(bt, wn * WTN + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          if constexpr (sizeof(T) == 2) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(s16x8, fa[i]), __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
-          } else {
-            f32x4 va = __builtin_bit_cast(f32x4, fa[i]);
-            f32x4 vb = __builtin_bit_cast(f32x4, fb[j]);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[0], vb[0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[1], vb[1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[2], vb[2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[3], vb[3], acc[i][j], 0, 0, 0);
-          }
-        }
-    }
-    if (t + 1 < nk) stash(buf ^ 1);
-    __syncthreads();
-  }
-  (void)frow;
-  (void)fq;
+  const bool interior = m0 + BM <= M && n0 + BN <= N && ((kend - kbeg) % C::BK) == 0 && la.fast() && lb.fast();
+  if (interior) C::template run<false>(la, lb, smem, m0, n0, kbeg, kend, acc);
+  else C::template run<true>(la, lb, smem, m0, n0, kbeg, kend, acc);
 
   // ------------------------------------------------------------- epilogue ---
   // The accumulator tile is staged through LDS in 64-row halves (f32, padded
@@ -604,12 +666,13 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_kernel(LA la, LB lb, int
 
 
 
+
 // host-side launcher --------------------------------------------------------
 // Effective split-K count after rounding each split to whole K-tiles (never
 // more than requested).  Callers that reduce slabs must use this count.
 template <typename T>
 inline int plan_splits(int K, int splits, int* kps_out = nullptr) {
-  constexpr int BK = 64 / sizeof(T);
+  constexpr int BK = KSTAGE / sizeof(T);
   if (splits < 1) splits = 1;
   int kps = (K + splits - 1) / splits;
   kps = ((kps + BK - 1) / BK) * BK;
@@ -628,11 +691,21 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep, hi
     hvit_set_error("launch_gemm: split-K requires EPI_SLAB");
     return HVIT_ERR_ARG;
   }
-  int big = force_tile ? (force_tile == 128)
-                       : ((long)cdiv(M, 128) * cdiv(N, 128) * splits >= 160);
-  if (big) {
+  // tile: 128x128 when the grid still fills the chip; 128x64 for narrow
+  // outputs (N <= 64: conv layers with 64 channels); else 64x64
+  int tile = force_tile;
+  if (!tile) {
+    if (N <= 64 && (long)cdiv(M, 128) * splits >= 160) tile = 12864;
+    else if (N > 64 && (long)cdiv(M, 128) * cdiv(N, 128) * splits >= 160) tile = 128;
+    else tile = 64;
+  }
+  if (tile == 128) {
     dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
     hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb,
+                       M, N, K, kps, ep);
+  } else if (tile == 12864) {
+    dim3 g(cdiv(M, 128), cdiv(N, 64), splits);
+    hipLaunchKernelGGL((gemm_kernel<T, 128, 64, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb,
                        M, N, K, kps, ep);
   } else {
     dim3 g(cdiv(M, 64), cdiv(N, 64), splits);

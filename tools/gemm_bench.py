@@ -53,6 +53,13 @@ def linear(M, N, K, tag):
     report(f"dgrad {tag}", 2 * M * N * K, us)
     us = timeit(lambda: HF.linear_wgrad(L.BF16, dy, x, M, N, K))
     report(f"wgrad {tag}", 2 * M * N * K, us)
+    # library reference (hipBLASLt via torch) for the same three products
+    us = timeit(lambda: torch.nn.functional.linear(x, w))
+    report(f"  torch fwd   {tag}", 2 * M * N * K, us)
+    us = timeit(lambda: dy @ w)
+    report(f"  torch dgrad {tag}", 2 * M * N * K, us)
+    us = timeit(lambda: dy.t() @ x)
+    report(f"  torch wgrad {tag}", 2 * M * N * K, us)
 
 
 def conv(N, Hs, Ws, C1, C2, U, Cout, tag):
