@@ -105,7 +105,7 @@ __global__ void tanh_bwd_kernel(const void* dy, int dydt, const float* y, void* 
   }
 }
 
-// out[n] += sum_m x[m*ld + n]; block = 256 columns x row-chunk
+// out[n] += sum_m x[m*ld + n]; block = 256 columns x row-chunk (generic path)
 __global__ void reduce_rows_kernel(const void* x, int dt, long M, long N, long ld, int rows_per_block,
                                    float* out) {
   long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -117,11 +117,76 @@ __global__ void reduce_rows_kernel(const void* x, int dt, long M, long N, long l
   atomicAdd(out + n, s);
 }
 
+// Vectorised column sums: each thread owns one 16-byte column chunk (VEC
+// elements) and walks rows ty, ty+RY, ... of the block's R-row slice; the RY
+// partial rows are folded through LDS and one atomic per column and block is
+// issued.  Needs N % VEC == 0, ld % VEC == 0, 16-byte aligned base.
+constexpr int RC_TX = 32, RC_RY = 8;
+template <typename T>
+__global__ __launch_bounds__(256) void reduce_cols_vec_kernel(const T* x, int M, int N, int ld, int R, float* out) {
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float red[RC_RY][RC_TX * VEC + 4];
+  const int tx = threadIdx.x % RC_TX, ty = threadIdx.x / RC_TX;
+  const int n = (blockIdx.x * RC_TX + tx) * VEC;
+  const int m0 = blockIdx.y * R;
+  const int m1 = min(M, m0 + R);
+  float acc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+  if (n < N) {
+    const T* p = x + (long)(m0 + ty) * ld + n;
+    int m = m0 + ty;
+    // two rows in flight per iteration
+    for (; m + RC_RY < m1; m += 2 * RC_RY, p += 2L * RC_RY * ld) {
+      const u32x4 a = *(const u32x4*)p;
+      const u32x4 b = *(const u32x4*)(p + (long)RC_RY * ld);
+      const T* ea = (const T*)&a;
+      const T* eb = (const T*)&b;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] += Elem<T>::to_f(ea[e]) + Elem<T>::to_f(eb[e]);
+    }
+    if (m < m1) {
+      const u32x4 a = *(const u32x4*)p;
+      const T* ea = (const T*)&a;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] += Elem<T>::to_f(ea[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) red[ty][tx * VEC + e] = acc[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < RC_TX * VEC; c += blockDim.x) {
+    const int col = blockIdx.x * RC_TX * VEC + c;
+    if (col >= N) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < RC_RY; ++k) s += red[k][c];
+    atomicAdd(out + col, s);
+  }
+}
+
+// out[i] = sum_k ws[k*n + i]; 4 consecutive elements per thread, 4 slabs in flight
 __global__ void sum_slabs_kernel(const float* ws, int splits, long n, float* out) {
   GRID_STRIDE(i, n) {
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += ws[(long)k * n + i];
     out[i] = s;
+  }
+}
+
+__global__ void sum_slabs4_kernel(const float* ws, int splits, int n4, float* out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const f32x4* p = (const f32x4*)ws + i;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    int k = 0;
+    for (; k + 4 <= splits; k += 4) {
+      s0 += p[(long)k * n4];
+      s1 += p[(long)(k + 1) * n4];
+      s2 += p[(long)(k + 2) * n4];
+      s3 += p[(long)(k + 3) * n4];
+    }
+    for (; k < splits; ++k) s0 += p[(long)k * n4];
+    ((f32x4*)out)[i] = (s0 + s1) + (s2 + s3);
   }
 }
 
@@ -201,9 +266,27 @@ extern "C" int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long lon
 extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate,
                                 float* out, void* stream) {
   HVIT_CHECK(x && out, "hvit_reduce_rows: null pointer");
+  HVIT_CHECK(dt == HVIT_F32 || dt == HVIT_BF16, "hvit_reduce_rows: dtype");
   hipStream_t st = (hipStream_t)stream;
   if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
   if (M <= 0 || N <= 0) return HVIT_OK;
+  const int vec = dt == HVIT_F32 ? 4 : 8;
+  if (N % vec == 0 && ld % vec == 0 && ((uintptr_t)x & 15) == 0 && M * ld < (1LL << 31)) {
+    const int gx = (int)((N / vec + RC_TX - 1) / RC_TX);
+    // about 1024 workgroups, row slices a multiple of 2*RC_RY
+    long R = (M * gx + 1023) / 1024;
+    R = ((R + 2 * RC_RY - 1) / (2 * RC_RY)) * (2 * RC_RY);
+    if (R < 2 * RC_RY) R = 2 * RC_RY;
+    const int gy = (int)((M + R - 1) / R);
+    if (dt == HVIT_F32)
+      hipLaunchKernelGGL(reduce_cols_vec_kernel<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, (int)M,
+                         (int)N, (int)ld, (int)R, out);
+    else
+      hipLaunchKernelGGL(reduce_cols_vec_kernel<bf16_t>, dim3(gx, gy), dim3(256), 0, st, (const bf16_t*)x, (int)M,
+                         (int)N, (int)ld, (int)R, out);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   int rpb = 64;
   long gy = (M + rpb - 1) / rpb;
   long gx = (N + 255) / 256;
@@ -217,8 +300,13 @@ extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N,
 extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream) {
   HVIT_CHECK(ws && out && splits > 0, "hvit_sum_slabs: bad args");
   if (n <= 0) return HVIT_OK;
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, splits, (long)n,
-                     out);
+  if (n % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)out & 15) == 0 && n < (1LL << 31)) {
+    hipLaunchKernelGGL(sum_slabs4_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, ws, splits,
+                       (int)(n / 4), out);
+  } else {
+    hipLaunchKernelGGL(sum_slabs_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, splits,
+                       (long)n, out);
+  }
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

@@ -51,16 +51,27 @@ int check_epi(const hvit_epilogue_t* e) {
   return HVIT_OK;
 }
 
-// choose split-K so that a wgrad launch has enough workgroups
-int wgrad_splits(long M, long N, long K, int bk) {
-  long tiles = (long)cdiv(M, 64) * cdiv(N, 64);
-  long want = (512 + tiles - 1) / tiles;
+// choose split-K so that a wgrad launch has enough workgroups: about 256
+// workgroups of the given tile (one per CU, two for 64x64 tiles; each keeps
+// >= 4 K-stages)
+int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64) {
+  long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
+  const long target = bm * bn <= 64 * 64 ? 512 : 256;  // small tiles: two per CU
+  long want = (target + tiles - 1) / tiles;
   long maxs = K / (4 * bk);
   if (want > maxs) want = maxs;
   if (want > 256) want = 256;
   if (want < 1) want = 1;
   return (int)want;
 }
+// wgrad tiles: dense x dense -> 128x128; dense x im2col -> 128x64 (fits the
+// register budget of the gathered operand's cursors)
+constexpr int LIN_WG_BM = 128, LIN_WG_BN = 128, LIN_WG_TILE = 128;
+// (64x64 when Cout <= 64 so no half-empty tiles)
+struct ConvWgTile {
+  int bm, bn, tile;
+  explicit ConvWgTile(int cout) : bm(cout <= 64 ? 64 : 128), bn(64), tile(cout <= 64 ? 64 : 12864) {}
+};
 
 template <typename T>
 LdConv<T, true> conv_a(const hvit_conv_geom_t* g, const void* s1, int C1, const void* s2, int C2, int Hs, int Ws,
@@ -173,7 +184,7 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
 
 extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
   // dw is [N_out x K_in] reduced over M rows ; slabs only when splitting
-  int s = wgrad_splits(N, K, M, 32);
+  int s = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
   return s > 1 ? (long long)s * N * K : 0;
 }
 
@@ -183,7 +194,7 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
   HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_wgrad: bad shape");
   HVIT_CHECK(aligned16(dy) && aligned16(x), "hvit_linear_wgrad: alignment");
   hipStream_t st = (hipStream_t)stream;
-  int splits = wgrad_splits(N, K, M, 32);
+  int splits = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
   if ((long long)splits * N * K > ws_elems || !ws) splits = 1;
   if (M == 0) {
     (void)hipMemsetAsync(dw, 0, sizeof(float) * N * K, st);
@@ -200,7 +211,7 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
     ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
     ep.out = splits > 1 ? (void*)ws : (void*)dw;
     int rc = launch_gemm<T>(dense<T, false>(dy, N, N, M), dense<T, false>(x, K, K, M), N, K, M, splits, ep, st,
-                            splits > 1 ? 64 : 0);
+                            LIN_WG_TILE);
     if (rc) return rc;
   });
   if (splits > 1) return hvit_sum_slabs(ws, splits, (long long)N * K, dw, stream);
@@ -289,7 +300,8 @@ extern "C" long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g) {
   const long Ho = (Hi + 2 * g->pad - g->KS) / g->stride + 1;
   const long Wo = (Wi + 2 * g->pad - g->KS) / g->stride + 1;
   const long Kt = (long)g->KS * g->KS * (g->C1 + g->C2);
-  int s = wgrad_splits(g->Cout, Kt, g->N * Ho * Wo, 32);
+  const ConvWgTile t(g->Cout);
+  int s = wgrad_splits(g->Cout, Kt, g->N * Ho * Wo, t.bm, t.bn);
   return s > 1 ? (long long)s * g->Cout * Kt : 0;
 }
 
@@ -307,7 +319,8 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     static_assert(sizeof(lb) == sizeof(la), "layout");
     __builtin_memcpy(&lb, &la, sizeof(la));
     const int M = g->Cout, N = la.Kt, K = la.P;
-    int splits = wgrad_splits(M, N, K, 32);
+    const ConvWgTile t(M);
+    int splits = wgrad_splits(M, N, K, t.bm, t.bn);
     if ((long long)splits * M * N > ws_elems || !ws) splits = 1;
     splits = plan_splits<T>(K, splits);
     Epi ep;
@@ -315,7 +328,7 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     ep.out = splits > 1 ? (void*)ws : (void*)dw_packed;
     ep.out_dt = HVIT_F32;
     ep.ldo = N;
-    int rc = launch_gemm<T>(dense<T, false>(dy, M, M, K), lb, M, N, K, splits, ep, st, splits > 1 ? 64 : 0);
+    int rc = launch_gemm<T>(dense<T, false>(dy, M, M, K), lb, M, N, K, splits, ep, st, t.tile);
     if (rc) return rc;
     if (splits > 1) return hvit_sum_slabs(ws, splits, (long long)M * N, dw_packed, stream);
     return HVIT_OK;

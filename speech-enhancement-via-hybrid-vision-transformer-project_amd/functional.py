@@ -344,9 +344,9 @@ class ViTBlockFn(torch.autograd.Function):
         df2b = col_sum(g2, M, D)
         df2w = linear_wgrad(dt, g2, a, M, D, hid)
         dh = _empty((M, hid), dt, dev)
+        df1b = torch.zeros(hid, dtype=torch.float32, device=dev)  # fc1 bias grad: fused column sum
         call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
-             epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1), s)
-        df1b = col_sum(dh, M, hid)
+             epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1, colsum=df1b), s)
         df1w = linear_wgrad(dt, dh, xn2, M, hid, D)
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
