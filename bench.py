@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the dominant-kernel timing loop (used for rocprofv3 --pmc passes)")
     return ap.parse_args()
 
 
@@ -74,8 +76,20 @@ def dominant_kernel_roofline(hv, batch):
     achieved = flops / sec / 1e12
     return {"kernel": "hvit gemm_kernel<bf16,128,128,LdDense,LdDense> (fc1 + GELU_DUAL epilogue)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": measured_traffic(),
             "flops_per_launch": flops, "avg_launch_us": round(sec * 1e6, 2)}
+
+
+def measured_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed PMC pass
+    (profiles/roofline_pmc.json, written by tools/pmc_summary.py from
+    rocprofv3 --pmc FETCH_SIZE WRITE_SIZE on ``bench.py --roofline-only``;
+    FETCH_SIZE doubled per the gfx950 correction).  None when absent."""
+    p = os.path.join(ROOT, "profiles", "roofline_pmc.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(batch, budget_s):
@@ -124,6 +138,9 @@ def main():
     import hvit_amd_loader
 
     hv = hvit_amd_loader.load()
+    if args.roofline_only:
+        print(json.dumps(dominant_kernel_roofline(hv, args.batch)), flush=True)
+        return
     from hvit_amd.data import spectrogram_batch
     from hvit_amd.dp import GradAllReducer, broadcast_module
 

@@ -41,12 +41,14 @@ static inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0;
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  // round-to-nearest-even; NaN stays NaN
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+// f32 -> bf16, round-to-nearest-even, NaN stays NaN: the plain conversion
+// compiles to the gfx950 v_cvt_pk_bf16_f32 (one instruction per pair)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t f2bf2(float lo, float hi) {
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 template <typename T> struct Elem;
@@ -100,13 +102,25 @@ static inline uint32_t drop_threshold(float p) {
 }
 
 // ----------------------------------------------------------------- GELU(erf) --
+// GELU (erf form, as torch.nn.GELU()) without the branchy libm erff: erf by
+// Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), one rcp + one exp; the same
+// exp(-x^2/2) also gives the Gaussian density for the derivative.
+__device__ __forceinline__ float erf_gauss(float z, float& e) {  // e = exp(-z^2)
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * az);
+  e = __expf(-az * az);
+  const float poly =
+      t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.f - poly * e, z);
+}
 __device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  float e;
+  return 0.5f * x * (1.f + erf_gauss(x * 0.70710678118654752f, e));
 }
 __device__ __forceinline__ float gelu_grad(float x) {
-  float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;
+  const float cdf = 0.5f * (1.f + erf_gauss(x * 0.70710678118654752f, e));
+  return cdf + x * (0.39894228040143268f * e);
 }
 
 // ---------------------------------------------------------- wave reductions --

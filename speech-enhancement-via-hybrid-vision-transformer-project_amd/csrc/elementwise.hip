@@ -91,8 +91,8 @@ __global__ void dropout_scale4_kernel(const void* g, int gdt, void* out, int odt
       *(f32x4*)((float*)out + i) = v;
     } else {
       uint2 u;
-      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      u.x = f2bf2(v[0], v[1]);
+      u.y = f2bf2(v[2], v[3]);
       *(uint2*)((bf16_t*)out + i) = u;
     }
   }

@@ -24,6 +24,8 @@
 // sources; the 4x4/stride-4 patch embedding); each thread keeps a cursor per
 // 16-byte chunk (its pixel / tap decomposition) that advances incrementally.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace hvit {
@@ -196,6 +198,11 @@ struct LdConv {
 // ------------------------------------------------------------ epilogue -------
 enum EpiMode { EPI_STORE = 0, EPI_SLAB = 1, EPI_PATCH = 2, EPI_SPLIT2 = 3 };
 enum EpiAct { ACT_NONE = 0, ACT_GELU_DUAL = 1, ACT_TANH = 2, ACT_GELU_BWD = 3 };
+// compile-time epilogue kind: a lean kernel for plain stores (+bias, BN stats,
+// column sums) and for split-K slabs; everything else takes the generic one
+// and for the three fused ViT epilogues (fc1 GELU, residual adds, GELU
+// backward), which are only chosen when every tile is full and vector-aligned
+enum EpiKind { EK_GEN = 0, EK_STORE = 1, EK_SLAB = 2, EK_GELU_DUAL = 3, EK_RESID = 4, EK_GELU_BWD = 5 };
 
 struct Epi {
   int mode = EPI_STORE;
@@ -224,61 +231,133 @@ struct Epi {
   int rows_per_sample = 1;
   float* stats = nullptr;   // BN partials [64-row tile][N][2] = (mean, M2)
   float* colsum = nullptr;  // atomic column sums of the final v
+  bool vec_ok = false;      // N % 4 == 0, every operand 16-B aligned with ld % 4 == 0
   // EPI_PATCH: m = token (b, py, px) of Hp x Wp, n = (ky*P + kx)*C + c
   int pP = 0, pC = 0, pHp = 0, pWp = 0, pH = 0, pW = 0;
 };
 
 // 4 adjacent output columns (n .. n+nv-1) of row m: store helpers and the
 // fused epilogue math.
+// ragged / misaligned fallbacks are out of line: they are rare and would
+// otherwise be inlined once per unrolled epilogue row (code size, i-cache)
+__device__ __attribute__((noinline)) void store4_slow(void* p, long off, f32x4 v, int nv, int dt) {
+  for (int e = 0; e < nv; ++e) st_dt(p, off + e, v[e], dt);
+}
+__device__ __attribute__((noinline)) f32x4 load4_slow(const void* p, long off, int nv, int dt) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < nv; ++e) v[e] = ld_dt(p, off + e, dt);
+  return v;
+}
+
 __device__ __forceinline__ void store4(void* p, long off, const f32x4& v, int nv, int dt) {
   if (dt == HVIT_F32) {
     float* q = (float*)p + off;
     if (nv == 4 && (((uintptr_t)q) & 15) == 0) *(f32x4*)q = v;
-    else for (int e = 0; e < nv; ++e) q[e] = v[e];
+    else store4_slow(p, off, v, nv, dt);
   } else {
     bf16_t* q = (bf16_t*)p + off;
     if (nv == 4 && (((uintptr_t)q) & 7) == 0) {
       uint2 u;
-      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      u.x = f2bf2(v[0], v[1]);
+      u.y = f2bf2(v[2], v[3]);
       *(uint2*)q = u;
     } else {
-      for (int e = 0; e < nv; ++e) q[e] = f2bf(v[e]);
+      store4_slow(p, off, v, nv, dt);
     }
   }
 }
 
 __device__ __forceinline__ f32x4 load4(const void* p, long off, int nv, int dt) {
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (dt == HVIT_F32) {
     const float* q = (const float*)p + off;
     if (nv == 4 && (((uintptr_t)q) & 15) == 0) return *(const f32x4*)q;
-    for (int e = 0; e < nv; ++e) v[e] = q[e];
   } else {
     const bf16_t* q = (const bf16_t*)p + off;
     if (nv == 4 && (((uintptr_t)q) & 7) == 0) {
       uint2 u = *(const uint2*)q;
+      f32x4 v;
       v[0] = __uint_as_float(u.x << 16);
       v[1] = __uint_as_float(u.x & 0xffff0000u);
       v[2] = __uint_as_float(u.y << 16);
       v[3] = __uint_as_float(u.y & 0xffff0000u);
       return v;
     }
-    for (int e = 0; e < nv; ++e) v[e] = bf2f(q[e]);
   }
-  return v;
+  return load4_slow(p, off, nv, dt);
 }
 
-__device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, int N, f32x4& v) {
-  if (ep.bias) {
-    f32x4 b = load4(ep.bias, n, nv, HVIT_F32);
-    v += b;
+// FAST: caller guarantees 4 in-range columns and 16-byte (f32) / 8-byte (bf16)
+// alignment -- plain vector accesses, no per-lane branches
+template <bool FAST>
+__device__ __forceinline__ void store4v(void* p, long off, const f32x4& v, int nv, int dt) {
+  if constexpr (FAST) {
+    if (dt == HVIT_F32) {
+      *(f32x4*)((float*)p + off) = v;
+    } else {
+      uint2 u;
+      u.x = f2bf2(v[0], v[1]);
+      u.y = f2bf2(v[2], v[3]);
+      *(uint2*)((bf16_t*)p + off) = u;
+    }
+  } else {
+    store4(p, off, v, nv, dt);
   }
-  if (ep.rowadd) v += load4(ep.rowadd, (long)(m % ep.rowadd_mod) * ep.rowadd_ld + n, nv, HVIT_F32);
+}
+template <bool FAST>
+__device__ __forceinline__ f32x4 load4v(const void* p, long off, int nv, int dt) {
+  if constexpr (FAST) {
+    if (dt == HVIT_F32) return *(const f32x4*)((const float*)p + off);
+    const uint2 u = *(const uint2*)((const bf16_t*)p + off);
+    f32x4 v;
+    v[0] = __uint_as_float(u.x << 16);
+    v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16);
+    v[3] = __uint_as_float(u.y & 0xffff0000u);
+    return v;
+  } else {
+    return load4(p, off, nv, dt);
+  }
+}
+
+// dropout multipliers of 4 adjacent elements (index i0 = m*N + n, i0 % 4 == 0):
+// one 64-bit hash gives the four 16-bit uniforms
+__device__ __forceinline__ f32x4 keep4(const Epi& ep, int m, int n, int N) {
+  const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
+  const uint64_t h = mix64(ep.seed ^ ((uint64_t)ep.site << 48) ^ ((i0 >> 2) * 0xD6E8FEB86659FD93ull));
+  f32x4 k;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) k[e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= ep.drop_thr) ? ep.drop_scale : 0.f;
+  return k;
+}
+
+// Inputs the epilogue reads besides the accumulator, loaded for all of a
+// thread's rows BEFORE any of its stores: the compiler cannot reorder a load
+// above a store that may alias it, so loading inside the store loop would
+// serialise one global-load latency per row.
+struct EpiIn {
+  f32x4 rowadd, aux, resid;
+  float rowscale;
+};
+
+template <bool FAST>
+__device__ __forceinline__ void epi_load4(const Epi& ep, int m, int n, int nv, bool ok, EpiIn& in) {
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  in.rowadd =
+      (ep.rowadd && ok) ? load4v<FAST>(ep.rowadd, (long)(m % ep.rowadd_mod) * ep.rowadd_ld + n, nv, HVIT_F32) : z;
+  in.aux = (ep.act == ACT_GELU_BWD && ok) ? load4v<FAST>(ep.aux, (long)m * ep.ldaux + n, nv, ep.aux_dt) : z;
+  in.resid = (ep.resid && ok) ? load4v<FAST>(ep.resid, (long)m * ep.ldr + n, nv, HVIT_F32) : z;
+  in.rowscale = (ep.resid && ep.rowscale && ok) ? ep.rowscale[m / ep.rows_per_sample] : 1.f;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, int N, f32x4& v, const f32x4& bias,
+                                           const EpiIn& in) {
+  v += bias;
+  if (ep.rowadd) v += in.rowadd;
   float keep[4] = {1.f, 1.f, 1.f, 1.f};
   if (ep.drop_thr) {
     const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-    if ((i0 & 3) == 0) {
+    if (FAST || (i0 & 3) == 0) {
       uint64_t h = mix64(ep.seed ^ ((uint64_t)ep.site << 48) ^ ((i0 >> 2) * 0xD6E8FEB86659FD93ull));
 #pragma unroll
       for (int e = 0; e < 4; ++e) keep[e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= ep.drop_thr) ? ep.drop_scale : 0.f;
@@ -291,11 +370,11 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, 
     for (int e = 0; e < 4; ++e) keep[e] = ep.drop_scale;
   }
   if (ep.act == ACT_GELU_DUAL) {
-    store4(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
+    store4v<FAST>(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
     f32x4 g;
 #pragma unroll
     for (int e = 0; e < 4; ++e) g[e] = gelu_f(v[e]) * keep[e];
-    store4(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
+    store4v<FAST>(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
     return;
   }
   if (ep.act == ACT_TANH) {
@@ -305,18 +384,15 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, 
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] *= keep[e];
   if (ep.act == ACT_GELU_BWD) {
-    f32x4 h = load4(ep.aux, (long)m * ep.ldaux + n, nv, ep.aux_dt);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(h[e]);
+    for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(in.aux[e]);
   }
   if (ep.resid) {
-    const float s = ep.rowscale ? ep.rowscale[m / ep.rows_per_sample] : 1.f;
-    f32x4 r = load4(ep.resid, (long)m * ep.ldr + n, nv, HVIT_F32);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = r[e] + s * v[e];
+    for (int e = 0; e < 4; ++e) v[e] = in.resid[e] + in.rowscale * v[e];
   }
   if (ep.mode == EPI_STORE) {
-    store4(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
+    store4v<FAST>(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
   } else if (ep.mode == EPI_SPLIT2) {
     for (int e = 0; e < nv; ++e) {
       if (n + e < ep.split_col) st_dt(ep.out, (long)m * ep.ldo + n + e, v[e], ep.out_dt);
@@ -527,12 +603,28 @@ struct GemmCore {
   }
 };
 
+// Diagnostic build only (-DHVIT_GEMM_STAMPS): per-workgroup wall-clock stamps
+// (100 MHz s_memrealtime) at start / after the K loop / at exit, read back with
+// hvit_debug_gemm_stamps().  Never enabled in the shipped library.
+#ifdef HVIT_GEMM_STAMPS
+extern __device__ unsigned long long g_gemm_stamps[65536 * 4];
+#define GEMM_STAMP(i)                                                                          \
+  do {                                                                                         \
+    const unsigned bid_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);      \
+    if (threadIdx.x == 0 && bid_ < 65536) g_gemm_stamps[bid_ * 4 + (i)] = wall_clock64();      \
+  } while (0)
+#else
+#define GEMM_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 #ifndef HVIT_BIG_OCC
 #define HVIT_BIG_OCC 2
 #endif
-template <typename T, int BM, int BN, class LA, class LB>
-__global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N, int K,
-                                                               int kps, Epi ep) {
+template <typename T, int BM, int BN, class LA, class LB, int EK>
+__global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
+                                                                                            int K, int kps, Epi ep) {
   using C = GemmCore<T, BM, BN, LA, LB>;
   constexpr int WM = C::WM, WN = C::WN, WTM = C::WTM, WTN = C::WTN, FM = C::FM, FN = C::FN;
   constexpr int SM_LOOP = C::SM_LOOP;
@@ -555,24 +647,41 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // epilogue column ownership (see below); the bias is fetched before the K
+  // loop so its latency hides behind the MFMAs
+  constexpr int CP = BN + 4;                 // LDS tile pitch (floats)
+  constexpr int HALVES = BM / 64;
+  constexpr int C4 = BN / 4;                 // 4-column chunks per row
+  constexpr int RSTEP = GEMM_THREADS / C4;   // rows advanced per sweep
+  constexpr int NR = 64 / RSTEP;             // rows per thread per 64-row half
+  const int c4 = tid % C4;
+  const int r0 = tid / C4;
+  const int n = n0 + c4 * 4;
+  const bool nok = n < N;
+  const bool full = n + 3 < N;
+  const int nv = full ? 4 : N - n;
+  const f32x4 bias4 = (ep.bias && nok) ? load4(ep.bias, n, nv, HVIT_F32) : (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  GEMM_STAMP(0);
   const bool interior = m0 + BM <= M && n0 + BN <= N && ((kend - kbeg) % C::BK) == 0 && la.fast() && lb.fast();
   if (interior) C::template run<false>(la, lb, smem, m0, n0, kbeg, kend, acc);
   else C::template run<true>(la, lb, smem, m0, n0, kbeg, kend, acc);
+  GEMM_STAMP(1);
+  // Retire every outstanding global load here (the bias, and the K loop's
+  // never-consumed tail prefetches) with one explicit wait that the compiler's
+  // wait-count pass sees: otherwise it re-emits vmcnt(0) per predicated output
+  // row, and on gfx9 vmcnt also counts the epilogue's own stores -- each row
+  // would wait for the previous row's store to land.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt/lgkmcnt untouched
 
   // ------------------------------------------------------------- epilogue ---
   // The accumulator tile is staged through LDS in 64-row halves (f32, padded
   // rows) and then processed row-contiguously: each thread owns 4 adjacent
   // columns, so bias / residual / aux loads and output stores are vectorised
-  // and coalesced, and every acc[][] index stays static (no scratch).
-  constexpr int CP = BN + 4;                 // LDS tile pitch (floats)
-  constexpr int HALVES = BM / 64;
-  constexpr int C4 = BN / 4;                 // 4-column chunks per row
-  constexpr int RSTEP = GEMM_THREADS / C4;   // rows advanced per sweep
+  // and coalesced, and every acc[][] index stays static (no scratch).  Halves
+  // whose rows and columns are all in range take a branch-free row loop.
   static_assert((64 * CP + RSTEP * BN) * 4 <= (int)sizeof(smem), "epilogue tile exceeds LDS");
   float* Cs = (float*)smem;
-  const int c4 = tid % C4;
-  const int r0 = tid / C4;
-  const int n = n0 + c4 * 4;
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
@@ -591,31 +700,128 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
     __syncthreads();
     const int mbase = m0 + hh * 64;
     const int rows_here = min(64, M - mbase);
+    const bool all_in = mbase + 64 <= M && n0 + BN <= N && ep.vec_ok;  // uniform
     float st_sum[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int row = r0; row < 64; row += RSTEP) {
-      const int m = mbase + row;
-      if (m >= M || n >= N) continue;
-      f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
-      const bool full = n + 3 < N;
-      const int nv = full ? 4 : N - n;
-      if (ep.mode == EPI_SLAB) {
-        float* slab = (float*)ep.out + (long)blockIdx.z * M * ep.ldo + (long)m * ep.ldo + n;
-        if (full && (ep.ldo & 3) == 0) *(f32x4*)slab = v;
-        else for (int e = 0; e < nv; ++e) slab[e] = v[e];
-        continue;
-      }
-      epi_apply4(ep, m, n, nv, N, v);
+
+    auto rows = [&](auto pred) {
+      constexpr bool PRED = decltype(pred)::value;
+      if constexpr (EK == EK_SLAB) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (e < nv) {
-          csum[e] += v[e];
-          st_sum[e] += v[e];
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          if (PRED && (m >= M || !nok)) continue;
+          const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
+          float* slab = (float*)ep.out + (long)blockIdx.z * M * ep.ldo + (long)m * ep.ldo + n;
+          if (!PRED || (full && (ep.ldo & 3) == 0)) *(f32x4*)slab = v;
+          else store4_slow(slab, 0, v, nv, HVIT_F32);
+        }
+      } else if constexpr (EK == EK_STORE) {
+        // host guarantees N % 4 == 0, ldo % 4 == 0 and an aligned output
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          if (PRED && (m >= M || !nok)) continue;
+          const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
+          if (ep.out_dt == HVIT_F32) {
+            *(f32x4*)((float*)ep.out + (long)m * ep.ldo + n) = v;
+          } else {
+            uint2 u;
+            u.x = f2bf2(v[0], v[1]);
+            u.y = f2bf2(v[2], v[3]);
+            *(uint2*)((bf16_t*)ep.out + (long)m * ep.ldo + n) = u;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            csum[e] += v[e];
+            st_sum[e] += v[e];
+          }
+          if (ep.stats) *(f32x4*)(Cs + row * CP + c4 * 4) = v;
+        }
+      } else if constexpr (EK == EK_GELU_DUAL) {
+        // h = v + b (saved for backward), a = dropout(gelu(h))
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
+          store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
+          const f32x4 k = ep.drop_thr ? keep4(ep, m, n, N) : (f32x4){1.f, 1.f, 1.f, 1.f};
+          f32x4 g;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) g[e] = gelu_f(v[e]) * k[e];
+          store4v<true>(ep.out2, (long)m * ep.ldo2 + n, g, 4, ep.out2_dt);
+        }
+      } else if constexpr (EK == EK_RESID) {
+        // out = resid + rowscale[m / rps] * dropout(v + b)   (f32 residual stream)
+        f32x4 r[NR];
+        float rs[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int m = mbase + r0 + i * RSTEP;
+          r[i] = *(const f32x4*)((const float*)ep.resid + (long)m * ep.ldr + n);
+          rs[i] = ep.rowscale ? ep.rowscale[m / ep.rows_per_sample] : 1.f;
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
+          if (ep.drop_thr) v *= keep4(ep, m, n, N);
+          v = r[i] + rs[i] * v;
+          store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
+        }
+      } else if constexpr (EK == EK_GELU_BWD) {
+        // dh = dropout_mask(v) * gelu'(h)   (+ column sums for the bias grad)
+        f32x4 h[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int m = mbase + r0 + i * RSTEP;
+          h[i] = load4v<true>(ep.aux, (long)m * ep.ldaux + n, 4, ep.aux_dt);
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
+          if (ep.drop_thr) v *= keep4(ep, m, n, N);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(h[i][e]);
+          store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) csum[e] += v[e];
+        }
+      } else {
+        EpiIn in[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int m = mbase + r0 + i * RSTEP;
+          epi_load4<!PRED>(ep, m, n, nv, !PRED || (m < M && nok), in[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          if (PRED && (m >= M || !nok)) continue;
+          f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
+          epi_apply4<!PRED>(ep, m, n, PRED ? nv : 4, N, v, bias4, in[i]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (!PRED || e < nv) {
+              csum[e] += v[e];
+              st_sum[e] += v[e];
+            }
+          }
+          *(f32x4*)(Cs + row * CP + c4 * 4) = v;
         }
       }
-      Cs[row * CP + c4 * 4 + 0] = v[0];
-      Cs[row * CP + c4 * 4 + 1] = v[1];
-      Cs[row * CP + c4 * 4 + 2] = v[2];
-      Cs[row * CP + c4 * 4 + 3] = v[3];
+    };
+    if constexpr (EK >= EK_GELU_DUAL) {
+      rows(std::false_type());  // host guarantees full, aligned tiles
+    } else {
+      if (all_in) rows(std::false_type());
+      else rows(std::true_type());
     }
     if (ep.stats && rows_here > 0) {
       // per-column (mean, M2) of this 64-row sub-tile: sums -> mean -> M2
@@ -662,6 +868,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
         atomicAdd(ep.colsum + n + e, s);
       }
   }
+  GEMM_STAMP(2);
 }
 
 
@@ -682,8 +889,12 @@ inline int plan_splits(int K, int splits, int* kps_out = nullptr) {
 }
 
 template <typename T, class LA, class LB>
-int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep, hipStream_t st,
+int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in, hipStream_t st,
                 int force_tile = 0) {
+  Epi ep = ep_in;
+  auto vok = [](const void* p, long ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
+  ep.vec_ok = N % 4 == 0 && vok(ep.out, ep.ldo) && vok(ep.out2, ep.ldo2) && vok(ep.aux, ep.ldaux) &&
+              vok(ep.resid, ep.ldr) && vok(ep.rowadd, ep.rowadd_ld);
   if (M <= 0 || N <= 0) return HVIT_OK;
   int kps = 0;
   splits = plan_splits<T>(K, splits, &kps);
@@ -699,18 +910,43 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep, hi
     else if (N > 64 && (long)cdiv(M, 128) * cdiv(N, 128) * splits >= 160) tile = 128;
     else tile = 64;
   }
-  if (tile == 128) {
-    dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
-    hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb,
-                       M, N, K, kps, ep);
-  } else if (tile == 12864) {
-    dim3 g(cdiv(M, 128), cdiv(N, 64), splits);
-    hipLaunchKernelGGL((gemm_kernel<T, 128, 64, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb,
-                       M, N, K, kps, ep);
-  } else {
-    dim3 g(cdiv(M, 64), cdiv(N, 64), splits);
-    hipLaunchKernelGGL((gemm_kernel<T, 64, 64, LA, LB>), g, dim3(GEMM_THREADS), 0, st, la, lb, M,
-                       N, K, kps, ep);
+  const bool lean_store = ep.mode == EPI_STORE && ep.act == ACT_NONE && !ep.rowadd && !ep.resid && !ep.drop_thr &&
+                          ep.drop_scale == 1.f && N % 4 == 0 && ep.ldo % 4 == 0 && ((uintptr_t)ep.out & 15) == 0;
+  int ek = ep.mode == EPI_SLAB ? EK_SLAB : (lean_store ? EK_STORE : EK_GEN);
+  {
+    const int bm = tile == 128 || tile == 12864 ? 128 : 64, bn = tile == 128 ? 128 : 64;
+    const bool full_tiles = ep.vec_ok && M % bm == 0 && N % bn == 0 && ep.mode == EPI_STORE && !ep.rowadd &&
+                            !ep.stats;
+    const bool drop_ok = ep.drop_thr ? N % 4 == 0 : ep.drop_scale == 1.f;
+    if (ek == EK_GEN && full_tiles && drop_ok) {
+      if (ep.act == ACT_GELU_DUAL && !ep.resid) ek = EK_GELU_DUAL;
+      else if (ep.act == ACT_NONE && ep.resid && ep.resid != ep.out) ek = EK_RESID;
+      else if (ep.act == ACT_GELU_BWD && !ep.resid && ep.aux) ek = EK_GELU_BWD;
+    }
+  }
+  auto go = [&](auto ekc) {
+    constexpr int EKc = decltype(ekc)::value;
+    if (tile == 128) {
+      dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
+      hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB, EKc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N, K, kps,
+                         ep);
+    } else if (tile == 12864) {
+      dim3 g(cdiv(M, 128), cdiv(N, 64), splits);
+      hipLaunchKernelGGL((gemm_kernel<T, 128, 64, LA, LB, EKc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N, K, kps,
+                         ep);
+    } else {
+      dim3 g(cdiv(M, 64), cdiv(N, 64), splits);
+      hipLaunchKernelGGL((gemm_kernel<T, 64, 64, LA, LB, EKc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N, K, kps,
+                         ep);
+    }
+  };
+  switch (ek) {
+    case EK_SLAB: go(std::integral_constant<int, EK_SLAB>()); break;
+    case EK_STORE: go(std::integral_constant<int, EK_STORE>()); break;
+    case EK_GELU_DUAL: go(std::integral_constant<int, EK_GELU_DUAL>()); break;
+    case EK_RESID: go(std::integral_constant<int, EK_RESID>()); break;
+    case EK_GELU_BWD: go(std::integral_constant<int, EK_GELU_BWD>()); break;
+    default: go(std::integral_constant<int, EK_GEN>()); break;
   }
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
