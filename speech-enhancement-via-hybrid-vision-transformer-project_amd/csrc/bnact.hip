@@ -46,11 +46,22 @@ struct BnArgs {
   uint32_t site;
 };
 
+// Dropout2d multipliers of channels c .. c+CV-1 of sample n (element index
+// n*C + c, a multiple of 4: one 64-bit hash yields four 16-bit uniforms)
 template <int CV>
 __device__ __forceinline__ void drop_mask(const BnArgs& a, int n, int c, float* m) {
+  if (!a.thr) {
 #pragma unroll
-  for (int e = 0; e < CV; ++e)
-    m[e] = a.thr ? (rng_keep(a.seed, a.site, (uint64_t)n * a.C + c + e, a.thr) ? a.dscale : 0.f) : 1.f;
+    for (int e = 0; e < CV; ++e) m[e] = 1.f;
+    return;
+  }
+  const uint64_t i0 = (uint64_t)n * a.C + c;
+#pragma unroll
+  for (int e4 = 0; e4 < CV; e4 += 4) {
+    const uint64_t h = mix64(a.seed ^ ((uint64_t)a.site << 48) ^ (((i0 + e4) >> 2) * 0xD6E8FEB86659FD93ull));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e4 + e] = ((uint32_t)(h >> (16 * e)) & 0xffffu) >= a.thr ? a.dscale : 0.f;
+  }
 }
 
 // forward: y[n, oy, ox, c..] over full windows
@@ -60,21 +71,23 @@ __global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z,
   const int G = a.C / CV;
   const int Ho = a.H / a.pool, Wo = a.W / a.pool;
   const int total = a.N * Ho * Wo * G;
+  // a thread's channel group never changes (256 % G == 0, grid stride % G == 0)
+  const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
+  float sc[CV], sh[CV];
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    sc[e] = a.invstd[c + e] * a.gamma[c + e];
+    sh[e] = a.beta[c + e] - a.mean[c + e] * sc[e];
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int cg = i % G;
     int t = i / G;
     const int ox = t % Wo;
     t /= Wo;
     const int oy = t % Ho;
     const int n = t / Ho;
-    const int c = cg * CV;
-    float sc[CV], sh[CV], best[CV];
+    float best[CV];
 #pragma unroll
-    for (int e = 0; e < CV; ++e) {
-      sc[e] = a.invstd[c + e] * a.gamma[c + e];
-      sh[e] = a.beta[c + e] - a.mean[c + e] * sc[e];
-      best[e] = 0.f;  // relu output >= 0
-    }
+    for (int e = 0; e < CV; ++e) best[e] = 0.f;  // relu output >= 0
     for (int dy = 0; dy < a.pool; ++dy)
       for (int dx = 0; dx < a.pool; ++dx) {
         float v[CV];
@@ -114,24 +127,25 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
   float acc1[CV], acc2[CV];
 #pragma unroll
   for (int e = 0; e < CV; ++e) acc1[e] = acc2[e] = 0.f;
-  int cg_fixed = -1;
+  // a thread's channel group never changes (256 % G == 0, grid stride % G == 0):
+  // per-channel constants are loaded once
+  const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
+  float sc[CV], sh[CV], mu[CV], is[CV], s1[CV], s2[CV];
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    mu[e] = a.mean[c + e];
+    is[e] = a.invstd[c + e];
+    sc[e] = is[e] * a.gamma[c + e];
+    sh[e] = a.beta[c + e] - mu[e] * sc[e];
+    s1[e] = (APPLY && training) ? sums[c + e] * invM : 0.f;
+    s2[e] = (APPLY && training) ? sums[a.C + c + e] * invM : 0.f;
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int cg = i % G;
-    cg_fixed = cg;
     int t = i / G;
     const int wx = t % Ww;
     t /= Ww;
     const int wy = t % Hw;
     const int n = t / Hw;
-    const int c = cg * CV;
-    float sc[CV], sh[CV], mu[CV], is[CV];
-#pragma unroll
-    for (int e = 0; e < CV; ++e) {
-      mu[e] = a.mean[c + e];
-      is[e] = a.invstd[c + e];
-      sc[e] = is[e] * a.gamma[c + e];
-      sh[e] = a.beta[c + e] - mu[e] * sc[e];
-    }
     // window values
     float zv[MAXW][CV];
     bool inb[MAXW];
@@ -195,7 +209,7 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
           const float k = sc[e];
           if (training) {
             const float xh = (zv[q][e] - mu[e]) * is[e];
-            o[e] = k * (g[q][e] - sums[c + e] * invM - xh * sums[a.C + c + e] * invM);
+            o[e] = k * (g[q][e] - s1[e] - xh * s2[e]);
           } else {
             o[e] = k * g[q][e];
           }
@@ -227,14 +241,13 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
       // spread the per-block partials over BN_SLOTS copies so that few blocks
       // add to the same address (same-address atomics serialise)
       float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
-      const int c = threadIdx.x * CV;
+      const int cc = threadIdx.x * CV;
 #pragma unroll
       for (int e = 0; e < CV; ++e) {
-        atomicAdd(slot + c + e, t1[e]);
-        atomicAdd(slot + a.C + c + e, t2[e]);
+        atomicAdd(slot + cc + e, t1[e]);
+        atomicAdd(slot + a.C + cc + e, t2[e]);
       }
     }
-    (void)cg_fixed;
   }
 }
 

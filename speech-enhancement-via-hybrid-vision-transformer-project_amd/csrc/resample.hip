@@ -68,6 +68,23 @@ __device__ __forceinline__ void out_range(int i, int in, int out, float scale, i
   if (hi > out - 1) hi = out - 1;
 }
 
+constexpr int TAPS = 16;
+__device__ __forceinline__ int taps_of(int i, int in, int out, float scale, int* o_idx, float* w) {
+  int lo, hi;
+  out_range(i, in, out, scale, lo, hi);
+  int nt = 0;
+  for (int o = lo; o <= hi && nt < TAPS; ++o) {
+    const float wt = lin_w(o, i, in, scale);
+    if (wt != 0.f) {
+      o_idx[nt] = o;
+      w[nt] = wt;
+      ++nt;
+    }
+  }
+  return nt;
+}
+
+// generic (any C / dtype pair): one thread per input element
 __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const void* dy, int dy_dt, void* dx, int dx_dt, int N,
                                                           int Hi, int Wi, int C, int Ho, int Wo, float sh,
                                                           float sw, int accumulate) {
@@ -79,23 +96,77 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const void* dy, int d
     const int t = p / Wi;
     const int iy = t % Hi;
     const int n = t / Hi;
-    int ylo, yhi, xlo, xhi;
-    out_range(iy, Hi, Ho, sh, ylo, yhi);
-    out_range(ix, Wi, Wo, sw, xlo, xhi);
+    int oy[TAPS], ox[TAPS];
+    float wy[TAPS], wx[TAPS];
+    const int ny = taps_of(iy, Hi, Ho, sh, oy, wy);
+    const int nx = taps_of(ix, Wi, Wo, sw, ox, wx);
     float acc = 0.f;
-    for (int oy = ylo; oy <= yhi; ++oy) {
-      const float wy = lin_w(oy, iy, Hi, sh);
-      if (wy == 0.f) continue;
+    for (int a = 0; a < ny; ++a) {
+      const int base = (n * Ho + oy[a]) * Wo;
       float row = 0.f;
-      const int base = (n * Ho + oy) * Wo;
-      for (int ox = xlo; ox <= xhi; ++ox) {
-        const float wx = lin_w(ox, ix, Wi, sw);
-        if (wx != 0.f) row += wx * ld_dt(dy, (base + ox) * C + c, dy_dt);
-      }
-      acc += wy * row;
+      for (int b = 0; b < nx; ++b) row += wx[b] * ld_dt(dy, (base + ox[b]) * C + c, dy_dt);
+      acc += wy[a] * row;
     }
     if (accumulate) acc += ld_dt(dx, i, dx_dt);
     st_dt(dx, i, acc, dx_dt);
+  }
+}
+
+// Vectorised gather backward: one thread per (input pixel, 16-byte channel
+// group); the output taps that sample the pixel (<= TAPS per dimension) and
+// their weights are computed once per thread and reused for all CV channels.
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void bilinear_bwd_vec_kernel(const TI* __restrict__ dy, TO* __restrict__ dx,
+                                                              int N, int Hi, int Wi, int C, int Ho, int Wo,
+                                                              float sh, float sw, int accumulate) {
+  constexpr int CV = 8;  // channels per thread (one or two 16-byte vectors)
+  const int G = C / CV;
+  const int total = N * Hi * Wi * G;  // < 2^31 (checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % G;
+    const int p = i / G;
+    const int ix = p % Wi;
+    const int t = p / Wi;
+    const int iy = t % Hi;
+    const int n = t / Hi;
+    int oy[TAPS], ox[TAPS];
+    float wy[TAPS], wx[TAPS];
+    const int ny = taps_of(iy, Hi, Ho, sh, oy, wy);
+    const int nx = taps_of(ix, Wi, Wo, sw, ox, wx);
+    float acc[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) acc[e] = 0.f;
+    for (int a = 0; a < ny; ++a) {
+      const TI* row = dy + ((size_t)(n * Ho + oy[a]) * Wo) * C + cg * CV;
+      for (int b = 0; b < nx; ++b) {
+        const float w = wy[a] * wx[b];
+        const TI* q = row + (size_t)ox[b] * C;
+        float v[CV];
+        if constexpr (sizeof(TI) == 2) {
+          const u32x4 u = *(const u32x4*)q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] = __uint_as_float(u[e] << 16);
+            v[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+          }
+        } else {
+          const f32x4 lo = *(const f32x4*)q, hi = *(const f32x4*)(q + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = lo[e];
+            v[4 + e] = hi[e];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < CV; ++e) acc[e] += w * v[e];
+      }
+    }
+    TO* d = dx + (size_t)p * C + cg * CV;
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      if (accumulate) acc[e] += Elem<TO>::to_f(d[e]);
+      d[e] = Elem<TO>::from_f(acc[e]);
+    }
   }
 }
 
@@ -154,6 +225,22 @@ extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int W
   if (total <= 0) return HVIT_OK;
   HVIT_CHECK(total < (1L << 31) && (long)N * Ho * Wo * C < (1L << 31), "resample: tensor too large");
   float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
+  // vector path: 8-channel groups, at most TAPS output taps per dimension
+  const bool taps_ok = (float)Ho / (float)Hi <= 6.f && (float)Wo / (float)Wi <= 6.f;
+  if (C % 8 == 0 && taps_ok && dy_dt == dx_dt && aligned16(dy) && aligned16(dx)) {
+    const long groups = (long)N * Hi * Wi * (C / 8);
+    if (dy_dt == HVIT_BF16)
+      hipLaunchKernelGGL((bilinear_bwd_vec_kernel<bf16_t, bf16_t>), dim3(grid_for(groups)), dim3(256), 0,
+                         (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, N, Hi, Wi, C, Ho, Wo, sh, sw,
+                         accumulate);
+    else
+      hipLaunchKernelGGL((bilinear_bwd_vec_kernel<float, float>), dim3(grid_for(groups)), dim3(256), 0,
+                         (hipStream_t)stream, (const float*)dy, (float*)dx, N, Hi, Wi, C, Ho, Wo, sh, sw,
+                         accumulate);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
+  HVIT_CHECK(taps_ok, "hvit_bilinear_bwd: upsampling factor above 6 not supported");
   hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dy, dy_dt,
                      dx, dx_dt, N, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
   HVIT_LAUNCH_CHECK();
