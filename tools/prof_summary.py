@@ -11,9 +11,9 @@ import sys
 
 def short(name):
     grid = re.search(r" grid=\S+", name)
-    name = re.sub(r"\(.*", "", name) + (grid.group(0) if grid else "")
-    name = name.replace("void ", "").replace("hvit::", "")
-    return name[:110]
+    name = re.sub(r"\(.*", "", name)
+    name = name.replace("void ", "").replace("hvit::", "").replace("unsigned short", "bf16")
+    return name[:100] + (grid.group(0) if grid else "")
 
 
 def main():
@@ -23,8 +23,19 @@ def main():
     top = int(args[2]) if len(args) > 2 else 40
     by_grid = "--grid" in sys.argv
     f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    tr = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     if f and not by_grid:
         rows = list(csv.DictReader(open(f[0])))
+    elif tr:
+        agg = {}
+        for r in csv.DictReader(open(tr[0])):
+            wg = int(r["Workgroup_Size_X"]) or 1
+            key = r["Kernel_Name"] + (f" grid={int(r['Grid_Size_X']) // wg}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}"
+                                      if by_grid else "")
+            a = agg.setdefault(key, [0, 0.0])
+            a[0] += 1
+            a[1] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+        rows = [dict(Name=k, Calls=v[0], TotalDurationNs=v[1], AverageNs=v[1] / v[0]) for k, v in agg.items()]
     else:
         import sqlite3
         db = sqlite3.connect(glob.glob(os.path.join(d, "**", "*.db"), recursive=True)[0])
