@@ -127,9 +127,10 @@ int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, cons
  * dgamma / dbeta [D] overwritten. */
 int hvit_layernorm_fwd(const float* x, const float* gamma, const float* beta, int M, int D, float eps, void* y,
                        int y_dt, float* mean, float* rstd, void* stream);
+long long hvit_layernorm_bwd_ws_elems(int M, int D);   /* f32 slab for dgamma/dbeta partials */
 int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean, const float* rstd,
                        const float* gamma, int M, int D, const float* resid, float* dx, float* dgamma,
-                       float* dbeta, void* stream);
+                       float* dbeta, float* ws, long long ws_elems, void* stream);  /* ws may be NULL */
 
 /* ---- BatchNorm2d -> ReLU -> Dropout2d -> MaxPool2d(pool) tail of ConvBlock /
  * TransposeConvBlock (components.py:67-85, :161-178).  z is the pre-BN conv

@@ -63,7 +63,8 @@ _SIGS = {
     "hvit_mhsa_fwd": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_layernorm_fwd": ([vp, vp, vp, i32, i32, f32, vp, i32, vp, vp, vp], i32),
-    "hvit_layernorm_bwd": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp], i32),
+    "hvit_layernorm_bwd_ws_elems": ([i32, i32], i64),
+    "hvit_layernorm_bwd": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, i64, vp], i32),
     "hvit_bn_finalize": ([vp, i32, i32, i64, i32, vp, vp, vp, vp, vp, f32, f32, vp], i32),
     "hvit_bn_eval_prep": ([vp, vp, i32, f32, vp, vp, vp], i32),
     "hvit_bn_act_fwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, vp], i32),

@@ -300,6 +300,11 @@ extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N,
 extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream) {
   HVIT_CHECK(ws && out && splits > 0, "hvit_sum_slabs: bad args");
   if (n <= 0) return HVIT_OK;
+  if (splits >= 64 && n <= 65536) {
+    // many short slabs (per-workgroup partials): a column reduction of the
+    // [splits][n] matrix spreads the work over all CUs
+    return hvit_reduce_rows(ws, HVIT_F32, splits, n, n, 0, out, stream);
+  }
   if (n % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)out & 15) == 0 && n < (1LL << 31)) {
     hipLaunchKernelGGL(sum_slabs4_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, ws, splits,
                        (int)(n / 4), out);

@@ -61,41 +61,81 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// rows per workgroup for the backward (4 waves x 16 rows)
+// rows per workgroup for the backward (4 waves x 4 rows)
 constexpr int LNB_ROWS = 16;
 
-template <typename TD, int MAXV>
+template <typename TD>
+__device__ __forceinline__ f32x4 load_row4(const TD* p) {
+  if constexpr (sizeof(TD) == 4) {
+    return *(const f32x4*)p;
+  } else {
+    const uint2 u = *(const uint2*)p;
+    return (f32x4){__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                   __uint_as_float(u.y & 0xffff0000u)};
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) (+ resid);
+// dgamma/dbeta partials per workgroup: written to the slab ws[blk][2][D]
+// (SLAB) and summed by ln_slab_sum_kernel, else added atomically.
+template <typename TD, int MAXV, bool SLAB>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, const float* __restrict__ x,
                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                                     const float* __restrict__ g, const float* __restrict__ resid,
                                                     float* __restrict__ dx, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta, int M, int D) {
+                                                    float* __restrict__ dbeta, float* __restrict__ ws, int M, int D) {
   __shared__ float red[4][2][1024];
-  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  f32x4 ag[MAXV], ab[MAXV];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x4 ag[MAXV], ab[MAXV], gam[MAXV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) ag[i] = ab[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int rr = 0; rr < LNB_ROWS / 4; ++rr) {
-    int row = blockIdx.x * LNB_ROWS + w * (LNB_ROWS / 4) + rr;
-    if (row >= M) break;
-    float mu = mean[row], rs = rstd[row];
+  for (int i = 0; i < MAXV; ++i) {
+    ag[i] = ab[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int c = lane * 4 + i * 256;
+    gam[i] = c < D ? *(const f32x4*)(g + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  // the wave's rows are software-pipelined: row r+1's x / dy / resid loads are
+  // issued before row r is reduced and stored
+  const int row0 = blockIdx.x * LNB_ROWS + w * (LNB_ROWS / 4);
+  const int nrows = max(0, min(LNB_ROWS / 4, M - row0));
+  f32x4 xn[MAXV], dn[MAXV], rn[MAXV];
+  auto fetch = [&](int row) {
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane * 4 + i * 256;
+      if (c < D) {
+        xn[i] = *(const f32x4*)(x + (long)row * D + c);
+        dn[i] = load_row4<TD>(dy + (long)row * D + c);
+        rn[i] = resid ? *(const f32x4*)(resid + (long)row * D + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  if (nrows > 0) fetch(row0);
+  for (int rr = 0; rr < nrows; ++rr) {
+    const int row = row0 + rr;
+    f32x4 xv[MAXV], dv[MAXV], rv[MAXV];
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      xv[i] = xn[i];
+      dv[i] = dn[i];
+      rv[i] = rn[i];
+    }
+    if (rr + 1 < nrows) fetch(row + 1);
+    const float mu = mean[row], rs = rstd[row];
     f32x4 xh[MAXV], gy[MAXV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
-      int c = lane * 4 + i * 256;
+      const int c = lane * 4 + i * 256;
       if (c < D) {
-        f32x4 xv = *(const f32x4*)(x + (long)row * D + c);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float d = Elem<TD>::to_f(dy[(long)row * D + c + e]);
-          float xhat = (xv[e] - mu) * rs;
+          const float xhat = (xv[i][e] - mu) * rs;
           xh[i][e] = xhat;
-          gy[i][e] = d * g[c + e];
+          gy[i][e] = dv[i][e] * gam[i][e];
           s1 += gy[i][e];
           s2 += gy[i][e] * xhat;
-          ag[i][e] += d * xhat;
-          ab[i][e] += d;
+          ag[i][e] += dv[i][e] * xhat;
+          ab[i][e] += dv[i][e];
         }
       }
     }
@@ -103,29 +143,59 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     s2 = wave_sum(s2) / (float)D;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
-      int c = lane * 4 + i * 256;
+      const int c = lane * 4 + i * 256;
       if (c < D) {
         f32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = rs * (gy[i][e] - s1 - xh[i][e] * s2);
-        if (resid) o += *(const f32x4*)(resid + (long)row * D + c);
-        *(f32x4*)(dx + (long)row * D + c) = o;
+        *(f32x4*)(dx + (long)row * D + c) = o + rv[i];
       }
     }
   }
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    int c = lane * 4 + i * 256;
-    if (c < D)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { red[w][0][c + e] = ag[i][e]; red[w][1][c + e] = ab[i][e]; }
+    const int c = lane * 4 + i * 256;
+    if (c < D) {
+      *(f32x4*)&red[w][0][c] = ag[i];
+      *(f32x4*)&red[w][1][c] = ab[i];
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += 256) {
-    float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-    float bb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    atomicAdd(dgamma + c, a);
-    atomicAdd(dbeta + c, bb);
+    const float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    const float bb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    if (SLAB) {
+      ws[(size_t)blockIdx.x * 2 * D + c] = a;
+      ws[(size_t)blockIdx.x * 2 * D + D + c] = bb;
+    } else {
+      atomicAdd(dgamma + c, a);
+      atomicAdd(dbeta + c, bb);
+    }
+  }
+}
+
+// dgamma[c] / dbeta[c] = column sums of the slab ws[nblk][2D]; a block owns 64
+// columns, its 4 waves split the slab rows, folded through LDS
+__global__ __launch_bounds__(256) void ln_slab_sum_kernel(const float* __restrict__ ws, int nblk, int D,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float part[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f;
+  if (col < 2 * D) {
+    int k = w;
+    for (; k + 4 < nblk; k += 8) {
+      s0 += ws[(size_t)k * 2 * D + col];
+      s1 += ws[(size_t)(k + 4) * 2 * D + col];
+    }
+    for (; k < nblk; k += 4) s0 += ws[(size_t)k * 2 * D + col];
+  }
+  part[w][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (w == 0 && col < 2 * D) {
+    const float t = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    if (col < D) dgamma[col] = t;
+    else dbeta[col - D] = t;
   }
 }
 
@@ -213,22 +283,44 @@ extern "C" int hvit_layernorm_fwd(const float* x, const float* gamma, const floa
   return HVIT_OK;
 }
 
+extern "C" long long hvit_layernorm_bwd_ws_elems(int M, int D) {
+  return M > 0 ? (long long)cdiv(M, LNB_ROWS) * 2 * D : 0;
+}
+
 extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean,
                                   const float* rstd, const float* gamma, int M, int D, const float* resid,
-                                  float* dx, float* dgamma, float* dbeta, void* stream) {
+                                  float* dx, float* dgamma, float* dbeta, float* ws, long long ws_elems,
+                                  void* stream) {
   HVIT_CHECK(dy && x && mean && rstd && gamma && dx && dgamma && dbeta, "hvit_layernorm_bwd: null pointer");
   HVIT_CHECK(D % 4 == 0 && D <= 1024 && D > 0, "hvit_layernorm_bwd: bad D=%d", D);
-  HVIT_CHECK(aligned16(x) && aligned16(dx) && (!resid || aligned16(resid)), "hvit_layernorm_bwd: alignment");
+  HVIT_CHECK(aligned16(x) && aligned16(dx) && aligned16(gamma) && aligned16(dy) && (!resid || aligned16(resid)),
+             "hvit_layernorm_bwd: alignment");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(dgamma, 0, sizeof(float) * D, st);
-  (void)hipMemsetAsync(dbeta, 0, sizeof(float) * D, st);
+  const int nblk = cdiv(M, LNB_ROWS);
+  const bool slab = M > 0 && ws && ws_elems >= hvit_layernorm_bwd_ws_elems(M, D);
+  if (!slab) {
+    (void)hipMemsetAsync(dgamma, 0, sizeof(float) * D, st);
+    (void)hipMemsetAsync(dbeta, 0, sizeof(float) * D, st);
+  }
   if (M <= 0) return HVIT_OK;
-  dim3 g(cdiv(M, LNB_ROWS));
-#define LNB(TD, V) hipLaunchKernelGGL((ln_bwd_kernel<TD, V>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma, resid, dx, dgamma, dbeta, M, D)
+  dim3 g(nblk);
+#define LNB(TD, V)                                                                                                \
+  do {                                                                                                            \
+    if (slab)                                                                                                     \
+      hipLaunchKernelGGL((ln_bwd_kernel<TD, V, true>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma,  \
+                         resid, dx, dgamma, dbeta, ws, M, D);                                                     \
+    else                                                                                                          \
+      hipLaunchKernelGGL((ln_bwd_kernel<TD, V, false>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma, \
+                         resid, dx, dgamma, dbeta, ws, M, D);                                                     \
+  } while (0)
   if (dy_dt == HVIT_F32) { if (D <= 256) LNB(float, 1); else if (D <= 512) LNB(float, 2); else LNB(float, 4); }
   else { if (D <= 256) LNB(bf16_t, 1); else if (D <= 512) LNB(bf16_t, 2); else LNB(bf16_t, 4); }
 #undef LNB
   HVIT_LAUNCH_CHECK();
+  if (slab) {
+    hipLaunchKernelGGL(ln_slab_sum_kernel, dim3(cdiv(2 * D, 64)), dim3(256), 0, st, ws, nblk, D, dgamma, dbeta);
+    HVIT_LAUNCH_CHECK();
+  }
   return HVIT_OK;
 }
 

@@ -130,7 +130,9 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
 }
 
 // partial[blk][co][tap] = sum over the block's pixels of dz[p][co] * x[p + tap]
-constexpr int WG_PIX = 2048;
+// (pixel chunks sized for >= 4 workgroups per CU at the model's shapes)
+constexpr int WG_PIX = 2048;   // Cin = 1 wgrad (2M pixels at B=32)
+constexpr int WG_PIX_O1 = 256; // Cout = 1 wgrad (131k pixels at B=32)
 template <typename T>
 __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
                                                        float* __restrict__ part, int N, int H, int W, int Cout) {
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
-#pragma unroll 2
+#pragma unroll 4
   for (int p = pbeg + pl; p < pend; p += lanes) {
     float d[8];
     Vec8<T>::load(dz + (size_t)p * Cout + cc * 8, d);
@@ -243,12 +245,13 @@ __global__ __launch_bounds__(256) void o1_wgrad_kernel(const T* __restrict__ x, 
   const int cc = threadIdx.x % CC, lg = threadIdx.x / CC;
   const int H = Hs * U, W = Ws * U;
   const int P = N * H * W;
-  const int pbeg = blockIdx.x * WG_PIX, pend = min(P, pbeg + WG_PIX);
+  const int pbeg = blockIdx.x * WG_PIX_O1, pend = min(P, pbeg + WG_PIX_O1);
   float acc[9][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
+#pragma unroll 2
   for (int p = pbeg + lg; p < pend; p += G) {
     const float d = Elem<TD>::to_f(dz[p]);
     const int n = p / (H * W), rem = p - n * H * W, yy = rem / W, xx = rem - yy * W;
@@ -368,7 +371,7 @@ int hvit_thin_o1_dgrad(int dt, const hvit_conv_geom_t* g, const void* dz, const 
 
 long long hvit_thin_o1_wgrad_ws(const hvit_conv_geom_t* g) {
   const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
-  return (long long)((P + WG_PIX - 1) / WG_PIX) * 9 * g->C1;
+  return (long long)((P + WG_PIX_O1 - 1) / WG_PIX_O1) * 9 * g->C1;
 }
 
 int hvit_thin_o1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
@@ -376,7 +379,7 @@ int hvit_thin_o1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float*
   const int C = g->C1;
   HVIT_CHECK(C % 8 == 0 && C / 8 <= 64 && 64 % (C / 8) == 0, "thin conv wgrad: Cin=%d unsupported", C);
   const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
-  const int nb = (int)((P + WG_PIX - 1) / WG_PIX);
+  const int nb = (int)((P + WG_PIX_O1 - 1) / WG_PIX_O1);
   HVIT_CHECK(ws && ws_elems >= (long long)nb * 9 * C, "thin conv wgrad: workspace too small");
   const size_t smem = 4 * 9 * C * sizeof(float);
   if (dt == HVIT_BF16)

@@ -316,8 +316,17 @@ def test_layernorm(hv, dt, M, D):
     dx = torch.empty(M, D, device=DEV)
     dg = torch.empty(D, device=DEV)
     db = torch.empty(D, device=DEV)
+    ws_n = l.lib().hvit_layernorm_bwd_ws_elems(M, D)
+    ws = torch.empty(ws_n, device="cuda")
     l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), s())
+           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), ws.data_ptr(),
+           ws_n, s())
+    assert rel(dx - resid, x.grad) < 1e-4
+    assert rel(dg, g.grad) < 1e-4
+    assert rel(db, b.grad) < 1e-4
+    # atomic path (no workspace)
+    l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), None, 0, s())
     assert rel(dx - resid, x.grad) < 1e-4
     assert rel(dg, g.grad) < 1e-4
     assert rel(db, b.grad) < 1e-4
