@@ -85,8 +85,9 @@ int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int
 int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, int N, int K, void* dx, int dx_dt,
                       const hvit_epilogue_t* epi, void* stream);                 /* dx[M,K] = dy[M,N] w */
 long long hvit_wgrad_workspace(int M, int N, int K);                              /* f32 elements */
-int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* ws,
-                      long long ws_elems, void* stream);                        /* dw[N,K] = dy^T x */
+int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                      float* ws, long long ws_elems, void* stream);  /* dw[N,K] = dy^T x; db[N] = colsum(dy)
+                                                                        (nullable; fused when db == dw + N*K) */                        /* dw[N,K] = dy^T x */
 
 /* ---- Convolution as implicit GEMM (ConvBlock conv components.py:55-62,
  * TransposeConvBlock upsample+conv components.py:146-158, PatchEmbedding

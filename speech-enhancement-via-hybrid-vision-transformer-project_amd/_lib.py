@@ -53,7 +53,7 @@ _SIGS = {
     "hvit_linear_fwd": ([i32, vp, vp, vp, i32, i32, i32, vp, i32, P(Epilogue), vp], i32),
     "hvit_linear_dgrad": ([i32, vp, vp, i32, i32, i32, vp, i32, P(Epilogue), vp], i32),
     "hvit_wgrad_workspace": ([i32, i32, i32], i64),
-    "hvit_linear_wgrad": ([i32, vp, vp, i32, i32, i32, vp, vp, i64, vp], i32),
+    "hvit_linear_wgrad": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp], i32),
     "hvit_conv_fwd": ([i32, P(ConvGeom), vp, vp, vp, i32, vp, P(Epilogue), vp], i32),
     "hvit_conv_dgrad": ([i32, P(ConvGeom), vp, vp, vp, i32, vp], i32),
     "hvit_conv_wgrad_workspace": ([P(ConvGeom)], i64),

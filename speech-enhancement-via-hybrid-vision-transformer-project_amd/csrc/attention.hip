@@ -466,6 +466,384 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_kernel(const T* __restric
   }
 }
 
+// ============================================================================
+// v2 fast path: bf16, head_dim 64, N <= 256 keys (the HybridViT shapes).
+//
+// The whole K and V (or Q and dO) of one (b, h) live in LDS as row-major
+// [row][64] bf16 images (128-B rows, 16-B chunks XOR-swizzled by row & 7), so
+// every tile is staged once per workgroup with plain 16-byte copies -- no
+// transposed staging.  Scores are computed TRANSPOSED (S^T = K Q^T): the
+// 16x16 MFMA accumulator then holds, per lane, 4 consecutive keys of one
+// query, which is exactly the B-operand layout of v_mfma_f32_16x16x16_bf16,
+// so P^T (and dS^T) feed the next MFMA straight from registers; the other
+// operand (V^T, K^T, dO^T, Q^T) is read with ds_read_b64_tr_b16.  A lane's 4
+// keys also form one dropout-hash group (one 64-bit hash per 16x16 tile).
+// ============================================================================
+constexpr int V2_KMAX = 256;
+constexpr int V2_ROWB = 128;  // bytes per 64-element bf16 row
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+__device__ __forceinline__ int v2_off(int row, int chunk) { return row * V2_ROWB + ((chunk ^ (row & 7)) << 4); }
+
+// rows [0, rows) of a [*, 64] bf16 matrix with element pitch `pitch` -> LDS
+// image (rows >= n zero-filled; `rows` a multiple of 16)
+__device__ __forceinline__ void v2_stage(char* dst, const bf16_t* src, long pitch, int n, int rows) {
+  for (int ch = threadIdx.x; ch < rows * 8; ch += AT_THREADS) {
+    const int r = ch >> 3, c = ch & 7;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r < n) v = *(const u32x4*)(src + (long)r * pitch + c * 8);
+    *(u32x4*)(dst + v2_off(r, c)) = v;
+  }
+}
+// Same image filled by LDS-DMA (global_load_lds_dwordx4): no registers, no
+// per-chunk load->store latency chain.  One wave-instruction writes 1 KiB =
+// 8 rows; the destination is lane-linear, so the XOR swizzle moves to the
+// source address (lane L fetches logical chunk (L%8) ^ row&7 of row 8p + L/8).
+// Rows >= n re-read row n-1 (finite data; every use of those rows is masked or
+// multiplied by an exact zero).  `rows` is a multiple of 8.
+__device__ __forceinline__ void v2_stage_glds(char* dst, const bf16_t* src, long pitch, int n, int rows) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rl = lane >> 3, cp = lane & 7;
+  for (int pc = w; pc < (rows >> 3); pc += AT_THREADS / 64) {
+    const int row = pc * 8 + rl;
+    const int srow = row < n ? row : n - 1;
+    const bf16_t* g = src + (long)srow * pitch + ((cp ^ rl) << 3);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, 0, 0);
+  }
+}
+// 16x16x32 operand fragment: row `row`, k = 32*s + 8*fq .. +7
+__device__ __forceinline__ u32x4 v2_frag(const char* img, int row, int s, int fq) {
+  return *(const u32x4*)(img + v2_off(row, 4 * s + fq));
+}
+// transposed 4-row read: lane (g = lane>>4, i = lane&15) receives
+// img[k0 + 4g + 0..3][c0 + i]  (k0 multiple of 16, c0 multiple of 16)
+__device__ __forceinline__ v4s_t v2_tr(const char* img, int k0, int c0, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int row = k0 + 4 * g + (li >> 2);
+  const int col = c0 + 4 * (li & 3);
+  const char* a = img + row * V2_ROWB + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)a);
+}
+// Per-lane constant parts of the two read patterns (row = 16*j + lane part,
+// and row & 7 depends on the lane part only), so a tile read is one LDS
+// instruction at base + 2048*j + const.
+struct V2Lane {
+  int kc[2];  // v2_frag offsets for s = 0, 1 (row = frow)
+  int tr[4];  // v2_tr offsets for column block t = 0..3 (rows 4g + li/4)
+  __device__ __forceinline__ V2Lane(int lane) {
+    const int frow = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) kc[s2] = frow * V2_ROWB + (((4 * s2 + fq) ^ (frow & 7)) << 4);
+    const int r0 = 4 * fq + (frow >> 2), cb = (frow & 3) >> 1, inner = (frow & 1) * 8;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) tr[t] = r0 * V2_ROWB + (((2 * t + cb) ^ (r0 & 7)) << 4) + inner;
+  }
+};
+__device__ __forceinline__ u32x4 v2_fragj(const char* img, const V2Lane& L, int j, int s2) {
+  return *(const u32x4*)(img + j * 16 * V2_ROWB + L.kc[s2]);
+}
+__device__ __forceinline__ v4s_t v2_trj(const char* img, const V2Lane& L, int j, int t) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(img + j * 16 * V2_ROWB + L.tr[t]));
+}
+__device__ __forceinline__ f32x4 v2_mma32(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, a), __builtin_bit_cast(s16x8, b), c, 0,
+                                                 0, 0);
+}
+__device__ __forceinline__ f32x4 v2_mma16(v4s_t a, v4s_t b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ v4s_t v2_pack(f32x4 v) {
+  uint2 u;
+  u.x = f2bf2(v[0], v[1]);
+  u.y = f2bf2(v[2], v[3]);
+  return __builtin_bit_cast(v4s_t, u);
+}
+// dropout multipliers of 4 consecutive keys kj..kj+3 (kj % 4 == 0) of query qi
+__device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uint32_t thr, float dscale,
+                                         unsigned long long seed, uint32_t site) {
+  const uint64_t idx = (bh * N + qi) * (uint64_t)N + kj;
+  const uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
+  f32x4 k;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) k[e] = ((uint32_t)(h >> (16 * e)) & 0xffffu) >= thr ? dscale : 0.f;
+  return k;
+}
+
+// forward: workgroup = (b, h, 64 queries); wave = 16 queries x all keys
+__global__ __launch_bounds__(AT_THREADS) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                         float* __restrict__ lse, int N, int H, float scale,
+                                                         uint32_t thr, float dscale, unsigned long long seed,
+                                                         uint32_t site) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
+  char* Ks = smem;
+  char* Vs = smem + V2_KMAX * V2_ROWB;
+  const int D = H * 64;
+  const long pitch = 3L * D;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+  const V2Lane LN(lane);
+  const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
+  const int NK = (N + 15) & ~15;
+  const int nkt = NK >> 4;
+  const int q = blockIdx.x * AT_TILE + w * 16 + frow;  // this lane's query
+  u32x4 qf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    qf[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+  v2_stage_glds(Ks, base + D, pitch, N, NK);
+  v2_stage_glds(Vs, base + 2 * D, pitch, N, NK);
+  __syncthreads();
+  const float c2 = scale * 1.4426950408889634f;
+  // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q), log2 units
+  f32x4 st[V2_KMAX / 16];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < V2_KMAX / 16; ++j) {
+    if (j < nkt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      a = v2_mma32(v2_fragj(Ks, LN, j, 0), qf[0], a);
+      a = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], a);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = (16 * j + 4 * fq + r < N) ? a[r] * c2 : -INFINITY;
+        a[r] = v;
+        mx = fmaxf(mx, v);
+      }
+      st[j] = a;
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < V2_KMAX / 16; ++j) {
+    if (j < nkt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(st[j][r] - mx);
+        st[j][r] = p;
+        sum += p;
+      }
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  const uint64_t bh = (uint64_t)b * H + h;
+  // O^T[d][q] += V^T[d][keys] P^T[keys][q]   (4 d-blocks of 16)
+  f32x4 ot[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < V2_KMAX / 16; ++j) {
+    if (j < nkt) {
+      f32x4 p = st[j] * inv;
+      if (thr) p *= v2_keep(bh, N, q < N ? q : 0, 16 * j + 4 * fq, thr, dscale, seed, site);
+      const v4s_t pb = v2_pack(p);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ot[t] = v2_mma16(v2_trj(Vs, LN, j, t), pb, ot[t]);
+    }
+  }
+  if (q < N) {
+    bf16_t* op = o + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint2 u;
+      u.x = f2bf2(ot[t][0], ot[t][1]);
+      u.y = f2bf2(ot[t][2], ot[t][3]);
+      *(uint2*)(op + 16 * t + 4 * fq) = u;
+    }
+    if (fq == 0) lse[bh * N + q] = (mx + log2f(sum)) * 0.6931471805599453f;
+  }
+}
+
+// dQ (+ delta = rowsum(dO * O), written for the dK/dV kernel):
+// workgroup = (b, h, 64 queries); K, V images in LDS
+__global__ __launch_bounds__(AT_THREADS) void mhsa_dq_v2(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+                                                        const bf16_t* __restrict__ dout,
+                                                        const float* __restrict__ lse, float* __restrict__ delta,
+                                                        bf16_t* __restrict__ dqkv, int N, int H, float scale,
+                                                        uint32_t thr, float dscale, unsigned long long seed,
+                                                        uint32_t site) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
+  char* Ks = smem;
+  char* Vs = smem + V2_KMAX * V2_ROWB;
+  const int D = H * 64;
+  const long pitch = 3L * D;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+  const V2Lane LN(lane);
+  const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
+  const int NK = (N + 15) & ~15;
+  const int nkt = NK >> 4;
+  const int q = blockIdx.x * AT_TILE + w * 16 + frow;
+  const bool qv = q < N;
+  const uint64_t bh = (uint64_t)b * H + h;
+  u32x4 qf[2], df[2];
+  float dl = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    qf[s2] = df[s2] = (u32x4){0u, 0u, 0u, 0u};
+    if (qv) {
+      qf[s2] = *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq);
+      df[s2] = *(const u32x4*)(dout + ((long)b * N + q) * D + h * 64 + 32 * s2 + 8 * fq);
+      const u32x4 of = *(const u32x4*)(o + ((long)b * N + q) * D + h * 64 + 32 * s2 + 8 * fq);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dl += __uint_as_float(df[s2][e] << 16) * __uint_as_float(of[e] << 16) +
+              __uint_as_float(df[s2][e] & 0xffff0000u) * __uint_as_float(of[e] & 0xffff0000u);
+    }
+  }
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  if (qv && fq == 0) delta[bh * N + q] = dl;
+  const float lse2 = qv ? lse[bh * N + q] * 1.4426950408889634f : 0.f;
+  v2_stage_glds(Ks, base + D, pitch, N, NK);
+  v2_stage_glds(Vs, base + 2 * D, pitch, N, NK);
+  __syncthreads();
+  const float c2 = scale * 1.4426950408889634f;
+  f32x4 dq[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dq[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int j = 0; j < nkt; ++j) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+    s = v2_mma32(v2_fragj(Ks, LN, j, 0), qf[0], s);
+    s = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], s);
+    dp = v2_mma32(v2_fragj(Vs, LN, j, 0), df[0], dp);
+    dp = v2_mma32(v2_fragj(Vs, LN, j, 1), df[1], dp);
+    const f32x4 keep = thr ? v2_keep(bh, N, qv ? q : 0, 16 * j + 4 * fq, thr, dscale, seed, site)
+                           : (f32x4){1.f, 1.f, 1.f, 1.f};
+    f32x4 ds;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool valid = qv && (16 * j + 4 * fq + r < N);
+      const float p = valid ? exp2f(s[r] * c2 - lse2) : 0.f;
+      ds[r] = p * (dp[r] * keep[r] - dl);
+    }
+    const v4s_t db = v2_pack(ds);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dq[t] = v2_mma16(v2_trj(Ks, LN, j, t), db, dq[t]);
+  }
+  if (qv) {
+    bf16_t* dp_out = dqkv + ((long)b * N + q) * pitch + h * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint2 u;
+      u.x = f2bf2(dq[t][0] * scale, dq[t][1] * scale);
+      u.y = f2bf2(dq[t][2] * scale, dq[t][3] * scale);
+      *(uint2*)(dp_out + 16 * t + 4 * fq) = u;
+    }
+  }
+}
+
+// dK, dV: workgroup = (b, h, 64 keys); wave = 16 keys x all queries;
+// Q, dO images + lse, delta of all queries in LDS
+__global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_v2(const bf16_t* __restrict__ qkv,
+                                                         const bf16_t* __restrict__ dout,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                         int N, int H, float scale, uint32_t thr, float dscale,
+                                                         unsigned long long seed, uint32_t site) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4];
+  char* Qs = smem;
+  char* Ds = smem + V2_KMAX * V2_ROWB;
+  float* Ls = (float*)(smem + 2 * V2_KMAX * V2_ROWB);
+  float* Dl = Ls + V2_KMAX;
+  const int D = H * 64;
+  const long pitch = 3L * D;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+  const V2Lane LN(lane);
+  const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
+  const int NQ = (N + 15) & ~15;
+  const int nqt = NQ >> 4;
+  const int key = blockIdx.x * AT_TILE + w * 16 + frow;  // this lane's key (B operand column)
+  const bool kv = key < N;
+  const uint64_t bh = (uint64_t)b * H + h;
+  u32x4 kf[2], vf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    kf[s2] = kv ? *(const u32x4*)(base + D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+    vf[s2] = kv ? *(const u32x4*)(base + 2 * D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+  }
+  v2_stage_glds(Qs, base, pitch, N, NQ);
+  v2_stage_glds(Ds, dout + (long)b * N * D + h * 64, D, N, NQ);
+  for (int i = threadIdx.x; i < NQ; i += AT_THREADS) {
+    Ls[i] = i < N ? lse[bh * N + i] * 1.4426950408889634f : 0.f;
+    Dl[i] = i < N ? delta[bh * N + i] : 0.f;
+  }
+  __syncthreads();
+  const float c2 = scale * 1.4426950408889634f;
+  // accumulators: rows = d (16t + 4fq + r), column = this lane's key
+  f32x4 dkt[4], dvt[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dkt[t] = dvt[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+  for (int j = 0; j < nqt; ++j) {
+    // S^T-free form: S[q][key] with m = queries 16j + 4fq + r, n = key (lane)
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+    s = v2_mma32(v2_fragj(Qs, LN, j, 0), kf[0], s);
+    s = v2_mma32(v2_fragj(Qs, LN, j, 1), kf[1], s);
+    dp = v2_mma32(v2_fragj(Ds, LN, j, 0), vf[0], dp);
+    dp = v2_mma32(v2_fragj(Ds, LN, j, 1), vf[1], dp);
+    // dropout: lane (quad position c = key & 3) hashes query row 16j+4fq+c of
+    // its key group; the quad exchanges the 16-bit slices (4 queries x 4 keys)
+    uint32_t hlo = 0u, hhi = 0u;
+    if (thr) {
+      const int qc = 16 * j + 4 * fq + (frow & 3);
+      const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
+      const uint64_t hv = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
+      hlo = (uint32_t)hv;
+      hhi = (uint32_t)(hv >> 32);
+    }
+    f32x4 pd, ds;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qi = 16 * j + 4 * fq + r;
+      const bool valid = kv && qi < N;
+      const float p = valid ? exp2f(s[r] * c2 - Ls[qi]) : 0.f;
+      float kp = 1.f;
+      if (thr) {
+        const int src = (lane & ~3) | r;
+        const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
+        const uint32_t word = (key & 2) ? hi : lo;
+        const uint32_t u16 = (key & 1) ? (word >> 16) : (word & 0xffffu);
+        kp = (valid && u16 >= thr) ? dscale : 0.f;
+      }
+      pd[r] = p * kp;
+      ds[r] = p * (dp[r] * kp - Dl[qi]);
+    }
+    // dV^T[d][key] += dO^T[d][q] P~[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+    const v4s_t pb = v2_pack(pd), sb = v2_pack(ds);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dvt[t] = v2_mma16(v2_trj(Ds, LN, j, t), pb, dvt[t]);
+      dkt[t] = v2_mma16(v2_trj(Qs, LN, j, t), sb, dkt[t]);
+    }
+  }
+  if (kv) {
+    bf16_t* row = dqkv + ((long)b * N + key) * pitch + h * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint2 u;
+      u.x = f2bf2(dkt[t][0] * scale, dkt[t][1] * scale);
+      u.y = f2bf2(dkt[t][2] * scale, dkt[t][3] * scale);
+      *(uint2*)(row + D + 16 * t + 4 * fq) = u;
+      u.x = f2bf2(dvt[t][0], dvt[t][1]);
+      u.y = f2bf2(dvt[t][2], dvt[t][3]);
+      *(uint2*)(row + 2 * D + 16 * t + 4 * fq) = u;
+    }
+  }
+}
+
+static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 && N <= V2_KMAX && N % 4 == 0; }
+
 // ------------------------------------------------------------------- host ---
 template <typename T, int HD>
 static int mhsa_fwd_t(const void* qkv, void* o, float* lse, float* probs, int B, int N, int H,
@@ -531,6 +909,15 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
   HVIT_CHECK(aligned16(qkv) && aligned16(o), "hvit_mhsa_fwd: qkv/o must be 16-byte aligned");
   HVIT_CHECK(dt == HVIT_F32 || dt == HVIT_BF16, "hvit_mhsa_fwd: bad dtype");
   hipStream_t st = (hipStream_t)stream;
+  if (v2_ok(dt, hd, N) && !probs) {
+    const hvit_dropout_t* dr = dropout;
+    const uint32_t thr = dr ? drop_threshold(dr->p) : 0;
+    const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
+    hipLaunchKernelGGL(mhsa_fwd_v2, dim3(cdiv(N, AT_TILE), H, B), dim3(AT_THREADS), 0, st, (const bf16_t*)qkv,
+                       (bf16_t*)o, lse, N, H, scale, thr, ds, dr ? dr->seed : 0ull, dr ? dr->site : 0u);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   HVIT_HD_DISPATCH(mhsa_fwd_t, qkv, o, lse, probs, B, N, H, scale, dropout, st);
 }
 
@@ -544,5 +931,20 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
              "hvit_mhsa_bwd: tensors must be 16-byte aligned");
   HVIT_CHECK(dt == HVIT_F32 || dt == HVIT_BF16, "hvit_mhsa_bwd: bad dtype");
   hipStream_t st = (hipStream_t)stream;
+  if (v2_ok(dt, hd, N)) {
+    const hvit_dropout_t* dr = dropout;
+    const uint32_t thr = dr ? drop_threshold(dr->p) : 0;
+    const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
+    const unsigned long long seed = dr ? dr->seed : 0ull;
+    const uint32_t site = dr ? dr->site : 0u;
+    dim3 g(cdiv(N, AT_TILE), H, B);
+    hipLaunchKernelGGL(mhsa_dq_v2, g, dim3(AT_THREADS), 0, st, (const bf16_t*)qkv, (const bf16_t*)o,
+                       (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+    HVIT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(mhsa_dkv_v2, g, dim3(AT_THREADS), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
+                       (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   HVIT_HD_DISPATCH(mhsa_bwd_t, qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, dropout, st);
 }

@@ -297,6 +297,30 @@ extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N,
   return HVIT_OK;
 }
 
+// out[i] = sum_k ws[k * stride + i], i < n (slabs of `stride` elements)
+__global__ void sum_slabs_strided_kernel(const float* ws, int splits, long stride, long n, float* out) {
+  GRID_STRIDE(i, n) {
+    float s0 = 0.f, s1 = 0.f;
+    int k = 0;
+    for (; k + 1 < splits; k += 2) {
+      s0 += ws[(long)k * stride + i];
+      s1 += ws[(long)(k + 1) * stride + i];
+    }
+    if (k < splits) s0 += ws[(long)k * stride + i];
+    out[i] = s0 + s1;
+  }
+}
+
+int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream) {
+  if (stride == n) return hvit_sum_slabs(ws, splits, n, out, stream);
+  HVIT_CHECK(ws && out && splits > 0 && stride >= n, "hvit_sum_slabs_strided: bad args");
+  if (n <= 0) return HVIT_OK;
+  hipLaunchKernelGGL(sum_slabs_strided_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, splits,
+                     (long)stride, (long)n, out);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
 extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream) {
   HVIT_CHECK(ws && out && splits > 0, "hvit_sum_slabs: bad args");
   if (n <= 0) return HVIT_OK;

@@ -231,6 +231,9 @@ struct Epi {
   int rows_per_sample = 1;
   float* stats = nullptr;   // BN partials [64-row tile][N][2] = (mean, M2)
   float* colsum = nullptr;  // atomic column sums of the final v
+  long slab_stride = 0;     // EPI_SLAB: elements between split-K slabs (0: M * ldo)
+  float* rs_ptr = nullptr;  // row sums of the A operand (wgrad bias grad): rs_ptr[z * rs_stride + m]
+  long rs_stride = 0;
   bool vec_ok = false;      // N % 4 == 0, every operand 16-B aligned with ld % 4 == 0
   // EPI_PATCH: m = token (b, py, px) of Hp x Wp, n = (ky*P + kx)*C + c
   int pP = 0, pC = 0, pHp = 0, pWp = 0, pH = 0, pW = 0;
@@ -493,9 +496,14 @@ struct GemmCore {
   static constexpr int SM_LOOP = 2 * (TA::BYTES + TB::BYTES);
 
   // the K loop: acc += A[m0.., kbeg..kend) * B[n0.., kbeg..kend)^T
-  template <bool CHECK>
+  // RS: also accumulate row sums of the A tile (bf16 k-major A only: the
+  // wgrad dy operand, whose row sums over the token reduction are the bias
+  // gradient); rs_on is uniform (only the blocks of the first N tile)
+  static constexpr int RS_RG = BM / 8, RS_KG = GEMM_THREADS / RS_RG, RS_KPG = BK / RS_KG;
+  template <bool CHECK, bool RS = false>
   __device__ __forceinline__ static void run(const LA& la, const LB& lb, char* smem, int m0, int n0, int kbeg,
-                                             int kend, f32x4 (&acc)[FM][FN]) {
+                                             int kend, f32x4 (&acc)[FM][FN], float* rsacc = nullptr,
+                                             bool rs_on = false) {
     char* As = smem;
     char* Bs = smem + 2 * TA::BYTES;
     const int tid = threadIdx.x;
@@ -582,6 +590,24 @@ struct GemmCore {
       }
     };
 
+    auto rowsum = [&](int buf) {
+      if constexpr (RS) {
+        static_assert(TA::TR, "row sums need the k-major bf16 A tile");
+        if (!rs_on) return;
+        const char* at = As + buf * TA::BYTES;
+        const int rg = tid % RS_RG, kg = tid / RS_RG;
+#pragma unroll
+        for (int i = 0; i < RS_KPG; ++i) {
+          const u32x4 v = *(const u32x4*)(at + MnTile<BM>::off(kg * RS_KPG + i, rg * 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            rsacc[2 * e] += __uint_as_float(v[e] << 16);
+            rsacc[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+          }
+        }
+      }
+    };
+
     // prologue: stage 0 -> regs0 -> LDS0; stage 1 -> regs1 (in flight)
     fetch(ra0, rb0);
     fetch(ra1, rb1);
@@ -591,12 +617,14 @@ struct GemmCore {
       // even stage t in LDS0; stage t+1 in regs1; prefetch stage t+2 -> regs0
       fetch(ra0, rb0);
       compute(0);
+      rowsum(0);
       if (t + 1 < nk) stash(ra1, rb1, 1);
       __syncthreads();
       if (t + 1 >= nk) break;
       // odd stage t+1 in LDS1; stage t+2 in regs0; prefetch stage t+3 -> regs1
       fetch(ra1, rb1);
       compute(1);
+      rowsum(1);
       if (t + 2 < nk) stash(ra0, rb0, 0);
       __syncthreads();
     }
@@ -622,7 +650,7 @@ extern __device__ unsigned long long g_gemm_stamps[65536 * 4];
 #ifndef HVIT_BIG_OCC
 #define HVIT_BIG_OCC 2
 #endif
-template <typename T, int BM, int BN, class LA, class LB, int EK>
+template <typename T, int BM, int BN, class LA, class LB, int EK, bool RS = false>
 __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
                                                                                             int K, int kps, Epi ep) {
   using C = GemmCore<T, BM, BN, LA, LB>;
@@ -664,8 +692,25 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
 
   GEMM_STAMP(0);
   const bool interior = m0 + BM <= M && n0 + BN <= N && ((kend - kbeg) % C::BK) == 0 && la.fast() && lb.fast();
-  if (interior) C::template run<false>(la, lb, smem, m0, n0, kbeg, kend, acc);
-  else C::template run<true>(la, lb, smem, m0, n0, kbeg, kend, acc);
+  float rsacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool rs_on = RS && blockIdx.y == 0;
+  if (interior) C::template run<false, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
+  else C::template run<true, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
+  if constexpr (RS) {
+    if (rs_on) {  // fold the k-groups: red[kg][BM]
+      float* red = (float*)smem;
+      const int rg = tid % C::RS_RG, kg = tid / C::RS_RG;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[kg * BM + rg * 8 + e] = rsacc[e];
+      __syncthreads();
+      if (tid < BM && m0 + tid < M) {
+        float sum = 0.f;
+        for (int k = 0; k < C::RS_KG; ++k) sum += red[k * BM + tid];
+        ep.rs_ptr[(long)blockIdx.z * ep.rs_stride + m0 + tid] = sum;
+      }
+      __syncthreads();
+    }
+  }
   GEMM_STAMP(1);
   // Retire every outstanding global load here (the bias, and the K loop's
   // never-consumed tail prefetches) with one explicit wait that the compiler's
@@ -712,7 +757,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
           const int m = mbase + row;
           if (PRED && (m >= M || !nok)) continue;
           const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
-          float* slab = (float*)ep.out + (long)blockIdx.z * M * ep.ldo + (long)m * ep.ldo + n;
+          float* slab = (float*)ep.out + (long)blockIdx.z * ep.slab_stride + (long)m * ep.ldo + n;
           if (!PRED || (full && (ep.ldo & 3) == 0)) *(f32x4*)slab = v;
           else store4_slow(slab, 0, v, nv, HVIT_F32);
         }
@@ -892,6 +937,7 @@ template <typename T, class LA, class LB>
 int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in, hipStream_t st,
                 int force_tile = 0) {
   Epi ep = ep_in;
+  if (ep.slab_stride == 0) ep.slab_stride = (long)M * ep.ldo;
   auto vok = [](const void* p, long ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
   ep.vec_ok = N % 4 == 0 && vok(ep.out, ep.ldo) && vok(ep.out2, ep.ldo2) && vok(ep.aux, ep.ldaux) &&
               vok(ep.resid, ep.ldr) && vok(ep.rowadd, ep.rowadd_ld);
@@ -924,20 +970,35 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
       else if (ep.act == ACT_GELU_BWD && !ep.resid && ep.aux) ek = EK_GELU_BWD;
     }
   }
+  // A-row sums (bias grad) only exist for the bf16 k-major A operand (wgrad)
+  constexpr bool RS_OK = !LA::KC && sizeof(T) == 2;
+  if (ep.rs_ptr && !RS_OK) {
+    hvit_set_error("launch_gemm: A row sums need a bf16 k-major A operand");
+    return HVIT_ERR_ARG;
+  }
   auto go = [&](auto ekc) {
     constexpr int EKc = decltype(ekc)::value;
-    if (tile == 128) {
-      dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
-      hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB, EKc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N, K, kps,
-                         ep);
-    } else if (tile == 12864) {
-      dim3 g(cdiv(M, 128), cdiv(N, 64), splits);
-      hipLaunchKernelGGL((gemm_kernel<T, 128, 64, LA, LB, EKc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N, K, kps,
-                         ep);
+    auto launch = [&](auto rsc) {
+      constexpr bool RSc = decltype(rsc)::value && RS_OK;
+      if (tile == 128) {
+        dim3 g(cdiv(M, 128), cdiv(N, 128), splits);
+        hipLaunchKernelGGL((gemm_kernel<T, 128, 128, LA, LB, EKc, RSc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N,
+                           K, kps, ep);
+      } else if (tile == 12864) {
+        dim3 g(cdiv(M, 128), cdiv(N, 64), splits);
+        hipLaunchKernelGGL((gemm_kernel<T, 128, 64, LA, LB, EKc, RSc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N,
+                           K, kps, ep);
+      } else {
+        dim3 g(cdiv(M, 64), cdiv(N, 64), splits);
+        hipLaunchKernelGGL((gemm_kernel<T, 64, 64, LA, LB, EKc, RSc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N,
+                           K, kps, ep);
+      }
+    };
+    if constexpr (RS_OK && (EKc == EK_SLAB || EKc == EK_STORE)) {
+      if (ep.rs_ptr) launch(std::true_type());
+      else launch(std::false_type());
     } else {
-      dim3 g(cdiv(M, 64), cdiv(N, 64), splits);
-      hipLaunchKernelGGL((gemm_kernel<T, 64, 64, LA, LB, EKc>), g, dim3(GEMM_THREADS), 0, st, la, lb, M, N, K, kps,
-                         ep);
+      launch(std::false_type());
     }
   };
   switch (ek) {

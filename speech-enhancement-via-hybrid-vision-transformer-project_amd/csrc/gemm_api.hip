@@ -132,6 +132,7 @@ bool thin_o1(const hvit_conv_geom_t* g) {
 }  // namespace
 
 int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats, hipStream_t st);
+int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream);
 long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g);
 int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
                        hipStream_t st);
@@ -183,26 +184,31 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
 }
 
 extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
-  // dw is [N_out x K_in] reduced over M rows ; slabs only when splitting
+  // dw is [N_out x K_in] reduced over M rows; slabs only when splitting, each
+  // slab followed by N_out bias partials
   int s = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
-  return s > 1 ? (long long)s * N * K : 0;
+  return s > 1 ? (long long)s * ((long long)N * K + N) : 0;
 }
 
-extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* ws,
-                                 long long ws_elems, void* stream) {
+// db (nullable): bias gradient sum_m dy[m][n].  The fused path (bf16, db ==
+// dw + N*K) takes it from the A tiles the wgrad GEMM already stages (row sums
+// over the token reduction); otherwise a column reduction of dy.
+extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                                 float* ws, long long ws_elems, void* stream) {
   HVIT_CHECK(dy && x && dw, "hvit_linear_wgrad: null pointer");
   HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_wgrad: bad shape");
   HVIT_CHECK(aligned16(dy) && aligned16(x), "hvit_linear_wgrad: alignment");
   hipStream_t st = (hipStream_t)stream;
+  const long long NK = (long long)N * K;
   int splits = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
-  if ((long long)splits * N * K > ws_elems || !ws) splits = 1;
+  if ((long long)splits * (NK + N) > ws_elems || !ws) splits = 1;
   if (M == 0) {
-    (void)hipMemsetAsync(dw, 0, sizeof(float) * N * K, st);
+    (void)hipMemsetAsync(dw, 0, sizeof(float) * NK, st);
+    if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return HVIT_OK;
   }
+  const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK;
   Epi ep;
-  ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
-  ep.out = splits > 1 ? (void*)ws : (void*)dw;
   ep.out_dt = HVIT_F32;
   ep.ldo = K;
   DT_DISPATCH(dt, {
@@ -210,11 +216,20 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
     splits = plan_splits<T>(M, splits);
     ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
     ep.out = splits > 1 ? (void*)ws : (void*)dw;
+    ep.slab_stride = NK + N;
+    if (fused_db) {
+      ep.rs_ptr = splits > 1 ? ws + NK : db;
+      ep.rs_stride = splits > 1 ? NK + N : 0;
+    }
     int rc = launch_gemm<T>(dense<T, false>(dy, N, N, M), dense<T, false>(x, K, K, M), N, K, M, splits, ep, st,
                             LIN_WG_TILE);
     if (rc) return rc;
   });
-  if (splits > 1) return hvit_sum_slabs(ws, splits, (long long)N * K, dw, stream);
+  if (splits > 1) {
+    // sums [dw | db] when fused (db follows dw), else dw alone
+    if (int rc = hvit_sum_slabs_strided(ws, splits, NK + N, fused_db ? NK + N : NK, dw, stream)) return rc;
+  }
+  if (db && !fused_db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
   return HVIT_OK;
 }
 

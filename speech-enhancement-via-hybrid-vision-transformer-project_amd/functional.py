@@ -58,13 +58,17 @@ def col_sum(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
     return out
 
 
-def linear_wgrad(dt, dy, x, M, N, K) -> torch.Tensor:
-    dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+def linear_wgrad(dt, dy, x, M, N, K, bias=False):
+    """dw [N, K] = dy^T x (f32); with ``bias`` also db [N] = colsum(dy), which
+    the bf16 path fuses into the GEMM (db stored right after dw)."""
+    buf = torch.empty(N * K + (N if bias else 0), dtype=torch.float32, device=dy.device)
+    dw = buf[:N * K].view(N, K)
+    db = buf[N * K:] if bias else None
     ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
-    call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), ws_n,
+    call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db), ws.data_ptr(), ws_n,
          stream_ptr())
-    return dw
+    return (dw, db) if bias else dw
 
 
 def epilogue(act=L.ACT_NONE, out2=None, aux=None, drop=None, resid=None, rowscale=None, rps=1, rowadd=None,
@@ -342,8 +346,7 @@ class ViTBlockFn(torch.autograd.Function):
         # MLP branch
         g2 = _empty((M, D), dt, dev)
         call("hvit_dropout_scale", dx2.data_ptr(), F32, M, D, drf2, ptr(rs2), Nt, g2.data_ptr(), dt, s)
-        df2b = col_sum(g2, M, D)
-        df2w = linear_wgrad(dt, g2, a, M, D, hid)
+        df2w, df2b = linear_wgrad(dt, g2, a, M, D, hid, bias=True)
         dh = _empty((M, hid), dt, dev)
         df1b = torch.zeros(hid, dtype=torch.float32, device=dev)  # fc1 bias grad: fused column sum
         call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
@@ -355,16 +358,14 @@ class ViTBlockFn(torch.autograd.Function):
         # attention branch
         g1 = _empty((M, D), dt, dev)
         call("hvit_dropout_scale", dx1.data_ptr(), F32, M, D, drp, ptr(rs1), Nt, g1.data_ptr(), dt, s)
-        dpb = col_sum(g1, M, D)
-        dpw = linear_wgrad(dt, g1, o, M, D, D)
+        dpw, dpb = linear_wgrad(dt, g1, o, M, D, D, bias=True)
         do = _empty((M, D), dt, dev)
         call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H, D // H,
              scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
-        dqkvb = col_sum(dqkv, M, 3 * D)
-        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D)
+        dqkvw, dqkvb = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, bias=True)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None, s)
         dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1)
@@ -400,8 +401,7 @@ class HeadFn(torch.autograd.Function):
         B, Nt, D, C, dt = ctx.meta
         M = B * Nt
         dy = cast(dy, dt)
-        db = col_sum(dy, M, C)
-        dw = linear_wgrad(dt, dy, xn, M, C, D)
+        dw, db = linear_wgrad(dt, dy, xn, M, C, D, bias=True)
         dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
         call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32, None,
              stream_ptr())
@@ -442,8 +442,8 @@ class SkipFn(torch.autograd.Function):
         dev = r.device
         s = stream_ptr()
         dy = cast(dy, dt)
-        db = col_sum(dy, M, Cd)
-        dw = linear_wgrad(dt, dy, r, M, Cd, Ce).view(wshape)
+        dw, db = linear_wgrad(dt, dy, r, M, Cd, Ce, bias=True)
+        dw = dw.view(wshape)
         de = None
         if ctx.needs_input_grad[0]:
             dr = _empty((N, Ho, Wo, Ce), dt, dev)

@@ -117,10 +117,26 @@ def test_linear_wgrad(hv, dt, M, N, K):
     dw = torch.empty(N, K, device=DEV)
     ws_n = l.lib().hvit_wgrad_workspace(M, N, K)
     ws = torch.empty(max(ws_n, 1), device=DEV)
-    l.call("hvit_linear_wgrad", l.dt_of(dy), dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(),
-           ws_n, s())
+    l.call("hvit_linear_wgrad", l.dt_of(dy), dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), None,
+           ws.data_ptr(), ws_n, s())
     ref = dy.float().t() @ x.float()
-    assert rel(dw, ref) < (1e-4 if dt == "f32" else 2e-2)
+    tol_w = 1e-4 if dt == "f32" else 2e-2
+    assert rel(dw, ref) < tol_w
+    # with the bias gradient: fused (db right after dw) and separate
+    buf = torch.empty(N * K + N, device=DEV)
+    l.call("hvit_linear_wgrad", l.dt_of(dy), dy.data_ptr(), x.data_ptr(), M, N, K, buf.data_ptr(),
+           buf[N * K:].data_ptr(), ws.data_ptr(), ws_n, s())
+    assert rel(buf[:N * K].view(N, K), ref) < tol_w
+    assert rel(buf[N * K:], dy.float().sum(0)) < (1e-4 if dt == "f32" else 1e-2)
+    db = torch.empty(N, device=DEV)
+    l.call("hvit_linear_wgrad", l.dt_of(dy), dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), db.data_ptr(),
+           ws.data_ptr(), ws_n, s())
+    assert rel(db, dy.float().sum(0)) < (1e-4 if dt == "f32" else 1e-2)
+    # no workspace (single split)
+    l.call("hvit_linear_wgrad", l.dt_of(dy), dy.data_ptr(), x.data_ptr(), M, N, K, buf.data_ptr(),
+           buf[N * K:].data_ptr(), None, 0, s())
+    assert rel(buf[:N * K].view(N, K), ref) < tol_w
+    assert rel(buf[N * K:], dy.float().sum(0)) < (1e-4 if dt == "f32" else 1e-2)
 
 
 def test_reduce_rows_and_cast(hv):
@@ -281,6 +297,15 @@ def test_mhsa_fwd_bwd(hv, dt, B, N, H, hd, p):
            probs.data_ptr(), s())
     assert rel(o.float(), o_ref) < tol(dt)
     assert rel(probs, a_ref) < tol(dt)
+    # without return_attentions (the training path: bf16 / hd 64 / N <= 256 take
+    # the register-resident S^T kernels)
+    o2 = torch.empty_like(o)
+    lse2 = torch.empty_like(lse)
+    l.call("hvit_mhsa_fwd", dtc, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o2.data_ptr(), lse2.data_ptr(),
+           None, s())
+    assert rel(o2.float(), o_ref) < tol(dt)
+    assert rel(lse2, lse) < 1e-3
+    o, lse = o2, lse2
     go = torch.randn_like(o_ref)
     o_ref.backward(go)
     gq = go.to(tdt(dt)).contiguous()

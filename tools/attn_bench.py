@@ -1,0 +1,43 @@
+"""Attention micro-benchmark at the HybridViT shape (B=32, N=256, H=8, hd=64,
+bf16, attention dropout 0.1): fwd and bwd timed with HIP events."""
+
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import hvit_amd_loader  # noqa: E402
+from gemm_bench import timeit  # noqa: E402
+
+hv = hvit_amd_loader.load()
+L = hv._lib
+
+
+def main(p=0.1):
+    B, N, H, hd = 32, 256, 8, 64
+    D = H * hd
+    qkv = (torch.randn(B * N, 3 * D, device="cuda") * 0.7).to(torch.bfloat16)
+    o = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device="cuda")
+    dr = L.dropout(p, 1, 2)
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    fwd = lambda: L.call("hvit_mhsa_fwd", L.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(),  # noqa
+                         lse.data_ptr(), None, st())
+    us = timeit(fwd)
+    fl = 4 * B * H * N * N * hd
+    print(f"mhsa fwd p={p}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s", flush=True)
+    do = torch.randn_like(o)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty(B, H, N, device="cuda")
+    bwd = lambda: L.call("hvit_mhsa_bwd", L.BF16, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),  # noqa
+                         B, N, H, hd, hd ** -0.5, dr, dqkv.data_ptr(), delta.data_ptr(), st())
+    us = timeit(bwd)
+    print(f"mhsa bwd p={p}: {us:7.1f} us  {2 * fl / us / 1e6:6.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main(0.1)
+    main(0.0)

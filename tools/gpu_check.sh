@@ -13,6 +13,7 @@ for s in $STEPS; do
     tests) bash tools/gpu_tests.sh tests/test_gpu_kernels.py tests/test_gpu_model.py > gpurun_out/${TAG}_tests.log 2>&1 || exit $? ;;
     gemm) timeout -k 10 240 python tools/gemm_bench.py > gpurun_out/${TAG}_gemm.log 2>&1 || exit $? ;;
     stamps) HVIT_LIB=libhvit_stamps.so timeout -k 10 120 python tools/gemm_stamps.py > gpurun_out/${TAG}_stamps.log 2>&1 || exit $? ;;
+    attn) timeout -k 10 120 python tools/attn_bench.py > gpurun_out/${TAG}_attn.log 2>&1 || exit $? ;;
     probe) timeout -k 10 240 python tools/gemm_probe.py > gpurun_out/${TAG}_probe.log 2>&1 || exit $? ;;
     bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_bench.log 2>&1 || exit $? ;;
     fullbench) timeout -k 10 400 python bench.py > gpurun_out/${TAG}_fullbench.log 2>&1 || exit $? ;;
