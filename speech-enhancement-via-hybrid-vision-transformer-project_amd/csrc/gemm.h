@@ -195,6 +195,74 @@ struct LdConv {
   }
 };
 
+// Fast implicit-im2col A loader (bf16, KC role only) for the common case
+// where every K stage (64 channels) lies inside one tap and one source:
+// C1 % 64 == 0 and C2 % 64 == 0.  The tap / channel state of a stage is then
+// wave-uniform (SGPRs: the stage base is readfirstlane'd), the per-chunk state
+// is the pixel's (row base, iy0, ix0), and reads go through buffer loads with a
+// 32-bit byte offset: taps in the zero padding, or pixels past the end (row
+// base beyond the tensor), get an offset past num_records and read zeros --
+// no per-element selects or 64-bit address math.
+template <typename T>
+struct LdConvF {
+  static constexpr bool KC = true;
+  static constexpr int E = Elem<T>::PER16;
+  const T* src1;
+  const T* src2;
+  int C1, C2, Ctot;
+  int Hs, Ws, Hi, Wi, ushift;  // source dims, conv-input dims, log2(U)
+  int KS, S, Pd;
+  int Ho, Wo, P, Kt;
+  unsigned bytes1, bytes2;     // buffer extents
+
+  __device__ __forceinline__ bool fast() const { return true; }
+  struct Sh {
+    int c0, kx, ky;  // stage tap (uniform)
+    int klane;       // this thread's channel offset inside the stage
+  };
+  struct Cur {
+    int rb, iy0, ix0;  // n*Hs (source row base), oy*S - Pd, ox*S - Pd
+  };
+  __device__ __forceinline__ void init(Sh& sh, Cur& cu, int a, int b) const {
+    const int hw = Ho * Wo;
+    const int n = a / hw, rem = a - n * hw;
+    const int oy = rem / Wo, ox = rem - oy * Wo;
+    cu.rb = n * Hs;
+    cu.iy0 = oy * S - Pd;
+    cu.ix0 = ox * S - Pd;
+    const int kb = __builtin_amdgcn_readfirstlane(b & ~63);
+    sh.klane = b & 63;
+    const int tap = kb / Ctot;
+    sh.c0 = kb - tap * Ctot;
+    sh.ky = tap / KS;
+    sh.kx = tap - sh.ky * KS;
+  }
+  __device__ __forceinline__ void step_sh(Sh& sh, int bk) const {
+    sh.c0 += bk;
+    if (sh.c0 >= Ctot) {
+      sh.c0 -= Ctot;
+      if (++sh.kx == KS) {
+        sh.kx = 0;
+        ++sh.ky;
+      }
+    }
+  }
+  __device__ __forceinline__ void step(Cur&, int) const {}
+  template <bool CHECK>
+  __device__ __forceinline__ u32x4 fetch(const Sh& sh, const Cur& cu) const {
+    const bool first = sh.c0 < C1;  // uniform
+    const int Cx = first ? C1 : C2;
+    const int coff = (first ? sh.c0 : sh.c0 - C1) + sh.klane;
+    const int iy = cu.iy0 + sh.ky, ix = cu.ix0 + sh.kx;
+    const bool ok = (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+    const int off = (((cu.rb + (iy >> ushift)) * Ws + (ix >> ushift)) * Cx + coff) * (int)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(first ? src1 : src2), (short)0, (int)(first ? bytes1 : bytes2), 0x00020000);
+    const unsigned voff = ok ? (unsigned)off : 0x80000000u;
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+  }
+};
+
 // ------------------------------------------------------------ epilogue -------
 enum EpiMode { EPI_STORE = 0, EPI_SLAB = 1, EPI_PATCH = 2, EPI_SPLIT2 = 3 };
 enum EpiAct { ACT_NONE = 0, ACT_GELU_DUAL = 1, ACT_TANH = 2, ACT_GELU_BWD = 3 };
@@ -920,6 +988,11 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
 
 
 // host-side launcher --------------------------------------------------------
+template <class X>
+struct IsDenseKC : std::false_type {};
+template <typename T>
+struct IsDenseKC<LdDense<T, true>> : std::true_type {};
+
 // Effective split-K count after rounding each split to whole K-tiles (never
 // more than requested).  Callers that reduce slabs must use this count.
 template <typename T>
@@ -964,7 +1037,7 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
     const bool full_tiles = ep.vec_ok && M % bm == 0 && N % bn == 0 && ep.mode == EPI_STORE && !ep.rowadd &&
                             !ep.stats;
     const bool drop_ok = ep.drop_thr ? N % 4 == 0 : ep.drop_scale == 1.f;
-    if (ek == EK_GEN && full_tiles && drop_ok) {
+    if (IsDenseKC<LA>::value && ek == EK_GEN && full_tiles && drop_ok) {
       if (ep.act == ACT_GELU_DUAL && !ep.resid) ek = EK_GELU_DUAL;
       else if (ep.act == ACT_NONE && ep.resid && ep.resid != ep.out) ek = EK_RESID;
       else if (ep.act == ACT_GELU_BWD && !ep.resid && ep.aux) ek = EK_GELU_BWD;
@@ -1004,9 +1077,15 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
   switch (ek) {
     case EK_SLAB: go(std::integral_constant<int, EK_SLAB>()); break;
     case EK_STORE: go(std::integral_constant<int, EK_STORE>()); break;
-    case EK_GELU_DUAL: go(std::integral_constant<int, EK_GELU_DUAL>()); break;
-    case EK_RESID: go(std::integral_constant<int, EK_RESID>()); break;
-    case EK_GELU_BWD: go(std::integral_constant<int, EK_GELU_BWD>()); break;
+    case EK_GELU_DUAL:
+      if constexpr (IsDenseKC<LA>::value) go(std::integral_constant<int, EK_GELU_DUAL>());
+      break;
+    case EK_RESID:
+      if constexpr (IsDenseKC<LA>::value) go(std::integral_constant<int, EK_RESID>());
+      break;
+    case EK_GELU_BWD:
+      if constexpr (IsDenseKC<LA>::value) go(std::integral_constant<int, EK_GELU_BWD>());
+      break;
     default: go(std::integral_constant<int, EK_GEN>()); break;
   }
   HVIT_LAUNCH_CHECK();

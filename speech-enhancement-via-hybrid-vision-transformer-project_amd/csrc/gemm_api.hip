@@ -99,6 +99,40 @@ LdConv<T, true> conv_a(const hvit_conv_geom_t* g, const void* s1, int C1, const 
   return l;
 }
 
+// the fast loader applies when every 64-channel stage stays inside one tap
+// and one source, U is 1 or 2, and byte offsets fit 31 bits
+template <typename T>
+bool conv_fast_ok(const LdConv<T, true>& l, int N) {
+  if (sizeof(T) != 2 || !l.vec_ok) return false;
+  if (l.C1 % 64 || l.C2 % 64 || (l.U != 1 && l.U != 2)) return false;
+  const long b1 = (long)N * l.Hs * l.Ws * l.C1 * sizeof(T), b2 = (long)N * l.Hs * l.Ws * l.C2 * sizeof(T);
+  return b1 < (1L << 31) && b2 < (1L << 31);
+}
+template <typename T>
+LdConvF<T> conv_fast(const LdConv<T, true>& l, int N) {
+  LdConvF<T> f;
+  f.src1 = l.src1;
+  f.src2 = l.src2 ? l.src2 : l.src1;
+  f.C1 = l.C1;
+  f.C2 = l.C2;
+  f.Ctot = l.Ctot;
+  f.Hs = l.Hs;
+  f.Ws = l.Ws;
+  f.Hi = l.Hi;
+  f.Wi = l.Wi;
+  f.ushift = l.U == 2 ? 1 : 0;
+  f.KS = l.KS;
+  f.S = l.S;
+  f.Pd = l.Pd;
+  f.Ho = l.Ho;
+  f.Wo = l.Wo;
+  f.P = l.P;
+  f.Kt = l.Kt;
+  f.bytes1 = (unsigned)((long)N * l.Hs * l.Ws * l.C1 * sizeof(T));
+  f.bytes2 = (unsigned)((long)N * l.Hs * l.Ws * l.C2 * sizeof(T));
+  return f;
+}
+
 template <typename T, bool KC>
 LdDense<T, KC> dense(const void* p, long ld, int rows, int K) {
   LdDense<T, KC> l;
@@ -254,6 +288,11 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
     auto la = conv_a<T>(g, g->src1, g->C1, g->src2, g->C2, g->Hs, g->Ws, g->U, g->KS, g->stride, g->pad);
     HVIT_CHECK(la.Ho > 0 && la.Wo > 0, "hvit_conv_fwd: empty output");
     int Kt = la.Kt;
+    if constexpr (sizeof(T) == 2) {
+      if (conv_fast_ok(la, g->N))
+        return launch_gemm<T>(conv_fast(la, g->N), dense<T, true>(w_packed, Kt, g->Cout, Kt), la.P, g->Cout, Kt, 1,
+                              ep, (hipStream_t)stream);
+    }
     // odd reduction length (Cin=1 first conv): weights take the scalar load path
     return launch_gemm<T>(la, dense<T, true>(w_packed, Kt, g->Cout, Kt), la.P, g->Cout, Kt, 1, ep,
                           (hipStream_t)stream);
@@ -303,6 +342,10 @@ extern "C" int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     // dU = conv(dy, flipped/transposed W): im2col over dy (Cout channels, stride 1)
     auto la = conv_a<T>(g, dy, g->Cout, nullptr, 0, Ho, Wo, 1, g->KS, 1, g->pad);
     int Kt = la.Kt;
+    if constexpr (sizeof(T) == 2) {
+      if (conv_fast_ok(la, g->N))
+        return launch_gemm<T>(conv_fast(la, g->N), dense<T, true>(w, Kt, Ctot, Kt), la.P, Ctot, Kt, 1, ep, st);
+    }
     return launch_gemm<T>(la, dense<T, true>(w, Kt, Ctot, Kt), la.P, Ctot, Kt, 1, ep, st);
   });
 }
