@@ -24,6 +24,7 @@
 // sources; the 4x4/stride-4 patch embedding); each thread keeps a cursor per
 // 16-byte chunk (its pixel / tap decomposition) that advances incrementally.
 #pragma once
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -260,6 +261,72 @@ struct LdConvF {
         (void*)(first ? src1 : src2), (short)0, (int)(first ? bytes1 : bytes2), 0x00020000);
     const unsigned voff = ok ? (unsigned)off : 0x80000000u;
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+  }
+};
+
+// Im2col B loader of the conv weight gradient (MN role: a = im2col index k,
+// fixed per chunk for the whole K loop; b = output pixel, advancing).  The
+// tap / channel / source of a thread's k are resolved once at init; the pixel
+// cursor (row base n*Hs, oy, ox) advances incrementally; addresses use 32-bit
+// element offsets from a per-thread base pointer.
+template <typename T>
+struct LdConvWF {
+  static constexpr bool KC = false;
+  static constexpr int E = Elem<T>::PER16;
+  const T* src1;
+  const T* src2;
+  int C1, C2, Ctot;
+  int Hs, Ws, Hi, Wi, ushift;
+  int KS, S, Pd;
+  int Ho, Wo, P, Kt;
+
+  __device__ __forceinline__ bool fast() const { return true; }
+  struct Sh {
+    const T* base;
+    int Cx, coff, dy0, dx0;
+    bool kok;
+  };
+  struct Cur {
+    int p, rb, oy, ox;
+  };
+  __device__ __forceinline__ void init(Sh& sh, Cur& cu, int a, int b) const {
+    const int tap = a / Ctot, c = a - tap * Ctot;
+    const int ky = tap / KS, kx = tap - ky * KS;
+    const bool first = c < C1;
+    sh.base = first ? src1 : src2;
+    sh.Cx = first ? C1 : C2;
+    sh.coff = first ? c : c - C1;
+    sh.dy0 = ky - Pd;
+    sh.dx0 = kx - Pd;
+    sh.kok = a < Kt;
+    const int hw = Ho * Wo;
+    const int n = b / hw, rem = b - n * hw;
+    cu.p = b;
+    cu.rb = n * Hs;
+    cu.oy = rem / Wo;
+    cu.ox = rem - cu.oy * Wo;
+  }
+  __device__ __forceinline__ void step_sh(Sh&, int) const {}
+  __device__ __forceinline__ void step(Cur& cu, int bk) const {
+    cu.p += bk;
+    cu.ox += bk;
+    while (cu.ox >= Wo) {
+      cu.ox -= Wo;
+      if (++cu.oy == Ho) {
+        cu.oy = 0;
+        cu.rb += Hs;
+      }
+    }
+  }
+  template <bool CHECK>
+  __device__ __forceinline__ u32x4 fetch(const Sh& sh, const Cur& cu) const {
+    const int iy = cu.oy * S + sh.dy0, ix = cu.ox * S + sh.dx0;
+    bool ok = (unsigned)iy < (unsigned)Hi && (unsigned)ix < (unsigned)Wi;
+    if (CHECK) ok = ok && sh.kok && cu.p < P;
+    const int off = ok ? ((cu.rb + (iy >> ushift)) * Ws + (ix >> ushift)) * sh.Cx + sh.coff : 0;
+    const u32x4 v = *(const u32x4*)(sh.base + off);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    return ok ? v : z;
   }
 };
 
@@ -1025,8 +1092,15 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
   // outputs (N <= 64: conv layers with 64 channels); else 64x64
   int tile = force_tile;
   if (!tile) {
+    // 128x64 also when 128x128 would leave fewer than ~1.5 workgroups per CU
+    // or a half-empty last column tile (measured: 2.5 % per train step)
+    static const int policy = getenv("HVIT_TILE_POLICY") ? atoi(getenv("HVIT_TILE_POLICY")) : 2;
+    const long b128 = (long)cdiv(M, 128) * cdiv(N, 128) * splits;
+    const long b12864 = (long)cdiv(M, 128) * cdiv(N, 64) * splits;
     if (N <= 64 && (long)cdiv(M, 128) * splits >= 160) tile = 12864;
-    else if (N > 64 && (long)cdiv(M, 128) * cdiv(N, 128) * splits >= 160) tile = 128;
+    else if (policy >= 1 && N > 64 && b128 < 384 && b12864 >= 384) tile = 12864;
+    else if (policy >= 2 && N > 64 && N % 128 != 0 && N % 64 == 0 && b12864 >= 160) tile = 12864;
+    else if (N > 64 && b128 >= 160) tile = 128;
     else tile = 64;
   }
   const bool lean_store = ep.mode == EPI_STORE && ep.act == ACT_NONE && !ep.rowadd && !ep.resid && !ep.drop_thr &&

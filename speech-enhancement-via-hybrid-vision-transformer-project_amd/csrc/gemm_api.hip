@@ -6,6 +6,8 @@
 //     components.py:55-62, :149-158, with nearest-x2 upsample and the decoder's
 //     channel concat folded into the operand gather; the k=s=4 patch embedding,
 //     components.py:275-280, with the [B,N,D] token layout written directly).
+#include <algorithm>
+
 #include "gemm.h"
 
 using namespace hvit;
@@ -376,6 +378,28 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     LdConv<T, false> lb;
     static_assert(sizeof(lb) == sizeof(la), "layout");
     __builtin_memcpy(&lb, &la, sizeof(la));
+    LdConvWF<T> lf;
+    const bool wfast = sizeof(T) == 2 && la.vec_ok && (la.U == 1 || la.U == 2) &&
+                       (long)g->N * la.Hs * la.Ws * std::max(la.C1, la.C2) < (1L << 31);
+    if (wfast) {
+      lf.src1 = la.src1;
+      lf.src2 = la.src2 ? la.src2 : la.src1;
+      lf.C1 = la.C1;
+      lf.C2 = la.C2;
+      lf.Ctot = la.Ctot;
+      lf.Hs = la.Hs;
+      lf.Ws = la.Ws;
+      lf.Hi = la.Hi;
+      lf.Wi = la.Wi;
+      lf.ushift = la.U == 2 ? 1 : 0;
+      lf.KS = la.KS;
+      lf.S = la.S;
+      lf.Pd = la.Pd;
+      lf.Ho = la.Ho;
+      lf.Wo = la.Wo;
+      lf.P = la.P;
+      lf.Kt = la.Kt;
+    }
     const int M = g->Cout, N = la.Kt, K = la.P;
     const ConvWgTile t(M);
     int splits = wgrad_splits(M, N, K, t.bm, t.bn);
@@ -386,7 +410,8 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     ep.out = splits > 1 ? (void*)ws : (void*)dw_packed;
     ep.out_dt = HVIT_F32;
     ep.ldo = N;
-    int rc = launch_gemm<T>(dense<T, false>(dy, M, M, K), lb, M, N, K, splits, ep, st, t.tile);
+    int rc = wfast ? launch_gemm<T>(dense<T, false>(dy, M, M, K), lf, M, N, K, splits, ep, st, t.tile)
+                   : launch_gemm<T>(dense<T, false>(dy, M, M, K), lb, M, N, K, splits, ep, st, t.tile);
     if (rc) return rc;
     if (splits > 1) return hvit_sum_slabs(ws, splits, (long long)M * N, dw_packed, stream);
     return HVIT_OK;
