@@ -166,6 +166,18 @@ int hvit_upsample_split_bwd(const void* du, int du_dt, int N, int H, int W, int 
 
 /* ---- Elementwise / reductions */
 int hvit_cast(const void* src, int src_dt, void* dst, int dst_dt, long long n, void* stream);
+/* Multi-tensor weight preparation, one launch for many parameters (replaces
+ * per-weight hvit_cast / hvit_conv_weight_pack in the module forward):
+ * kind 0 = cast f32 -> dt (numel elements), kind 1 / 2 = conv packing mode 0 / 1
+ * of a [cout][cin][ks][ks] f32 weight.  numel % 4 == 0, 16-byte aligned src. */
+typedef struct {
+  const float* src;
+  void* dst;
+  long long numel;
+  int kind, dt;
+  int cout, cin, ks;
+} hvit_wprep_item_t;
+int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void* stream);
 int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, const hvit_dropout_t* dropout,
                        const float* rowscale, int rows_per_sample, void* out, int out_dt, void* stream);
 int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long long n, void* dz, int dz_dt, void* stream);

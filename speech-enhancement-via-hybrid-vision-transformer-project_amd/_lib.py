@@ -46,6 +46,11 @@ class ConvGeom(C.Structure):
     ]
 
 
+class WPrepItem(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("numel", i64), ("kind", i32), ("dt", i32),
+                ("cout", i32), ("cin", i32), ("ks", i32)]
+
+
 P = C.POINTER
 _SIGS = {
     "hvit_last_error": ([], C.c_char_p),
@@ -80,6 +85,7 @@ _SIGS = {
     "hvit_reduce_rows": ([vp, i32, i64, i64, i64, i32, vp, vp], i32),
     "hvit_sum_slabs": ([vp, i32, i64, vp, vp], i32),
     "hvit_droppath_scale": ([i32, P(Dropout), vp, vp], i32),
+    "hvit_weight_prep": ([i32, P(WPrepItem), vp], i32),
 }
 
 EXPORTED = sorted(k for k in _SIGS)

@@ -2,6 +2,8 @@
 // weight (re)packing for the implicit GEMMs, dropout/drop-path gradient
 // scaling, tanh backward, column reductions (bias / pos-embed gradients) and
 // split-K slab reduction.
+#include <algorithm>
+
 #include "common.h"
 
 namespace hvit {
@@ -190,6 +192,61 @@ __global__ void sum_slabs4_kernel(const float* ws, int splits, int n4, float* ou
   }
 }
 
+// Multi-tensor weight preparation (one launch per forward instead of one per
+// weight): f32 master parameters -> bf16/f32 copies (kind 0) or conv packings
+// (kind 1: [Cout][KS][KS][Cin], kind 2: flipped [Cin][KS][KS][Cout]).  The
+// flattened index space is split into 4-element units (every item's numel is
+// a multiple of 4); a thread locates its item in the prefix table.
+constexpr int WPREP_MAX = 32;
+struct WPrepItem {
+  const float* src;
+  void* dst;
+  int n4;    // numel / 4
+  int kind;  // 0 cast, 1 pack mode 0, 2 pack mode 1
+  int dt;
+  int co, ci, ks;
+};
+struct WPrepArgs {
+  int count;
+  int start[WPREP_MAX + 1];  // prefix sums of n4
+  WPrepItem it[WPREP_MAX];
+};
+
+__global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
+  const int total = a.start[a.count];
+  int j = 0;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+    while (u >= a.start[j + 1]) ++j;  // u only grows: the search resumes
+    const WPrepItem& w = a.it[j];
+    const int l4 = u - a.start[j];
+    const f32x4 v = *(const f32x4*)(w.src + 4L * l4);
+    if (w.kind == 0) {
+      if (w.dt == HVIT_F32) {
+        *(f32x4*)((float*)w.dst + 4L * l4) = v;
+      } else {
+        uint2 o;
+        o.x = f2bf2(v[0], v[1]);
+        o.y = f2bf2(v[2], v[3]);
+        *(uint2*)((bf16_t*)w.dst + 4L * l4) = o;
+      }
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * l4 + e;
+      const int kx = i % w.ks;
+      int t = i / w.ks;
+      const int ky = t % w.ks;
+      t /= w.ks;
+      const int ci = t % w.ci;
+      const int co = t / w.ci;
+      const long o = w.kind == 1 ? (((long)co * w.ks + ky) * w.ks + kx) * w.ci + ci
+                                 : (((long)ci * w.ks + (w.ks - 1 - ky)) * w.ks + (w.ks - 1 - kx)) * w.co + co;
+      st_dt(w.dst, o, v[e], w.dt);
+    }
+  }
+}
+
 __global__ void droppath_scale_kernel(int B, uint32_t thr, float ds, unsigned long long seed, uint32_t site,
                                       float* out) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -337,6 +394,32 @@ extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* o
                        (long)n, out);
   }
   HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void* stream) {
+  HVIT_CHECK(count >= 0 && (count == 0 || items), "hvit_weight_prep: bad args");
+  for (int base = 0; base < count; base += WPREP_MAX) {
+    WPrepArgs a;
+    a.count = std::min(WPREP_MAX, count - base);
+    a.start[0] = 0;
+    for (int k = 0; k < a.count; ++k) {
+      const hvit_wprep_item_t& it = items[base + k];
+      HVIT_CHECK(it.src && it.dst && it.numel >= 0 && it.numel % 4 == 0 && it.numel < (1LL << 31),
+                 "hvit_weight_prep: item %d: null pointer or numel %% 4 != 0", base + k);
+      HVIT_CHECK(it.kind >= 0 && it.kind <= 2, "hvit_weight_prep: item %d: kind", base + k);
+      HVIT_CHECK(it.kind == 0 || (long long)it.cout * it.cin * it.ks * it.ks == it.numel,
+                 "hvit_weight_prep: item %d: conv shape", base + k);
+      HVIT_CHECK(aligned16(it.src) && (it.kind != 0 || aligned16(it.dst)), "hvit_weight_prep: item %d: alignment",
+                 base + k);
+      a.it[k] = WPrepItem{it.src, it.dst, (int)(it.numel / 4), it.kind, it.dt, it.cout, it.cin, it.ks};
+      a.start[k + 1] = a.start[k] + (int)(it.numel / 4);
+    }
+    const int total = a.start[a.count];
+    if (total == 0) continue;
+    hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
+    HVIT_LAUNCH_CHECK();
+  }
   return HVIT_OK;
 }
 

@@ -162,10 +162,122 @@ __global__ __launch_bounds__(256) void bilinear_bwd_vec_kernel(const TI* __restr
       }
     }
     TO* d = dx + (size_t)p * C + cg * CV;
+    if constexpr (sizeof(TO) == 2) {
+      if (accumulate) {
+        const u32x4 u = *(const u32x4*)d;
 #pragma unroll
-    for (int e = 0; e < CV; ++e) {
-      if (accumulate) acc[e] += Elem<TO>::to_f(d[e]);
-      d[e] = Elem<TO>::from_f(acc[e]);
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(u[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf2(acc[2 * e], acc[2 * e + 1]);
+      *(u32x4*)d = o;
+    } else {
+      f32x4 lo = {acc[0], acc[1], acc[2], acc[3]}, hi = {acc[4], acc[5], acc[6], acc[7]};
+      if (accumulate) {
+        lo += *(const f32x4*)d;
+        hi += *(const f32x4*)(d + 4);
+      }
+      *(f32x4*)d = lo;
+      *(f32x4*)(d + 4) = hi;
+    }
+  }
+}
+
+// Row-blocked gather backward: one workgroup per input row (n, iy).  The
+// output taps of every input column of the row (and of the row itself) are
+// computed once into LDS, then threads walk (column, channel group) items.
+constexpr int RB_MAXW = 256, RB_TAPS = 12;
+template <typename TI, typename TO, int CV>
+__global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __restrict__ dy, TO* __restrict__ dx,
+                                                               int Hi, int Wi, int C, int Ho, int Wo, float sh,
+                                                               float sw, int accumulate) {
+  __shared__ int xo[RB_MAXW][RB_TAPS];
+  __shared__ float xw[RB_MAXW][RB_TAPS];
+  __shared__ int xn[RB_MAXW];
+  __shared__ int yo[RB_TAPS];
+  __shared__ float yw[RB_TAPS];
+  __shared__ int yn;
+  const int n = blockIdx.x / Hi, iy = blockIdx.x - n * Hi;
+  for (int ix = threadIdx.x; ix < Wi; ix += blockDim.x) {
+    int lo, hi;
+    out_range(ix, Wi, Wo, sw, lo, hi);
+    int nt = 0;
+    for (int o = lo; o <= hi && nt < RB_TAPS; ++o) {
+      const float wt = lin_w(o, ix, Wi, sw);
+      if (wt != 0.f) {
+        xo[ix][nt] = o;
+        xw[ix][nt] = wt;
+        ++nt;
+      }
+    }
+    xn[ix] = nt;
+  }
+  if (threadIdx.x == 0) {
+    int lo, hi;
+    out_range(iy, Hi, Ho, sh, lo, hi);
+    int nt = 0;
+    for (int o = lo; o <= hi && nt < RB_TAPS; ++o) {
+      const float wt = lin_w(o, iy, Hi, sh);
+      if (wt != 0.f) {
+        yo[nt] = o;
+        yw[nt] = wt;
+        ++nt;
+      }
+    }
+    yn = nt;
+  }
+  __syncthreads();
+  const int G = C / CV;
+  const int ny = yn;
+  for (int item = threadIdx.x; item < Wi * G; item += blockDim.x) {
+    const int ix = item / G, cg = item - ix * G;
+    float acc[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) acc[e] = 0.f;
+    const int nx = xn[ix];
+    for (int a = 0; a < ny; ++a) {
+      const TI* row = dy + ((size_t)(n * Ho + yo[a]) * Wo) * C + cg * CV;
+      const float wa = yw[a];
+      for (int b = 0; b < nx; ++b) {
+        const float w = wa * xw[ix][b];
+        const TI* q = row + (size_t)xo[ix][b] * C;
+        if constexpr (CV == 8 && sizeof(TI) == 2) {
+          const u32x4 u = *(const u32x4*)q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[2 * e] += w * __uint_as_float(u[e] << 16);
+            acc[2 * e + 1] += w * __uint_as_float(u[e] & 0xffff0000u);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < CV; ++e) acc[e] += w * Elem<TI>::to_f(q[e]);
+        }
+      }
+    }
+    TO* d = dx + ((size_t)(n * Hi + iy) * Wi + ix) * C + cg * CV;
+    if constexpr (CV == 8 && sizeof(TO) == 2) {
+      if (accumulate) {
+        const u32x4 u = *(const u32x4*)d;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(u[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf2(acc[2 * e], acc[2 * e + 1]);
+      *(u32x4*)d = o;
+    } else {
+#pragma unroll
+      for (int e = 0; e < CV; ++e) {
+        const float v = acc[e] + (accumulate ? Elem<TO>::to_f(d[e]) : 0.f);
+        d[e] = Elem<TO>::from_f(v);
+      }
     }
   }
 }
@@ -227,6 +339,20 @@ extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int W
   float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
   // vector path: 8-channel groups, at most TAPS output taps per dimension
   const bool taps_ok = (float)Ho / (float)Hi <= 6.f && (float)Wo / (float)Wi <= 6.f;
+  const bool rows_ok = (float)Ho / (float)Hi <= 4.f && (float)Wo / (float)Wi <= 4.f && Wi <= RB_MAXW &&
+                       (long)N * Hi < (1L << 31) && dy_dt == dx_dt;
+  if (rows_ok && C % 8 == 0 && dy_dt == HVIT_BF16 && aligned16(dy) && aligned16(dx)) {
+    hipLaunchKernelGGL((bilinear_bwd_rows_kernel<bf16_t, bf16_t, 8>), dim3(N * Hi), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
+  if (rows_ok && C == 1 && dy_dt == HVIT_F32) {
+    hipLaunchKernelGGL((bilinear_bwd_rows_kernel<float, float, 1>), dim3(N * Hi), dim3(256), 0,
+                       (hipStream_t)stream, (const float*)dy, (float*)dx, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   if (C % 8 == 0 && taps_ok && dy_dt == dx_dt && aligned16(dy) && aligned16(dx)) {
     const long groups = (long)N * Hi * Wi * (C / 8);
     if (dy_dt == HVIT_BF16)

@@ -25,8 +25,45 @@ def _empty(shape, dt, dev):
     return torch.empty(shape, dtype=L.torch_dtype(dt), device=dev)
 
 
+# Per-forward cache of prepared weights, filled by prep_weights() with one
+# multi-tensor launch: (id(param), kind, dt) -> (param._version, tensor).  A
+# hit requires the parameter to be unmodified since preparation.
+_PREP = {}
+
+
+def _prep_get(t, kind, dt):
+    hit = _PREP.get((id(t), kind, dt))
+    if hit is not None and hit[0] == t._version and hit[2] is t:
+        return hit[1]
+    return None
+
+
+def prep_weights(items, dev):
+    """items: [(param, kind, dt)], kind 0 = cast, 1/2 = conv pack mode 0/1.
+    Replaces the cache with freshly prepared copies (one kernel launch)."""
+    _PREP.clear()
+    todo = []
+    for w, kind, dt in items:
+        if kind == 0 and L.dt_of(w) == dt:
+            continue
+        out = _empty(w.shape if kind == 0 else (w.numel(),), dt, dev)
+        todo.append((w, kind, dt, out))
+    if not todo:
+        return
+    arr = (L.WPrepItem * len(todo))()
+    for i, (w, kind, dt, out) in enumerate(todo):
+        co, ci, ks = (w.shape[0], w.shape[1], w.shape[2]) if kind else (0, 0, 0)
+        arr[i] = L.WPrepItem(w.data_ptr(), out.data_ptr(), w.numel(), kind, dt, co, ci, ks)
+    call("hvit_weight_prep", len(todo), arr, stream_ptr())
+    for w, kind, dt, out in todo:
+        _PREP[(id(w), kind, dt)] = (w._version, out, w)
+
+
 def cast(t: torch.Tensor, dt: int) -> torch.Tensor:
     """Contiguous copy of ``t`` in dtype ``dt`` (no copy if already there)."""
+    hit = _prep_get(t, 0, dt)
+    if hit is not None:
+        return hit
     t = t.contiguous()
     if L.dt_of(t) == dt:
         return t
@@ -36,6 +73,9 @@ def cast(t: torch.Tensor, dt: int) -> torch.Tensor:
 
 
 def pack_conv(w: torch.Tensor, mode: int, dt: int) -> torch.Tensor:
+    hit = _prep_get(w, 1 + mode, dt)
+    if hit is not None:
+        return hit
     w = w.detach().contiguous()
     if w.dtype != torch.float32:
         raise TypeError("hvit: conv weights must be float32 parameters")
@@ -426,7 +466,7 @@ class SkipFn(torch.autograd.Function):
             call("hvit_bilinear_fwd", e.data_ptr(), dt, N, He, We, Ce, Ho, Wo, r.data_ptr(), dt, s)
         else:
             r = e.contiguous()
-        W = cast(w.view(Cd, Ce), dt)
+        W = cast(w, dt).view(Cd, Ce)
         y = _empty((N, Ho, Wo, Cd), dt, dev)
         M = N * Ho * Wo
         call("hvit_linear_fwd", dt, r.data_ptr(), W.data_ptr(), b.data_ptr(), M, Cd, Ce, y.data_ptr(), dt, None, s)

@@ -289,6 +289,28 @@ class HybridViT(nn.Module):
     def _seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
 
+    def _prep_weights(self, dt: int, dev) -> None:
+        """Cast / pack every weight this forward (and its backward) will use
+        in one multi-tensor launch instead of one launch per weight."""
+        grads = torch.is_grad_enabled()
+        items = []
+        for i, blk in enumerate(self.encoder):
+            items.append((blk.conv.weight, 1, dt))
+            if grads and i > 0:
+                items.append((blk.conv.weight, 2, dt))
+        items.append((self.patch_embed.projection.weight, 1, dt))
+        for blk in self.transformer.blocks:
+            items += [(blk.attn.qkv.weight, 0, dt), (blk.attn.proj.weight, 0, dt),
+                      (blk.mlp.net[0].weight, 0, dt), (blk.mlp.net[3].weight, 0, dt)]
+        items.append((self.to_feature_map.weight, 0, dt))
+        if self.use_skip_connections:
+            items += [(sp.weight, 0, dt) for sp in self.skip_projections]
+        for blk in self.decoder:
+            items.append((blk.conv.weight, 1, dt))
+            if grads:
+                items.append((blk.conv.weight, 2, dt))
+        HF.prep_weights(items, dev)
+
     @staticmethod
     def _nhwc(t: torch.Tensor) -> torch.Tensor:
         """NCHW logical tensor (possibly a channels-last view) -> NHWC contiguous."""
@@ -395,6 +417,7 @@ class HybridViT(nn.Module):
         dt = self._dt()
         seed = self._seed()
         F, T = x.shape[2], x.shape[3]
+        self._prep_weights(dt, x.device)
         xh = HF.CastFn.apply(self._nhwc(x.float() if x.dtype != torch.float32 else x), dt)
         feat, skips = self._encoder(xh, dt, seed)
         t, hw = self._tokens(feat, dt, seed)

@@ -416,3 +416,11 @@ def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
     dx = torch.empty(N, Hi, Wi, C, device=DEV)
     l.call("hvit_bilinear_bwd", ga.data_ptr(), l.F32, N, Ho, Wo, C, Hi, Wi, dx.data_ptr(), l.F32, 0, s())
     assert rel(nchw(dx), x.grad) < 1e-5
+    if C % 8 == 0:  # bf16 (the skip-connection path), incl. accumulate
+        gb = ga.to(torch.bfloat16)
+        dxb = torch.empty(N, Hi, Wi, C, device=DEV, dtype=torch.bfloat16)
+        l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, dxb.data_ptr(), l.BF16, 0, s())
+        refb = nhwc(x.grad)
+        assert rel(dxb.float(), refb) < 2e-2
+        l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, dxb.data_ptr(), l.BF16, 1, s())
+        assert rel(dxb.float(), 2 * refb) < 2e-2
