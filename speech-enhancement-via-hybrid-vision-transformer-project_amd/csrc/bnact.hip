@@ -130,15 +130,20 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
   // a thread's channel group never changes (256 % G == 0, grid stride % G == 0):
   // per-channel constants are loaded once
   const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
-  float sc[CV], sh[CV], mu[CV], is[CV], s1[CV], s2[CV];
+  // sc, sh: relu(bn(z)) = max(z*sc + sh, 0).  Reduce pass: xhat = (z - mu)*is.
+  // Apply pass (training): dz = sc*(g - s1 - xhat*s2) = sc*g + ca + cb*z.
+  float sc[CV], sh[CV], mu[CV], is[CV], ca[CV], cb[CV];
 #pragma unroll
   for (int e = 0; e < CV; ++e) {
-    mu[e] = a.mean[c + e];
-    is[e] = a.invstd[c + e];
-    sc[e] = is[e] * a.gamma[c + e];
-    sh[e] = a.beta[c + e] - mu[e] * sc[e];
-    s1[e] = (APPLY && training) ? sums[c + e] * invM : 0.f;
-    s2[e] = (APPLY && training) ? sums[a.C + c + e] * invM : 0.f;
+    const float m_ = a.mean[c + e], i_ = a.invstd[c + e];
+    sc[e] = i_ * a.gamma[c + e];
+    sh[e] = a.beta[c + e] - m_ * sc[e];
+    mu[e] = m_;
+    is[e] = i_;
+    const float s1 = (APPLY && training) ? sums[c + e] * invM : 0.f;
+    const float s2 = (APPLY && training) ? sums[a.C + c + e] * invM : 0.f;
+    cb[e] = -sc[e] * s2 * i_;
+    ca[e] = -sc[e] * s1 - cb[e] * m_;
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     int t = i / G;
@@ -156,11 +161,14 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
       if (inb[q]) V16<T>::load(z + ((size_t)(n * a.H + y) * a.W + x) * a.C + c, zv[q]);
     }
     const bool full = wy < Ho && wx < Wo;
-    float g[MAXW][CV];
+    // routed gradient: gv[e] at window position arg[e] (first maximum), 0 elsewhere
+    int arg[CV];
+    float gv[CV];
 #pragma unroll
-    for (int q = 0; q < MAXW; ++q)
-#pragma unroll
-      for (int e = 0; e < CV; ++e) g[q][e] = 0.f;
+    for (int e = 0; e < CV; ++e) {
+      arg[e] = 0;
+      gv[e] = 0.f;
+    }
     if (full) {
       float d[CV], m[CV];
       const TD* dp = dy + ((size_t)(n * Ho + wy) * Wo + wx) * a.C + c;
@@ -173,8 +181,6 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
       drop_mask<CV>(a, n, c, m);
 #pragma unroll
       for (int e = 0; e < CV; ++e) {
-        // first maximum of relu(bn(z)) over the window
-        int arg = 0;
         float best = fmaxf(zv[0][e] * sc[e] + sh[e], 0.f);
 #pragma unroll
         for (int q = 1; q < MAXW; ++q) {
@@ -182,37 +188,32 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
           const float v = fmaxf(zv[q][e] * sc[e] + sh[e], 0.f);
           if (v > best) {
             best = v;
-            arg = q;
+            arg[e] = q;
           }
         }
-        const float gv = best > 0.f ? d[e] * m[e] : 0.f;
-#pragma unroll
-        for (int q = 0; q < MAXW; ++q)
-          if (q == arg) g[q][e] = gv;
+        gv[e] = best > 0.f ? d[e] * m[e] : 0.f;
       }
     }
+    if (!APPLY) {
+      if (full) {
 #pragma unroll
-    for (int q = 0; q < MAXW; ++q) {
-      if (!inb[q]) continue;
-      if (!APPLY) {
-        if (full)
+        for (int e = 0; e < CV; ++e) {
+          float zr = zv[0][e];
 #pragma unroll
-          for (int e = 0; e < CV; ++e) {
-            const float xh = (zv[q][e] - mu[e]) * is[e];
-            acc1[e] += g[q][e];
-            acc2[e] += g[q][e] * xh;
-          }
-      } else {
+          for (int q = 1; q < MAXW; ++q) zr = arg[e] == q ? zv[q][e] : zr;
+          acc1[e] += gv[e];
+          acc2[e] += gv[e] * ((zr - mu[e]) * is[e]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < MAXW; ++q) {
+        if (!inb[q]) continue;
         float o[CV];
 #pragma unroll
         for (int e = 0; e < CV; ++e) {
-          const float k = sc[e];
-          if (training) {
-            const float xh = (zv[q][e] - mu[e]) * is[e];
-            o[e] = k * (g[q][e] - s1[e] - xh * s2[e]);
-          } else {
-            o[e] = k * g[q][e];
-          }
+          const float gq = arg[e] == q ? gv[e] : 0.f;
+          o[e] = training ? sc[e] * gq + ca[e] + cb[e] * zv[q][e] : sc[e] * gq;
         }
         const int y = wy * P + (q >> 1), x = wx * P + (q & 1);
         V16<T>::store(dz + ((size_t)(n * a.H + y) * a.W + x) * a.C + c, o);
@@ -260,12 +261,15 @@ __global__ void bn_slots_reduce_kernel(float* sums, int n2) {
   sums[i] = s;
 }
 
-static int grid_for(long n) {
+// grid-stride launches; per-kernel caps measured on the B=32 encoder shapes
+// (fewer, longer-lived workgroups stream better here than one item per thread)
+static int grid_for(long n, long cap) {
   long g = (n + 255) / 256;
-  if (g > 4096) g = 4096;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
 }
+constexpr long BN_GRID_FWD = 2048, BN_GRID_SUMS = 2048, BN_GRID_APPLY = 1024;
 
 static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const float* mean, const float* invstd,
                      const float* gamma, const float* beta, const hvit_dropout_t* dr, int cv) {
@@ -298,7 +302,7 @@ extern "C" int hvit_bn_act_fwd(int dt, const void* z, int N, int H, int W, int C
   const long total = (long)N * (H / pool) * (W / pool) * (C / cv);
   if (total <= 0) return HVIT_OK;
   hipStream_t st = (hipStream_t)stream;
-  dim3 g(grid_for(total));
+  dim3 g(grid_for(total, BN_GRID_FWD));
   if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
     hipLaunchKernelGGL((bnact_fwd_kernel<bf16_t, bf16_t>), g, dim3(256), 0, st, (const bf16_t*)z, (bf16_t*)y, a);
   else if (dt == HVIT_BF16)
@@ -318,7 +322,7 @@ static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* su
   const int P = a.pool;
   const long total = (long)a.N * ((a.H + P - 1) / P) * ((a.W + P - 1) / P) * (a.C / cv);
   if (total <= 0) return HVIT_OK;
-  dim3 g(grid_for(total));
+  dim3 g(grid_for(total, BN_GRID_SUMS)), ga(grid_for(total, BN_GRID_APPLY));
   if (training) {
     hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, false>), g, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
                        training, (T*)dz);
@@ -326,7 +330,7 @@ static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* su
     hipLaunchKernelGGL(bn_slots_reduce_kernel, dim3(cdiv(2 * a.C, 256)), dim3(256), 0, st, sums, 2 * a.C);
     HVIT_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, true>), g, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
+  hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, true>), ga, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
                      training, (T*)dz);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
