@@ -95,12 +95,14 @@ int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K
  * Weights are pre-packed with hvit_conv_weight_pack: mode 0 [Cout][KS][KS][Cin]
  * for fwd / wgrad / patch dgrad; mode 1 (flipped) [Cin][KS][KS][Cout] for the
  * 3x3 dgrad.  conv_fwd optionally writes BatchNorm partials
- * [ceil(P/64)][Cout][2] (mean, M2 per 64-row tile) for hvit_bn_finalize; its
+ * [ceil(P/R)][Cout][2] (mean, M2 per R-row tile, R = hvit_conv_bn_tile_rows)
+ * for hvit_bn_finalize; its
  * epilogue (nullable) may apply tanh (final decoder conv, components.py:166-167),
  * a row-periodic add (pos_embed, components.py:384) and dropout.
  * conv_dgrad: same-conv -> gradient of the (upsampled, concatenated) conv input
  * [N, Hs*U, Ws*U, C1+C2] (finish with hvit_upsample_split_bwd); patch conv
  * (KS == stride, pad 0) -> gradient of src1 [N, Hs, Ws, C1] directly. */
+int hvit_conv_bn_tile_rows(const hvit_conv_geom_t* g);
 int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* bias, void* y, int y_dt,
                   float* bn_partials, const hvit_epilogue_t* epi, void* stream);
 int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy, const void* w_packed, void* dx, int dx_dt,

@@ -86,6 +86,7 @@ _SIGS = {
     "hvit_sum_slabs": ([vp, i32, i64, vp, vp], i32),
     "hvit_droppath_scale": ([i32, P(Dropout), vp, vp], i32),
     "hvit_weight_prep": ([i32, P(WPrepItem), vp], i32),
+    "hvit_conv_bn_tile_rows": ([P(ConvGeom)], i32),
 }
 
 EXPORTED = sorted(k for k in _SIGS)

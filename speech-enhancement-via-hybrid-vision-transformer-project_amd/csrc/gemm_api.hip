@@ -169,6 +169,7 @@ bool thin_o1(const hvit_conv_geom_t* g) {
 
 int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats, hipStream_t st);
 int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream);
+int hvit_thin_c1_bn_tile_rows();
 long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g);
 int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
                        hipStream_t st);
@@ -269,6 +270,11 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
   return HVIT_OK;
 }
 
+// rows per BatchNorm partial tile written by hvit_conv_fwd for geometry g
+extern "C" int hvit_conv_bn_tile_rows(const hvit_conv_geom_t* g) {
+  return g && thin_c1(g) ? hvit_thin_c1_bn_tile_rows() : 64;
+}
+
 extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* bias,
                              void* y, int y_dt, float* bn_partials, const hvit_epilogue_t* epi, void* stream) {
   if (int rc = check_geom(g)) return rc;
@@ -281,6 +287,9 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
   const bool plain_epi = !epi || (epi->dropout.p == 0.f && !epi->rowadd && !epi->colsum);
   if (thin_c1(g) && plain_epi && !bias && (!epi || epi->act == HVIT_ACT_NONE) && aligned16(y))
     return hvit_thin_c1_fwd(dt, g, w_packed, y, y_dt, bn_partials, (hipStream_t)stream);
+  // BN partial tiles follow hvit_conv_bn_tile_rows(g): the thin path must have been taken
+  HVIT_CHECK(!bn_partials || !thin_c1(g), "hvit_conv_fwd: Cin=1 BatchNorm partials need the thin path "
+                                           "(no bias / epilogue, 16-byte aligned output)");
   if (thin_o1(g) && plain_epi && !bias && !bn_partials)
     return hvit_thin_o1_fwd(dt, g, w_packed, y, y_dt, epi && epi->act == HVIT_ACT_TANH, (hipStream_t)stream);
   Epi ep = to_epi(epi, y, y_dt, g->Cout);

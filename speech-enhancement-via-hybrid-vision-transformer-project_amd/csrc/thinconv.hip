@@ -47,23 +47,25 @@ struct Vec8 {  // 8 consecutive elements as floats (16 B for bf16, 32 B for f32)
 };
 
 constexpr int TC_PIX = 64;   // pixels per stats tile (= BN partial tile rows)
-constexpr int TC_TILES = 4;  // tiles per block
+constexpr int TC_TILES = 16;  // tiles per block
 
 // ---------------------------------------------------------------- Cin = 1 ---
 // z[p][co] = sum_tap x[p + tap] * w[co][tap]; BN partials per 64-pixel tile.
+// BN partial tile of the Cin = 1 path: one (mean, M2) per channel and block
+constexpr int C1_BLOCK_PIX = TC_PIX * TC_TILES;
+
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, TO* __restrict__ z,
                                                      float* __restrict__ stats, int N, int H, int W, int Cout) {
   // Each thread owns one 8-channel group cc (fixed: 256 % CC == 0) with its 72
-  // weights in registers and walks TC_TILES 64-pixel tiles; per tile the
-  // values go through an LDS tile for the (mean, M2) BN partials, reduced by
-  // all 256 threads.
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int CP = Cout + 1;
-  float* tile = sm;               // [64][Cout + 1]
-  float* red = sm + TC_PIX * CP;  // [256]
+  // weights in registers and walks the block's C1_BLOCK_PIX pixels with a
+  // stride of 256 / CC, keeping a Welford (mean, M2) per channel in registers;
+  // lanes of the same group merge (Chan) through shuffles, the four waves
+  // through LDS, once per block: BN partial tile = the block's pixels.
+  __shared__ float red[4][256][3];  // [wave][channel][count, mean, M2]
   const int CC = Cout / 8;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC, lanes = 256 / CC;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   float wr[9][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -71,61 +73,74 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
     for (int e = 0; e < 8; ++e) wr[t][e] = Elem<T>::to_f(w[(cc * 8 + e) * 9 + t]);
   const int P = N * H * W;
   const int HW = H * W;
-  const int c_red = threadIdx.x % Cout, rg = threadIdx.x / Cout, groups = 256 / Cout;
-  for (int tt = 0; tt < TC_TILES; ++tt) {
-    const int tile_id = blockIdx.x * TC_TILES + tt;
-    const int p0 = tile_id * TC_PIX;
-    if (p0 >= P) break;
-    for (int px = pl; px < TC_PIX; px += lanes) {
-      const int p = p0 + px;
-      if (p >= P) break;
-      const int n = p / HW, rem = p - n * HW, y = rem / W, xx = rem - y * W;
-      const T* xb = x + n * HW;
-      float xv[9];
+  const int p0 = blockIdx.x * C1_BLOCK_PIX, pend = min(P, p0 + C1_BLOCK_PIX);
+  float mu[8], m2[8], cnt = 0.f;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
-        xv[t] = (iy >= 0 && ix >= 0 && iy < H && ix < W) ? Elem<T>::to_f(xb[iy * W + ix]) : 0.f;
-      }
-      float o[8];
+  for (int e = 0; e < 8; ++e) mu[e] = m2[e] = 0.f;
+  for (int p = p0 + pl; p < pend; p += lanes) {
+    const int n = p / HW, rem = p - n * HW, y = rem / W, xx = rem - y * W;
+    const T* xb = x + n * HW;
+    float xv[9];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float s = 0.f;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) s += xv[t] * wr[t][e];
-        o[e] = s;
-      }
-      Vec8<TO>::store(z + (size_t)p * Cout + cc * 8, o);
-      if (stats) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) tile[px * CP + cc * 8 + e] = o[e];
-      }
+    for (int t = 0; t < 9; ++t) {
+      const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
+      xv[t] = (iy >= 0 && ix >= 0 && iy < H && ix < W) ? Elem<T>::to_f(xb[iy * W + ix]) : 0.f;
     }
-    if (!stats) continue;
-    __syncthreads();
-    const int rows = min(TC_PIX, P - p0);
-    float s = 0.f;
-    for (int r = rg; r < rows; r += groups) s += tile[r * CP + c_red];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    float tot = 0.f;
-    for (int g = 0; g < groups; ++g) tot += red[g * Cout + c_red];
-    const float mean = tot / (float)rows;
-    float q = 0.f;
-    for (int r = rg; r < rows; r += groups) {
-      const float d = tile[r * CP + c_red] - mean;
-      q += d * d;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc += xv[t] * wr[t][e];
+      o[e] = acc;
     }
-    __syncthreads();
-    red[threadIdx.x] = q;
-    __syncthreads();
-    if (rg == 0) {
-      float qt = 0.f;
-      for (int g = 0; g < groups; ++g) qt += red[g * Cout + c_red];
-      stats[((size_t)tile_id * Cout + c_red) * 2] = mean;
-      stats[((size_t)tile_id * Cout + c_red) * 2 + 1] = qt;
+    Vec8<TO>::store(z + (size_t)p * Cout + cc * 8, o);
+    cnt += 1.f;
+    const float inv = __builtin_amdgcn_rcpf(cnt);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = o[e] - mu[e];
+      mu[e] += d * inv;
+      m2[e] += d * (o[e] - mu[e]);
     }
-    __syncthreads();
+  }
+  if (!stats) return;
+  for (int off = CC; off < 64; off <<= 1) {
+    const float cb = __shfl_xor(cnt, off, 64);
+    const float ct = cnt + cb;
+    const float fb = ct > 0.f ? cb / ct : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float mb = __shfl_xor(mu[e], off, 64), qb = __shfl_xor(m2[e], off, 64);
+      const float d = mb - mu[e];
+      m2[e] += qb + d * d * cnt * fb;
+      mu[e] += d * fb;
+    }
+    cnt = ct;
+  }
+  if (ln < CC) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[wv][cc * 8 + e][0] = cnt;
+      red[wv][cc * 8 + e][1] = mu[e];
+      red[wv][cc * 8 + e][2] = m2[e];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < Cout) {
+    const int c = threadIdx.x;
+    float na = 0.f, ma = 0.f, qa = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float nb = red[v][c][0];
+      if (nb <= 0.f) continue;
+      const float nt = na + nb, d = red[v][c][1] - ma;
+      qa += red[v][c][2] + d * d * na * nb / nt;
+      ma += d * nb / nt;
+      na = nt;
+    }
+    stats[((size_t)blockIdx.x * Cout + c) * 2] = ma;
+    stats[((size_t)blockIdx.x * Cout + c) * 2 + 1] = qa;
   }
 }
 
@@ -289,8 +304,8 @@ int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, 
                      hipStream_t st) {
   HVIT_CHECK(g->Cout % 8 == 0 && g->Cout <= 256, "thin conv: Cout=%d must be a multiple of 8 <= 256", g->Cout);
   const int P = g->N * g->Hs * g->Ws;
-  const size_t smem = (TC_PIX * (g->Cout + 1) + 256) * sizeof(float);
-  dim3 grid(cdiv(cdiv(P, TC_PIX), TC_TILES));
+  const size_t smem = 0;
+  dim3 grid(cdiv(P, C1_BLOCK_PIX));
   if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
     hipLaunchKernelGGL((c1_fwd_kernel<bf16_t, bf16_t>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
                        (const bf16_t*)w, (bf16_t*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
@@ -306,6 +321,8 @@ int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, 
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }
+
+int hvit_thin_c1_bn_tile_rows() { return C1_BLOCK_PIX; }
 
 long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g) {
   const long P = (long)g->N * g->Hs * g->Ws;

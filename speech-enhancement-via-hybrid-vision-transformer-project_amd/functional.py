@@ -13,6 +13,8 @@ import math
 from dataclasses import dataclass
 from typing import Optional
 
+import ctypes as C
+
 import torch
 
 from . import _lib as L
@@ -189,10 +191,11 @@ class ConvBNActFn(torch.autograd.Function):
         invstd = torch.empty_like(mean)
         if training:
             P = N * H * W
-            nt = (P + 63) // 64  # BN partials per 64-row GEMM sub-tile
+            tr = L.lib().hvit_conv_bn_tile_rows(C.byref(g))  # rows per BN partial tile
+            nt = (P + tr - 1) // tr
             part = torch.empty((nt, Cout, 2), dtype=torch.float32, device=dev)
             call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, part.data_ptr(), None, s)
-            call("hvit_bn_finalize", part.data_ptr(), nt, 64, P, Cout, mean.data_ptr(), invstd.data_ptr(),
+            call("hvit_bn_finalize", part.data_ptr(), nt, tr, P, Cout, mean.data_ptr(), invstd.data_ptr(),
                  ptr(rmean), ptr(rvar), ptr(nbt), momentum, eps, s)
         else:
             call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, None, None, s)

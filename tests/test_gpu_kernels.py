@@ -196,14 +196,16 @@ def test_conv3x3_fwd_bwd(hv, dt, case):
     g = HF.geom(a1, C1, a2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
     wp = pack(hv, w, 0, dt)
     z = torch.empty(N, H, W, Cout, device=DEV)
-    nt = (N * H * W + 63) // 64
+    import ctypes
+    tr = l.lib().hvit_conv_bn_tile_rows(ctypes.byref(g))
+    nt = (N * H * W + tr - 1) // tr
     part = torch.empty(nt, Cout, 2, device=DEV)
     l.call("hvit_conv_fwd", dtc, g, wp.data_ptr(), None, z.data_ptr(), l.F32, part.data_ptr(), None, s())
     assert rel(nchw(z), ref) < tol(dt)
     # BatchNorm statistics from the fused partials
     mean = torch.empty(Cout, device=DEV)
     inv = torch.empty(Cout, device=DEV)
-    l.call("hvit_bn_finalize", part.data_ptr(), nt, 64, N * H * W, Cout, mean.data_ptr(), inv.data_ptr(), None,
+    l.call("hvit_bn_finalize", part.data_ptr(), nt, tr, N * H * W, Cout, mean.data_ptr(), inv.data_ptr(), None,
            None, None, 0.1, 1e-5, s())
     rm = ref.detach().mean((0, 2, 3))
     rv = ref.detach().var((0, 2, 3), unbiased=False)
