@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "gemm_kernel<unsigned short, 128, 128, hvit::LdDense<unsigned short, true>, hvit::LdDense<unsigned short, true> >"
+KERNEL = "gemm_kernel<unsigned short, 128, 128, hvit::LdDense<unsigned short, true>, hvit::LdDense<unsigned short, true>, 3"
 
 
 def main():
