@@ -1,0 +1,82 @@
+// C-ABI Linear fwd / dgrad / wgrad on the MFMA GEMM (see gemm_host.h).
+#include "gemm_host.h"
+
+extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int M, int N, int K,
+                               void* y, int y_dt, const hvit_epilogue_t* epi, void* stream) {
+  HVIT_CHECK(x && w && y, "hvit_linear_fwd: null pointer");
+  HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_fwd: bad shape M=%d N=%d K=%d", M, N, K);
+  HVIT_CHECK(aligned16(x) && aligned16(w), "hvit_linear_fwd: x/w must be 16-byte aligned");
+  if (int rc = check_epi(epi)) return rc;
+  Epi ep = to_epi(epi, y, y_dt, N);
+  ep.bias = bias;
+  DT_DISPATCH(dt, {
+    HVIT_CHECK(K % Elem<T>::PER16 == 0, "hvit_linear_fwd: K=%d must be a multiple of %d", K, Elem<T>::PER16);
+    return launch_gemm<T>(dense<T, true>(x, K, M, K), dense<T, true>(w, K, N, K), M, N, K, 1, ep,
+                          (hipStream_t)stream);
+  });
+}
+
+extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, int N, int K, void* dx, int dx_dt,
+                                 const hvit_epilogue_t* epi, void* stream) {
+  HVIT_CHECK(dy && w && dx, "hvit_linear_dgrad: null pointer");
+  HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_dgrad: bad shape");
+  HVIT_CHECK(aligned16(dy) && aligned16(w), "hvit_linear_dgrad: alignment");
+  if (int rc = check_epi(epi)) return rc;
+  Epi ep = to_epi(epi, dx, dx_dt, K);
+  DT_DISPATCH(dt, {
+    HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_dgrad: N, K alignment");
+    return launch_gemm<T>(dense<T, true>(dy, N, M, N), dense<T, false>(w, K, K, N), M, K, N, 1, ep,
+                          (hipStream_t)stream);
+  });
+}
+
+extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
+  // dw is [N_out x K_in] reduced over M rows; slabs only when splitting, each
+  // slab followed by N_out bias partials
+  int s = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
+  return s > 1 ? (long long)s * ((long long)N * K + N) : 0;
+}
+
+// db (nullable): bias gradient sum_m dy[m][n].  The fused path (bf16, db ==
+// dw + N*K) takes it from the A tiles the wgrad GEMM already stages (row sums
+// over the token reduction); otherwise a column reduction of dy.
+extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                                 float* ws, long long ws_elems, void* stream) {
+  HVIT_CHECK(dy && x && dw, "hvit_linear_wgrad: null pointer");
+  HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_wgrad: bad shape");
+  HVIT_CHECK(aligned16(dy) && aligned16(x), "hvit_linear_wgrad: alignment");
+  hipStream_t st = (hipStream_t)stream;
+  const long long NK = (long long)N * K;
+  int splits = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
+  if ((long long)splits * (NK + N) > ws_elems || !ws) splits = 1;
+  if (M == 0) {
+    (void)hipMemsetAsync(dw, 0, sizeof(float) * NK, st);
+    if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
+    return HVIT_OK;
+  }
+  const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK;
+  Epi ep;
+  ep.out_dt = HVIT_F32;
+  ep.ldo = K;
+  DT_DISPATCH(dt, {
+    HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_wgrad: N, K alignment");
+    splits = plan_splits<T>(M, splits);
+    ep.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
+    ep.out = splits > 1 ? (void*)ws : (void*)dw;
+    ep.slab_stride = NK + N;
+    if (fused_db) {
+      ep.rs_ptr = splits > 1 ? ws + NK : db;
+      ep.rs_stride = splits > 1 ? NK + N : 0;
+    }
+    int rc = launch_gemm<T>(dense<T, false>(dy, N, N, M), dense<T, false>(x, K, K, M), N, K, M, splits, ep, st,
+                            LIN_WG_TILE);
+    if (rc) return rc;
+  });
+  if (splits > 1) {
+    // sums [dw | db] when fused (db follows dw), else dw alone
+    if (int rc = hvit_sum_slabs_strided(ws, splits, NK + N, fused_db ? NK + N : NK, dw, stream)) return rc;
+  }
+  if (db && !fused_db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
+  return HVIT_OK;
+}
+
