@@ -66,12 +66,3 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     return HVIT_OK;
   });
 }
-
-#ifdef HVIT_GEMM_STAMPS
-__device__ unsigned long long hvit::g_gemm_stamps[65536 * 4];
-extern "C" int hvit_debug_gemm_stamps(unsigned long long* host, int n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(hvit::g_gemm_stamps), sizeof(unsigned long long) * n) == hipSuccess
-             ? 0
-             : 1;
-}
-#endif
