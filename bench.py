@@ -1,7 +1,8 @@
 """HybridViT training-step throughput on MI355X (BASELINE.json metric).
 
 One step = one HybridViT forward (train mode, dropout on) + CombinedLoss +
-backward + [DP gradient all-reduce] + clip_grad_norm_(1.0) + AdamW step, at
+backward + [DP gradient all-reduce] + clip_grad_norm_(1.0) + AdamW step (the
+clip fused into hvit FusedAdamW), at
 batch 32 per GPU of 1x256x256 synthetic magnitude spectrograms, bf16 compute
 (f32 master weights / statistics / gradients).  A frame is one STFT column, so
 one spectrogram = 256 frames.
@@ -150,10 +151,8 @@ def main():
     if world > 1:
         broadcast_module(model)
         reducer = GradAllReducer(model, bucket_mb=25, sliced={"pos_encoding.pos_embed": FRAMES})
-    try:
-        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
-    except Exception:
-        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, foreach=True)
+    # AdamW (training/optimizer.py:53-61) with clip_grad_norm_(1.0) (trainer.py:170-174) fused into it
+    opt = hv.FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, max_grad_norm=1.0)
     crit = hv.CombinedLoss()
     noisy, clean = spectrogram_batch(args.batch, seed=1234 + rank * args.batch)
     noisy, clean = noisy.cuda(), clean.cuda()
@@ -165,8 +164,7 @@ def main():
         loss.backward()
         if reducer is not None:
             reducer.finish()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
+        opt.step()  # clip to 1.0 + AdamW
         opt.zero_grad(set_to_none=True)
         return loss
 

@@ -30,6 +30,10 @@ extern "C" {
 enum { HVIT_F32 = 0, HVIT_BF16 = 1 };
 enum { HVIT_OK = 0, HVIT_ERR_ARG = 1, HVIT_ERR_LAUNCH = 2 };
 enum { HVIT_ACT_NONE = 0, HVIT_ACT_GELU_DUAL = 1, HVIT_ACT_TANH = 2, HVIT_ACT_GELU_BWD = 3 };
+/* flags of the backward calls that accumulate atomically: HVIT_ACC_ZEROED says
+ * the caller already zeroed the accumulator outputs (one fill for a whole
+ * backward pass), so the call skips its own clear. */
+enum { HVIT_ACC_ZEROED = 1 };
 
 /* Counter-based dropout: element i is kept iff a 16-bit hash of (seed, site, i)
  * is >= round(p * 65536); kept values are scaled by 1/(1-p).  Forward and
@@ -133,7 +137,8 @@ int hvit_layernorm_fwd(const float* x, const float* gamma, const float* beta, in
 long long hvit_layernorm_bwd_ws_elems(int M, int D);   /* f32 slab for dgamma/dbeta partials */
 int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean, const float* rstd,
                        const float* gamma, int M, int D, const float* resid, float* dx, float* dgamma,
-                       float* dbeta, float* ws, long long ws_elems, void* stream);  /* ws may be NULL */
+                       float* dbeta, float* ws, long long ws_elems, int flags, void* stream);  /* ws may be
+                       NULL; without ws, dgamma/dbeta are atomic targets (flags: HVIT_ACC_ZEROED) */
 
 /* ---- BatchNorm2d -> ReLU -> Dropout2d -> MaxPool2d(pool) tail of ConvBlock /
  * TransposeConvBlock (components.py:67-85, :161-178).  z is the pre-BN conv
@@ -142,7 +147,8 @@ int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* m
  * momentum and the unbiased variance, and increments num_batches_tracked);
  * eval: hvit_bn_eval_prep.  Backward: dz from dy = grad of the pooled output;
  * sums (hvit_bn_act_bwd_sums_elems(C) floats: [2][C] result followed by
- * per-slot partials) receives (dbeta, dgamma) in its first 2*C entries. */
+ * per-slot partials) receives (dbeta, dgamma) in its first 2*C entries; with
+ * flags & HVIT_ACC_ZEROED the caller has zeroed sums (else the call clears it). */
 long long hvit_bn_act_bwd_sums_elems(int C);
 int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C, float* mean,
                      float* invstd, float* running_mean, float* running_var, long long* num_batches_tracked,
@@ -154,7 +160,8 @@ int hvit_bn_act_fwd(int dt, const void* z, int N, int H, int W, int C, const flo
                     int y_dt, void* stream);
 int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean, const float* invstd,
                     const float* gamma, const float* beta, const hvit_dropout_t* dropout2d, int pool,
-                    const void* dy, int dy_dt, int training, void* dz, int dz_dt, float* sums, void* stream);
+                    const void* dy, int dy_dt, int training, void* dz, int dz_dt, float* sums, int flags,
+                    void* stream);
 
 /* ---- Resampling (F.interpolate bilinear align_corners=False, hybrid_vit.py:
  * 381-386 and :459-465; nearest x2 backward + concat split, components.py:146,
@@ -188,6 +195,55 @@ int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long 
 int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream);
 int hvit_droppath_scale(int B, const hvit_dropout_t* dropout, float* out, void* stream);  /* DropPath
                                                                      components.py:407-427 */
+
+/* ---- Train-step neighbours.
+ * CombinedLoss (training/losses.py:286-387; STOILoss :109-141, PerceptualLoss
+ * :270-283): pred/target are [B][P] f32 (P = C*F*T per sample, contiguous).
+ * hvit_loss_fwd writes stats [B][6] (per-sample sums the backward reads) and
+ * out[5] = {total, l1, mse, stoi, perceptual}; terms with weight 0 are left
+ * out of the total, as in the reference.  hvit_loss_bwd writes
+ * dpred = gout[0] * d total / d pred (gout may be NULL: 1). */
+typedef struct {
+  float w_l1, w_mse, w_stoi, w_perc;
+  int log_compression; /* log(x + 1e-8) on the L1 / MSE inputs (losses.py:319-321) */
+} hvit_loss_cfg_t;
+long long hvit_loss_ws_elems(int B, long long P);
+int hvit_loss_fwd(const float* pred, const float* tgt, int B, long long P, const hvit_loss_cfg_t* cfg, float* ws,
+                  long long ws_elems, float* stats, float* out, void* stream);
+int hvit_loss_bwd(const float* pred, const float* tgt, int B, long long P, const hvit_loss_cfg_t* cfg,
+                  const float* stats, const float* gout, float* dpred, void* stream);
+
+/* clip_grad_norm_ (training/trainer.py:170-174 -> torch.nn.utils, norm 2) and
+ * AdamW (training/optimizer.py:53-61 -> torch.optim.AdamW).  Tensor lists are
+ * passed by value to the kernels (40 per launch), so nothing is copied to the
+ * device.  hvit_clip_coef writes out[0] = total 2-norm of all tensors,
+ * out[1] = min(max_norm / (norm + 1e-6), 1); hvit_scale_tensors multiplies
+ * each tensor in place by coef[1] (torch's in-place clip).  hvit_adamw applies
+ * one AdamW step per item, multiplying each gradient by coef[1] when coef is
+ * non-NULL (clip fused into the update, gradients left untouched), and writes
+ * the updated weight as bf16 to shadow_bf16 when non-NULL. */
+typedef struct {
+  void* ptr;
+  long long numel;
+} hvit_tensor_t;
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  void* shadow_bf16;
+  long long numel;
+} hvit_adamw_item_t;
+typedef struct {
+  float lr, beta1, beta2, eps, weight_decay;
+  float bc1, bc2; /* 1 - beta1^step, 1 - beta2^step */
+} hvit_adamw_hyper_t;
+long long hvit_clip_ws_elems(int count);
+int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_norm, float* ws, long long ws_elems, float* out,
+                   void* stream);
+int hvit_scale_tensors(int count, const hvit_tensor_t* tensors, const float* coef, void* stream);
+int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp, const float* coef,
+               void* stream);
 
 #ifdef __cplusplus
 }

@@ -5,7 +5,8 @@ Public surface (mirrors the reference's ``models`` package, models/__init__.py,
 plus the factory it forgot to export):
     HybridViT, create_hybrid_vit, ConvBlock, TransposeConvBlock, FeedForward,
     PatchEmbedding, PositionalEncoding, MultiHeadSelfAttention,
-    TransformerEncoderBlock, VisionTransformer, CombinedLoss
+    TransformerEncoderBlock, VisionTransformer, CombinedLoss, create_loss_function,
+    FusedAdamW / clip_grad_norm_ / create_optimizer (training/optimizer.py, trainer.py:170-174)
 """
 
 from .hybrid_vit import (  # noqa: F401
@@ -22,10 +23,11 @@ from .hybrid_vit import (  # noqa: F401
     create_hybrid_vit,
 )
 from .losses import CombinedLoss, create_loss_function  # noqa: F401
+from .optim import FusedAdamW, clip_grad_norm_, create_optimizer  # noqa: F401
 from . import _lib  # noqa: F401
 
 __all__ = [
     "HybridViT", "create_hybrid_vit", "ConvBlock", "TransposeConvBlock", "FeedForward", "PatchEmbedding",
     "PositionalEncoding", "MultiHeadSelfAttention", "TransformerEncoderBlock", "VisionTransformer",
-    "CombinedLoss", "create_loss_function",
+    "CombinedLoss", "create_loss_function", "FusedAdamW", "clip_grad_norm_", "create_optimizer",
 ]

@@ -15,6 +15,7 @@ import torch
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD = 0, 1, 2, 3
+ACC_ZEROED = 1
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # HVIT_LIB selects an alternative in-tree build (kernel A/B benchmarking only)
@@ -51,6 +52,24 @@ class WPrepItem(C.Structure):
                 ("cout", i32), ("cin", i32), ("ks", i32)]
 
 
+class LossCfg(C.Structure):
+    _fields_ = [("w_l1", f32), ("w_mse", f32), ("w_stoi", f32), ("w_perc", f32), ("log_compression", i32)]
+
+
+class TensorRef(C.Structure):
+    _fields_ = [("ptr", vp), ("numel", i64)]
+
+
+class AdamWItem(C.Structure):
+    _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("shadow_bf16", vp),
+                ("numel", i64)]
+
+
+class AdamWHyper(C.Structure):
+    _fields_ = [("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32), ("bc1", f32),
+                ("bc2", f32)]
+
+
 P = C.POINTER
 _SIGS = {
     "hvit_last_error": ([], C.c_char_p),
@@ -69,12 +88,12 @@ _SIGS = {
     "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_layernorm_fwd": ([vp, vp, vp, i32, i32, f32, vp, i32, vp, vp, vp], i32),
     "hvit_layernorm_bwd_ws_elems": ([i32, i32], i64),
-    "hvit_layernorm_bwd": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, i64, vp], i32),
+    "hvit_layernorm_bwd": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, i64, i32, vp], i32),
     "hvit_bn_finalize": ([vp, i32, i32, i64, i32, vp, vp, vp, vp, vp, f32, f32, vp], i32),
     "hvit_bn_eval_prep": ([vp, vp, i32, f32, vp, vp, vp], i32),
     "hvit_bn_act_fwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, vp], i32),
     "hvit_bn_act_bwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, i32, vp,
-                         i32, vp, vp], i32),
+                         i32, vp, i32, vp], i32),
     "hvit_bn_act_bwd_sums_elems": ([i32], i64),
     "hvit_bilinear_fwd":([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_bilinear_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp], i32),
@@ -87,6 +106,13 @@ _SIGS = {
     "hvit_droppath_scale": ([i32, P(Dropout), vp, vp], i32),
     "hvit_weight_prep": ([i32, P(WPrepItem), vp], i32),
     "hvit_conv_bn_tile_rows": ([P(ConvGeom)], i32),
+    "hvit_loss_ws_elems": ([i32, i64], i64),
+    "hvit_loss_fwd": ([vp, vp, i32, i64, P(LossCfg), vp, i64, vp, vp, vp], i32),
+    "hvit_loss_bwd": ([vp, vp, i32, i64, P(LossCfg), vp, vp, vp, vp], i32),
+    "hvit_clip_ws_elems": ([i32], i64),
+    "hvit_clip_coef": ([i32, P(TensorRef), f32, vp, i64, vp, vp], i32),
+    "hvit_scale_tensors": ([i32, P(TensorRef), vp, vp], i32),
+    "hvit_adamw": ([i32, P(AdamWItem), P(AdamWHyper), vp, vp], i32),
 }
 
 EXPORTED = sorted(k for k in _SIGS)

@@ -341,7 +341,7 @@ extern "C" long long hvit_bn_act_bwd_sums_elems(int C) { return 2LL * C * (1 + B
 extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
                                const float* invstd, const float* gamma, const float* beta,
                                const hvit_dropout_t* dropout2d, int pool, const void* dy, int dy_dt,
-                               int training, void* dz, int dz_dt, float* sums, void* stream) {
+                               int training, void* dz, int dz_dt, float* sums, int flags, void* stream) {
   HVIT_CHECK(z && dy && dz && sums, "hvit_bn_act_bwd: null pointer");
   HVIT_CHECK(dz_dt == dt, "hvit_bn_act_bwd: dz dtype must equal z dtype");
   HVIT_CHECK(aligned16(z) && aligned16(dz) && aligned16(dy), "hvit_bn_act_bwd: alignment");
@@ -349,7 +349,7 @@ extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C
   const int cv = dt == HVIT_BF16 ? 8 : 4;
   if (int rc = make_args(a, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d, cv)) return rc;
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * (1 + BN_SLOTS), st);
+  if (!(flags & HVIT_ACC_ZEROED)) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * (1 + BN_SLOTS), st);
   if (dt == HVIT_BF16)
     return dy_dt == HVIT_BF16 ? bnact_bwd_t<bf16_t, bf16_t>(z, dy, a, sums, training, dz, st)
                               : bnact_bwd_t<bf16_t, float>(z, dy, a, sums, training, dz, st);

@@ -290,7 +290,7 @@ extern "C" long long hvit_layernorm_bwd_ws_elems(int M, int D) {
 extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean,
                                   const float* rstd, const float* gamma, int M, int D, const float* resid,
                                   float* dx, float* dgamma, float* dbeta, float* ws, long long ws_elems,
-                                  void* stream) {
+                                  int flags, void* stream) {
   HVIT_CHECK(dy && x && mean && rstd && gamma && dx && dgamma && dbeta, "hvit_layernorm_bwd: null pointer");
   HVIT_CHECK(D % 4 == 0 && D <= 1024 && D > 0, "hvit_layernorm_bwd: bad D=%d", D);
   HVIT_CHECK(aligned16(x) && aligned16(dx) && aligned16(gamma) && aligned16(dy) && (!resid || aligned16(resid)),
@@ -298,7 +298,7 @@ extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, con
   hipStream_t st = (hipStream_t)stream;
   const int nblk = cdiv(M, LNB_ROWS);
   const bool slab = M > 0 && ws && ws_elems >= hvit_layernorm_bwd_ws_elems(M, D);
-  if (!slab) {
+  if (!slab && !(flags & HVIT_ACC_ZEROED)) {
     (void)hipMemsetAsync(dgamma, 0, sizeof(float) * D, st);
     (void)hipMemsetAsync(dbeta, 0, sizeof(float) * D, st);
   }

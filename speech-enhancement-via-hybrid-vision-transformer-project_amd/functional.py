@@ -14,6 +14,7 @@ from dataclasses import dataclass
 from typing import Optional
 
 import ctypes as C
+import weakref
 
 import torch
 
@@ -25,6 +26,56 @@ F32, BF16 = L.F32, L.BF16
 
 def _empty(shape, dt, dev):
     return torch.empty(shape, dtype=L.torch_dtype(dt), device=dev)
+
+
+class ZSlot:
+    """A zeroed f32 accumulator (atomic target) that one backward call needs:
+    a slice of the forward pass's shared zero pool, or its own zeros when the
+    pool was never flushed (a Function used outside HybridViT.forward)."""
+
+    __slots__ = ("n", "t", "__weakref__")
+
+    def __init__(self, n):
+        self.n = n
+        self.t = None
+
+    def take(self, dev):
+        t, self.t = self.t, None  # the caller's reference is the only one left
+        return t if t is not None else torch.zeros(self.n, dtype=torch.float32, device=dev)
+
+
+_ZPENDING = []
+
+
+def zslot(n: int) -> ZSlot:
+    """Register an accumulator for this forward's backward (see zflush)."""
+    s = ZSlot(n)
+    if len(_ZPENDING) > 4096:
+        _ZPENDING[:] = [r for r in _ZPENDING if r() is not None]
+    _ZPENDING.append(weakref.ref(s))
+    return s
+
+
+def zflush(dev) -> None:
+    """Give every accumulator registered since the last flush its slice of ONE
+    zeroed buffer: one fill per forward instead of a clear per backward call
+    (LayerNorm dgamma/dbeta, BatchNorm slot sums, fused bias-grad column sums)."""
+    live = [s for s in (r() for r in _ZPENDING) if s is not None and s.t is None]
+    _ZPENDING.clear()
+    if not live:
+        return
+    offs, tot = [], 0
+    for s in live:
+        offs.append(tot)
+        tot += (s.n + 63) // 64 * 64  # 256-B aligned slices
+    buf = torch.zeros(tot, dtype=torch.float32, device=dev)
+    for s, o in zip(live, offs):
+        s.t = buf[o:o + s.n]
+
+
+def _zs(ctx, n):
+    """zslot(n) when this Function's backward can run (an input needs grad)."""
+    return zslot(n) if any(ctx.needs_input_grad) else None
 
 
 # Per-forward cache of prepared weights, filled by prep_weights() with one
@@ -40,13 +91,43 @@ def _prep_get(t, kind, dt):
     return None
 
 
+# Persistent bf16 copies of linear weights ("shadows"): id(param) ->
+# [weakref(param), bf16 tensor, param._version the copy matches or None].
+# FusedAdamW writes a parameter's shadow in the same pass that updates the
+# parameter (optim.py), so the next forward skips that cast.
+_SHADOW = {}
+
+
+def shadow_of(p):
+    """The persistent bf16 shadow of ``p`` (None if ``p`` has none)."""
+    e = _SHADOW.get(id(p))
+    return e[1] if e is not None and e[0]() is p else None
+
+
+def shadow_mark(p):
+    """Record that ``p``'s shadow now equals bf16(p) at its current version."""
+    e = _SHADOW.get(id(p))
+    if e is not None and e[0]() is p:
+        e[2] = p._version
+
+
 def prep_weights(items, dev):
     """items: [(param, kind, dt)], kind 0 = cast, 1/2 = conv pack mode 0/1.
-    Replaces the cache with freshly prepared copies (one kernel launch)."""
+    Replaces the cache with freshly prepared copies (one kernel launch); bf16
+    casts whose shadow is current are reused without a launch."""
     _PREP.clear()
     todo = []
     for w, kind, dt in items:
         if kind == 0 and L.dt_of(w) == dt:
+            continue
+        if kind == 0 and dt == BF16:
+            e = _SHADOW.get(id(w))
+            if e is None or e[0]() is not w or e[1].shape != w.shape:
+                e = _SHADOW[id(w)] = [weakref.ref(w), _empty(w.shape, dt, dev), None]
+            if e[2] == w._version:
+                _PREP[(id(w), kind, dt)] = (w._version, e[1], w)
+                continue
+            todo.append((w, kind, dt, e[1]))
             continue
         out = _empty(w.shape if kind == 0 else (w.numel(),), dt, dev)
         todo.append((w, kind, dt, out))
@@ -59,6 +140,8 @@ def prep_weights(items, dev):
     call("hvit_weight_prep", len(todo), arr, stream_ptr())
     for w, kind, dt, out in todo:
         _PREP[(id(w), kind, dt)] = (w._version, out, w)
+        if kind == 0 and dt == BF16:
+            shadow_mark(w)
 
 
 def cast(t: torch.Tensor, dt: int) -> torch.Tensor:
@@ -208,6 +291,7 @@ class ConvBNActFn(torch.autograd.Function):
         ctx.save_for_backward(x1, x2, w, gamma, beta)
         ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
         ctx.meta = (U, pool, training, dr, dt)
+        ctx.zs = _zs(ctx, L.lib().hvit_bn_act_bwd_sums_elems(Cout))
         return y
 
     @staticmethod
@@ -223,11 +307,11 @@ class ConvBNActFn(torch.autograd.Function):
         s = stream_ptr()
         dy = dy.contiguous()
         dz = _empty(z.shape, dt, dev)
-        sums = torch.empty(L.lib().hvit_bn_act_bwd_sums_elems(Cout), dtype=torch.float32, device=dev)
+        sums = ctx.zs.take(dev)
         call("hvit_bn_act_bwd", dt, z.data_ptr(), N, H, W, Cout, ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
              gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
-             dz.data_ptr(), dt, sums.data_ptr(), s)
-        dbeta, dgamma = sums[:Cout].clone(), sums[Cout:2 * Cout].clone()
+             dz.data_ptr(), dt, sums.data_ptr(), L.ACC_ZEROED, s)
+        dbeta, dgamma = sums[:Cout], sums[Cout:2 * Cout]
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
         dw = conv_wgrad(dt, g, dz, w.shape)
         dx1 = dx2 = None
@@ -269,6 +353,7 @@ class PatchEmbedFn(torch.autograd.Function):
         ctx.save_for_backward(feat, w)
         ctx.wp = wp
         ctx.meta = (Pp, dr, dt, Nt, pos.shape)
+        ctx.zs = _zs(ctx, D)
         return x0
 
     @staticmethod
@@ -283,7 +368,8 @@ class PatchEmbedFn(torch.autograd.Function):
         M = N * Nt
         gd = _empty((M, D), dt, dev)
         call("hvit_dropout_scale", dx0.data_ptr(), L.dt_of(dx0), M, D, dr, None, 1, gd.data_ptr(), dt, s)
-        db = col_sum(gd, M, D)
+        db = ctx.zs.take(dev)
+        call("hvit_reduce_rows", gd.data_ptr(), dt, M, D, D, 1, db.data_ptr(), s)
         dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
         call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
         g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
@@ -305,14 +391,16 @@ def _ln(x2d, gw, gb, dt):
     return y, mean, rstd
 
 
-def _ln_bwd(dy, x, mean, rstd, gw, resid):
+def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):
+    """zs: a zslot(2 * D) registered in the forward (dgamma | dbeta)."""
     M, D = x.shape
     dx = torch.empty((M, D), dtype=torch.float32, device=x.device)
-    dgw = torch.empty(D, dtype=torch.float32, device=x.device)
-    dgb = torch.empty_like(dgw)
+    acc = zs.take(x.device)
+    dgw, dgb = acc[:D], acc[D:2 * D]
     # atomic dgamma/dbeta partials (measured faster than the slab + reduce form at B*N = 8192)
     call("hvit_layernorm_bwd", dy.data_ptr(), L.dt_of(dy), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-         gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), None, 0, stream_ptr())
+         gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), None, 0, L.ACC_ZEROED,
+         stream_ptr())
     return dx, dgw, dgb
 
 
@@ -371,6 +459,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.save_for_backward(n1w, n2w)
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
+        ctx.zs = (_zs(ctx, 2 * D), _zs(ctx, 2 * D), _zs(ctx, hid))  # LN1, LN2 (dgamma|dbeta), fc1 bias grad
         if want_probs:
             ctx.mark_non_differentiable(probs)
         return x2.view(B, Nt, D), probs
@@ -391,13 +480,14 @@ class ViTBlockFn(torch.autograd.Function):
         call("hvit_dropout_scale", dx2.data_ptr(), F32, M, D, drf2, ptr(rs2), Nt, g2.data_ptr(), dt, s)
         df2w, df2b = linear_wgrad(dt, g2, a, M, D, hid, bias=True)
         dh = _empty((M, hid), dt, dev)
-        df1b = torch.zeros(hid, dtype=torch.float32, device=dev)  # fc1 bias grad: fused column sum
+        zln1, zln2, zf1b = ctx.zs
+        df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
         call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
              epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1, colsum=df1b), s)
         df1w = linear_wgrad(dt, dh, xn2, M, hid, D)
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
-        dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2)
+        dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2, zln2)
         # attention branch
         g1 = _empty((M, D), dt, dev)
         call("hvit_dropout_scale", dx1.data_ptr(), F32, M, D, drp, ptr(rs1), Nt, g1.data_ptr(), dt, s)
@@ -411,7 +501,7 @@ class ViTBlockFn(torch.autograd.Function):
         dqkvw, dqkvb = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, bias=True)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None, s)
-        dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1)
+        dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
                 None, None, None, None, None, None)
 
@@ -435,6 +525,7 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(nw)
         ctx.t = (x2d, xn, m, r, W)
         ctx.meta = (B, Nt, D, C, dt)
+        ctx.zs = _zs(ctx, 2 * D)
         return y
 
     @staticmethod
@@ -448,7 +539,7 @@ class HeadFn(torch.autograd.Function):
         dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
         call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32, None,
              stream_ptr())
-        dx, dnw, dnb = _ln_bwd(dxn, x2d, m, r, nw, None)
+        dx, dnw, dnb = _ln_bwd(dxn, x2d, m, r, nw, None, ctx.zs)
         return dx.view(B, Nt, D), dnw, dnb, dw, db, None, None
 
 

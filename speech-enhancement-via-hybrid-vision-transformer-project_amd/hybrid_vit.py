@@ -380,6 +380,7 @@ class HybridViT(nn.Module):
         self._check_device(x)
         dt = self._dt()
         h, skips = self._encoder(HF.CastFn.apply(self._nhwc(x), dt), dt, self._seed())
+        HF.zflush(x.device)
         return self._nchw(h), [self._nchw(s) for s in skips]
 
     def forward_transformer(self, x: torch.Tensor, spatial_shape: Tuple[int, int]) -> torch.Tensor:
@@ -393,7 +394,9 @@ class HybridViT(nn.Module):
         if self.training and self.dropout_p > 0:
             t = torch.nn.functional.dropout(t, self.dropout_p)
         t, _ = self._vit(t.contiguous(), dt, seed)
-        return self._nchw(self._head(t, spatial_shape, dt))
+        out = self._head(t, spatial_shape, dt)
+        HF.zflush(x.device)
+        return self._nchw(out)
 
     def forward_decoder(self, x: torch.Tensor, skip_features: List[torch.Tensor]) -> torch.Tensor:
         """hybrid_vit.py:352-394 (output before the final resize)."""
@@ -407,6 +410,7 @@ class HybridViT(nn.Module):
         for blk in self.decoder[:-1]:
             H, W = H * blk.up, W * blk.up
         out = self._decoder(xh, skips, (H * U, W * U), dt, self._seed())
+        HF.zflush(x.device)
         return self._nchw(out)
 
     def forward(self, x: torch.Tensor, return_attentions: bool = False):
@@ -424,6 +428,7 @@ class HybridViT(nn.Module):
         t, attns = self._vit(t, dt, seed, return_attentions)
         f = self._head(t, hw, dt)
         out = self._decoder(f, skips, (F, T), dt, seed)
+        HF.zflush(x.device)
         out = self._nchw(out)
         if return_attentions:
             return out, attns

@@ -1,0 +1,161 @@
+"""AdamW and gradient clipping of the reference training step on libhvit.so.
+
+The reference trainer builds ``torch.optim.AdamW(model.parameters(), lr,
+betas, eps, weight_decay, amsgrad)`` in ``create_optimizer``
+(training/optimizer.py:20-73, AdamW :53-61) and clips with
+``torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)``
+(training/trainer.py:170-174).  Here:
+
+* ``clip_grad_norm_`` -- same signature and in-place semantics (2-norm):
+  one multi-tensor sum-of-squares launch + one finalize block + one scale
+  launch, no host sync; returns the total norm as a 0-dim device tensor.
+* ``FusedAdamW`` -- torch.optim.AdamW's update rule (decoupled weight decay,
+  bias corrections, per-parameter ``step``) as one multi-tensor launch per 40
+  tensors.  With ``max_grad_norm`` the clip is fused: the update multiplies
+  each gradient by the clip coefficient as it reads it (gradients are not
+  rewritten; ``last_grad_norm`` holds the norm).  It also writes the bf16 copy
+  of each updated linear weight that the next bf16 forward's GEMMs read
+  (functional.shadow_*), so that forward skips the per-step weight cast.
+* ``create_optimizer`` -- the reference factory, returning FusedAdamW for
+  'adamw' and the torch optimizers for 'adam' / 'sgd'.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, Optional
+
+import torch
+
+from . import _lib as L
+from . import functional as HF
+
+_bump = getattr(torch.autograd.graph, "increment_version", None)
+
+
+def _grads(parameters) -> list:
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    return [p.grad for p in parameters if p.grad is not None]
+
+
+def _refs(tensors) -> "L.TensorRef * n":
+    arr = (L.TensorRef * max(len(tensors), 1))()
+    for i, t in enumerate(tensors):
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise TypeError("hvit: gradients must be contiguous float32 GPU tensors")
+        arr[i] = L.TensorRef(t.data_ptr(), t.numel())
+    return arr
+
+
+def _clip_coef(grads, max_norm: float) -> torch.Tensor:
+    """[norm, min(max_norm / (norm + 1e-6), 1)] on the device."""
+    dev = grads[0].device
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    ws_n = L.lib().hvit_clip_ws_elems(len(grads))
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
+    L.call("hvit_clip_coef", len(grads), _refs(grads), float(max_norm), ws.data_ptr(), ws_n, out.data_ptr(),
+           L.stream_ptr(dev))
+    return out
+
+
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_if_nonfinite: bool = False,
+                    foreach=None) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ (as called at trainer.py:171-174) for the
+    2-norm: grads *= min(max_norm / (total_norm + 1e-6), 1) in place."""
+    if float(norm_type) != 2.0:
+        raise NotImplementedError("hvit clip_grad_norm_: only the 2-norm (the trainer's) is implemented")
+    grads = _grads(parameters)
+    if not grads:
+        return torch.tensor(0.0)
+    out = _clip_coef(grads, max_norm)
+    if error_if_nonfinite and not torch.isfinite(out[0]).item():
+        raise RuntimeError("hvit clip_grad_norm_: the total norm of the gradients is non-finite")
+    L.call("hvit_scale_tensors", len(grads), _refs(grads), out.data_ptr(), L.stream_ptr(grads[0].device))
+    return out[0]
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW (amsgrad=False, maximize=False) on libhvit.so, with
+    optional fused gradient clipping (``max_grad_norm``)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
+                 max_grad_norm: Optional[float] = None, **unused):
+        if amsgrad or maximize:
+            raise NotImplementedError("hvit FusedAdamW: amsgrad / maximize are not implemented")
+        if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError("hvit FusedAdamW: invalid hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                                      maximize=False))
+        self.max_grad_norm = max_grad_norm
+        self.last_grad_norm: Optional[torch.Tensor] = None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        live = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if not live:
+            return loss
+        for p in live:
+            if p.grad.is_sparse:
+                raise RuntimeError("hvit FusedAdamW: sparse gradients are not supported")
+            if not p.is_cuda or p.dtype != torch.float32:
+                raise TypeError("hvit FusedAdamW: parameters must be float32 GPU tensors")
+        coef = None
+        if self.max_grad_norm is not None:
+            coef = _clip_coef([p.grad for p in live], self.max_grad_norm)
+            self.last_grad_norm = coef[0]
+        stream = L.stream_ptr(live[0].device)
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            by_step: Dict[float, list] = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                by_step.setdefault(float(st["step"]), []).append(p)
+            for step, ps in by_step.items():
+                items = (L.AdamWItem * len(ps))()
+                keep = []  # contiguous copies of strided grads live until the launch
+                for i, p in enumerate(ps):
+                    st = self.state[p]
+                    g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                    keep.append(g)
+                    sh = HF.shadow_of(p)
+                    items[i] = L.AdamWItem(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                           st["exp_avg_sq"].data_ptr(), sh.data_ptr() if sh is not None else None,
+                                           p.numel())
+                hp = L.AdamWHyper(float(group["lr"]), b1, b2, group["eps"], group["weight_decay"],
+                                  1.0 - b1 ** step, 1.0 - b2 ** step)
+                L.call("hvit_adamw", len(ps), items, hp, coef.data_ptr() if coef is not None else None, stream)
+                for p in ps:
+                    if _bump is not None:
+                        _bump(p)  # the kernel wrote p in place: keep version counters honest
+                    HF.shadow_mark(p)
+        return loss
+
+
+def create_optimizer(model: torch.nn.Module, config: Dict[str, Any]) -> torch.optim.Optimizer:
+    """training/optimizer.py:20-73 with AdamW on the HIP path."""
+    oc = config.get("optimizer", {})
+    name = oc.get("name", "adamw").lower()
+    lr = oc.get("lr", 1e-4)
+    wd = oc.get("weight_decay", 0.01)
+    if name == "adamw":
+        return FusedAdamW(model.parameters(), lr=lr, betas=oc.get("betas", (0.9, 0.999)), eps=oc.get("eps", 1e-8),
+                          weight_decay=wd, amsgrad=oc.get("amsgrad", False))
+    if name == "adam":
+        return torch.optim.Adam(model.parameters(), lr=lr, betas=oc.get("betas", (0.9, 0.999)),
+                                eps=oc.get("eps", 1e-8), weight_decay=wd, amsgrad=oc.get("amsgrad", False))
+    if name == "sgd":
+        return torch.optim.SGD(model.parameters(), lr=lr, momentum=oc.get("momentum", 0.9), weight_decay=wd,
+                               nesterov=oc.get("nesterov", True))
+    raise ValueError(f"Unknown optimizer: {name}")

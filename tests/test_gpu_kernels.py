@@ -347,16 +347,23 @@ def test_layernorm(hv, dt, M, D):
     ws = torch.empty(ws_n, device="cuda")
     l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
            g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), ws.data_ptr(),
-           ws_n, s())
+           ws_n, 0, s())
     assert rel(dx - resid, x.grad) < 1e-4
     assert rel(dg, g.grad) < 1e-4
     assert rel(db, b.grad) < 1e-4
     # atomic path (no workspace)
     l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), None, 0, s())
+           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), None, 0, 0, s())
     assert rel(dx - resid, x.grad) < 1e-4
     assert rel(dg, g.grad) < 1e-4
     assert rel(db, b.grad) < 1e-4
+    # atomic path into caller-zeroed accumulators (HVIT_ACC_ZEROED: no internal clear)
+    acc = torch.zeros(2 * D, device=DEV)
+    l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), acc.data_ptr(), acc[D:].data_ptr(), None, 0,
+           l.ACC_ZEROED, s())
+    assert rel(acc[:D], g.grad) < 1e-4
+    assert rel(acc[D:], b.grad) < 1e-4
 
 
 # ------------------------------------------------------------- batchnorm ---
@@ -394,8 +401,14 @@ def test_bn_act(hv, dt, N, H, W, C, pool, p):
     sums = torch.empty(l.lib().hvit_bn_act_bwd_sums_elems(C), device=DEV)
     gya = nhwc(gy)
     l.call("hvit_bn_act_bwd", dtc, za.data_ptr(), N, H, W, C, mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
-           beta.data_ptr(), dr, pool, gya.data_ptr(), l.F32, 1, dz.data_ptr(), dtc, sums.data_ptr(), s())
+           beta.data_ptr(), dr, pool, gya.data_ptr(), l.F32, 1, dz.data_ptr(), dtc, sums.data_ptr(), 0, s())
     assert rel(nchw(dz.float()), zr.grad) < (1e-4 if dt == "f32" else 1e-2)  # dz is stored in z's dtype
+    assert rel(sums[:C], beta.grad) < 1e-4
+    assert rel(sums[C:2 * C], gamma.grad) < 1e-4
+    sums.zero_()  # caller-zeroed slots (HVIT_ACC_ZEROED)
+    l.call("hvit_bn_act_bwd", dtc, za.data_ptr(), N, H, W, C, mean.data_ptr(), inv.data_ptr(), gamma.data_ptr(),
+           beta.data_ptr(), dr, pool, gya.data_ptr(), l.F32, 1, dz.data_ptr(), dtc, sums.data_ptr(), l.ACC_ZEROED,
+           s())
     assert rel(sums[:C], beta.grad) < 1e-4
     assert rel(sums[C:2 * C], gamma.grad) < 1e-4
 
