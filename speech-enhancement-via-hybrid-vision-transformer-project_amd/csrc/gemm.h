@@ -824,6 +824,23 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
   const bool full = n + 3 < N;
   const int nv = full ? 4 : N - n;
   const f32x4 bias4 = (ep.bias && nok) ? load4(ep.bias, n, nv, HVIT_F32) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  // EK_GELU_BWD with a bf16 h (the train path): this thread's h values for the
+  // whole tile (NR rows x 4 columns per half) are loaded here, before the K
+  // loop, so their HBM latency hides behind the MFMAs instead of stalling the
+  // epilogue (full tiles only: the host guarantees them for this kind)
+  constexpr int NPRE = EK == EK_GELU_BWD ? HALVES * NR : 1;
+  uint2 hpre[NPRE];
+  const bool hpre_on = EK == EK_GELU_BWD && ep.aux_dt == HVIT_BF16;
+  if constexpr (EK == EK_GELU_BWD) {
+    if (hpre_on) {
+#pragma unroll
+      for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+          hpre[hh * NR + i] =
+              *(const uint2*)((const bf16_t*)ep.aux + (long)(m0 + hh * 64 + r0 + i * RSTEP) * ep.ldaux + n);
+    }
+  }
 
   GEMM_STAMP(0);
   const bool interior = m0 + BM <= M && n0 + BN <= N && ((kend - kbeg) % C::BK) == 0 && la.fast() && lb.fast();
@@ -958,7 +975,13 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
           const int m = mbase + r0 + i * RSTEP;
-          h[i] = load4v<true>(ep.aux, (long)m * ep.ldaux + n, 4, ep.aux_dt);
+          if (hpre_on) {
+            const uint2 u = hpre[hh * NR + i];
+            h[i] = (f32x4){__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                           __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+          } else {
+            h[i] = load4v<true>(ep.aux, (long)m * ep.ldaux + n, 4, ep.aux_dt);
+          }
         }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
                                                     const float* __restrict__ g, const float* __restrict__ resid,
                                                     float* __restrict__ dx, float* __restrict__ dgamma,
                                                     float* __restrict__ dbeta, float* __restrict__ ws, int M, int D) {
-  __shared__ float red[4][2][1024];
+  __shared__ float red[4][2][MAXV * 256];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   f32x4 ag[MAXV], ab[MAXV], gam[MAXV];
 #pragma unroll
@@ -93,34 +93,33 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     const int c = lane * 4 + i * 256;
     gam[i] = c < D ? *(const f32x4*)(g + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  // the wave's rows are software-pipelined: row r+1's x / dy / resid loads are
-  // issued before row r is reduced and stored
-  const int row0 = blockIdx.x * LNB_ROWS + w * (LNB_ROWS / 4);
-  const int nrows = max(0, min(LNB_ROWS / 4, M - row0));
-  f32x4 xn[MAXV], dn[MAXV], rn[MAXV];
-  auto fetch = [&](int row) {
+  // all of the wave's rows are loaded before any is reduced: RPW rows x
+  // (x, dy, resid) in flight per wave hide the HBM latency at this occupancy
+  constexpr int RPW = LNB_ROWS / 4;
+  const int row0 = blockIdx.x * LNB_ROWS + w * RPW;
+  f32x4 xv[RPW][MAXV], dv[RPW][MAXV], rv[RPW][MAXV];
+  float mu[RPW], rs[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = min(row0 + r, M - 1);  // rows past M re-read the last row; never stored
+    mu[r] = mean[row];
+    rs[r] = rstd[row];
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int c = lane * 4 + i * 256;
       if (c < D) {
-        xn[i] = *(const f32x4*)(x + (long)row * D + c);
-        dn[i] = load_row4<TD>(dy + (long)row * D + c);
-        rn[i] = resid ? *(const f32x4*)(resid + (long)row * D + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        xv[r][i] = *(const f32x4*)(x + (long)row * D + c);
+        dv[r][i] = load_row4<TD>(dy + (long)row * D + c);
+        rv[r][i] = resid ? *(const f32x4*)(resid + (long)row * D + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      } else {
+        xv[r][i] = dv[r][i] = rv[r][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     }
-  };
-  if (nrows > 0) fetch(row0);
-  for (int rr = 0; rr < nrows; ++rr) {
-    const int row = row0 + rr;
-    f32x4 xv[MAXV], dv[MAXV], rv[MAXV];
+  }
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      xv[i] = xn[i];
-      dv[i] = dn[i];
-      rv[i] = rn[i];
-    }
-    if (rr + 1 < nrows) fetch(row + 1);
-    const float mu = mean[row], rs = rstd[row];
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    if (row >= M) break;  // uniform per wave
     f32x4 xh[MAXV], gy[MAXV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -129,13 +128,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
       if (c < D) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float xhat = (xv[i][e] - mu) * rs;
+          const float xhat = (xv[r][i][e] - mu[r]) * rs[r];
           xh[i][e] = xhat;
-          gy[i][e] = dv[i][e] * gam[i][e];
+          gy[i][e] = dv[r][i][e] * gam[i][e];
           s1 += gy[i][e];
           s2 += gy[i][e] * xhat;
-          ag[i][e] += dv[i][e] * xhat;
-          ab[i][e] += dv[i][e];
+          ag[i][e] += dv[r][i][e] * xhat;
+          ab[i][e] += dv[r][i][e];
         }
       }
     }
@@ -147,8 +146,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
       if (c < D) {
         f32x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rs * (gy[i][e] - s1 - xh[i][e] * s2);
-        *(f32x4*)(dx + (long)row * D + c) = o + rv[i];
+        for (int e = 0; e < 4; ++e) o[e] = rs[r] * (gy[i][e] - s1 - xh[i][e] * s2);
+        *(f32x4*)(dx + (long)row * D + c) = o + rv[r][i];
       }
     }
   }

@@ -50,6 +50,56 @@ constexpr int TC_PIX = 64;   // pixels per stats tile (= BN partial tile rows)
 constexpr int TC_TILES = 16;  // tiles per block
 
 // ---------------------------------------------------------------- Cin = 1 ---
+// A block owns a contiguous range [p0, pend) of flattened pixels p = (n, y, x)
+// of the single-channel input.  Every 3x3 tap of those pixels that lies inside
+// its image sits at flattened offset p + dy*W + dx, so the block stages the
+// range widened by W + 1 on each side into LDS once (f32) and reads taps from
+// there: no per-tap global loads, no per-pixel integer division (PixCursor
+// walks (y, x) incrementally).  Dynamic LDS: strip_floats(pixels, W) floats.
+__host__ __device__ inline int strip_floats(int pix, int W) { return pix + 2 * W + 2; }
+
+template <typename T>
+__device__ __forceinline__ long stage_strip(const T* __restrict__ x, int P, int p0, int pend, int W, float* xs) {
+  const long base = (long)p0 - W - 1;
+  const int n = (pend - p0) + 2 * W + 2;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const long q = base + i;
+    xs[i] = (q >= 0 && q < P) ? Elem<T>::to_f(x[q]) : 0.f;
+  }
+  __syncthreads();
+  return base;
+}
+
+struct PixCursor {
+  int y, x;
+  __device__ __forceinline__ PixCursor(int p, int H, int W) {
+    const int rem = p % (H * W);
+    y = rem / W;
+    x = rem - y * W;
+  }
+  __device__ __forceinline__ void advance(int d, int H, int W) {
+    x += d;
+    while (x >= W) {
+      x -= W;
+      if (++y == H) y = 0;
+    }
+  }
+};
+
+// xv[t] = input at tap t = (dy+1)*3 + (dx+1) of the pixel whose staged centre is c
+__device__ __forceinline__ void taps9(const float* c, int y, int x, int H, int W, float* xv) {
+  const bool up = y > 0, dn = y + 1 < H, lf = x > 0, rt = x + 1 < W;
+  xv[0] = (up && lf) ? c[-W - 1] : 0.f;
+  xv[1] = up ? c[-W] : 0.f;
+  xv[2] = (up && rt) ? c[-W + 1] : 0.f;
+  xv[3] = lf ? c[-1] : 0.f;
+  xv[4] = c[0];
+  xv[5] = rt ? c[1] : 0.f;
+  xv[6] = (dn && lf) ? c[W - 1] : 0.f;
+  xv[7] = dn ? c[W] : 0.f;
+  xv[8] = (dn && rt) ? c[W + 1] : 0.f;
+}
+
 // z[p][co] = sum_tap x[p + tap] * w[co][tap]; BN partials per 64-pixel tile.
 // BN partial tile of the Cin = 1 path: one (mean, M2) per channel and block
 constexpr int C1_BLOCK_PIX = TC_PIX * TC_TILES;
@@ -63,6 +113,7 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
   // lanes of the same group merge (Chan) through shuffles, the four waves
   // through LDS, once per block: BN partial tile = the block's pixels.
   __shared__ float red[4][256][3];  // [wave][channel][count, mean, M2]
+  extern __shared__ float xs[];     // the block's input strip (stage_strip)
   const int CC = Cout / 8;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC, lanes = 256 / CC;
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -72,20 +123,15 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
 #pragma unroll
     for (int e = 0; e < 8; ++e) wr[t][e] = Elem<T>::to_f(w[(cc * 8 + e) * 9 + t]);
   const int P = N * H * W;
-  const int HW = H * W;
   const int p0 = blockIdx.x * C1_BLOCK_PIX, pend = min(P, p0 + C1_BLOCK_PIX);
+  const long base = stage_strip(x, P, p0, pend, W, xs);
   float mu[8], m2[8], cnt = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) mu[e] = m2[e] = 0.f;
-  for (int p = p0 + pl; p < pend; p += lanes) {
-    const int n = p / HW, rem = p - n * HW, y = rem / W, xx = rem - y * W;
-    const T* xb = x + n * HW;
+  PixCursor pc(p0 + pl, H, W);
+  for (int p = p0 + pl; p < pend; p += lanes, pc.advance(lanes, H, W)) {
     float xv[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
-      xv[t] = (iy >= 0 && ix >= 0 && iy < H && ix < W) ? Elem<T>::to_f(xb[iy * W + ix]) : 0.f;
-    }
+    taps9(xs + (p - base), pc.y, pc.x, H, W, xv);
     float o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -154,29 +200,33 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, 
   // thread = (8-channel group cc, pixel lane); 72 accumulators in registers;
   // wave-level shuffles then LDS across the 4 waves.
   __shared__ float red[4][256 * 9];
+  extern __shared__ float xs[];  // the block's input strip (stage_strip)
   const int CC = Cout / 8;  // power of two, <= 32
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC, lanes = 256 / CC;
   const int P = N * H * W;
-  const int HW = H * W;
   const int pbeg = blockIdx.x * WG_PIX, pend = min(P, pbeg + WG_PIX);
+  const long base = stage_strip(x, P, pbeg, pend, W, xs);
   float acc[9][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
-#pragma unroll 4
-  for (int p = pbeg + pl; p < pend; p += lanes) {
+  // dz for the next pixel is loaded before the current one is accumulated
+  PixCursor pc(pbeg + pl, H, W);
+  int p = pbeg + pl;
+  float dn[8];
+  if (p < pend) Vec8<T>::load(dz + (size_t)p * Cout + cc * 8, dn);
+  for (; p < pend; p += lanes, pc.advance(lanes, H, W)) {
     float d[8];
-    Vec8<T>::load(dz + (size_t)p * Cout + cc * 8, d);
-    const int n = p / HW, rem = p - n * HW, y = rem / W, xx = rem - y * W;
-    const T* xb = x + n * HW;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int iy = y + t / 3 - 1, ix = xx + t % 3 - 1;
-      const float xv = (iy >= 0 && ix >= 0 && iy < H && ix < W) ? Elem<T>::to_f(xb[iy * W + ix]) : 0.f;
+    for (int e = 0; e < 8; ++e) d[e] = dn[e];
+    if (p + lanes < pend) Vec8<T>::load(dz + (size_t)(p + lanes) * Cout + cc * 8, dn);
+    float xv[9];
+    taps9(xs + (p - base), pc.y, pc.x, H, W, xv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[t][e] += d[e] * xv;
-    }
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t][e] += d[e] * xv[t];
   }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
@@ -299,25 +349,33 @@ __global__ __launch_bounds__(256) void o1_wgrad_kernel(const T* __restrict__ x, 
 
 using namespace hvit;
 
+// dynamic LDS above the 64 KiB default needs an opt-in per kernel
+template <typename K>
+static void allow_lds(K kern, size_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 // host dispatchers (called from gemm_api.hip) -----------------------------------
 int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats,
                      hipStream_t st) {
   HVIT_CHECK(g->Cout % 8 == 0 && g->Cout <= 256, "thin conv: Cout=%d must be a multiple of 8 <= 256", g->Cout);
   const int P = g->N * g->Hs * g->Ws;
-  const size_t smem = 0;
+  const size_t smem = sizeof(float) * strip_floats(C1_BLOCK_PIX, g->Ws);
+  HVIT_CHECK(smem + sizeof(float) * 4 * 256 * 3 <= 160 * 1024, "thin conv: W=%d too wide for the LDS strip", g->Ws);
   dim3 grid(cdiv(P, C1_BLOCK_PIX));
+  auto go = [&](auto kern, auto xp, auto yp) {
+    allow_lds(kern, smem);
+    hipLaunchKernelGGL(kern, grid, dim3(256), smem, st, xp, (decltype(xp))w, yp, stats, g->N, g->Hs, g->Ws, g->Cout);
+  };
   if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
-    hipLaunchKernelGGL((c1_fwd_kernel<bf16_t, bf16_t>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
-                       (const bf16_t*)w, (bf16_t*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+    go(c1_fwd_kernel<bf16_t, bf16_t>, (const bf16_t*)g->src1, (bf16_t*)y);
   else if (dt == HVIT_BF16)
-    hipLaunchKernelGGL((c1_fwd_kernel<bf16_t, float>), grid, dim3(256), smem, st, (const bf16_t*)g->src1,
-                       (const bf16_t*)w, (float*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+    go(c1_fwd_kernel<bf16_t, float>, (const bf16_t*)g->src1, (float*)y);
   else if (y_dt == HVIT_F32)
-    hipLaunchKernelGGL((c1_fwd_kernel<float, float>), grid, dim3(256), smem, st, (const float*)g->src1,
-                       (const float*)w, (float*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+    go(c1_fwd_kernel<float, float>, (const float*)g->src1, (float*)y);
   else
-    hipLaunchKernelGGL((c1_fwd_kernel<float, bf16_t>), grid, dim3(256), smem, st, (const float*)g->src1,
-                       (const float*)w, (bf16_t*)y, stats, g->N, g->Hs, g->Ws, g->Cout);
+    go(c1_fwd_kernel<float, bf16_t>, (const float*)g->src1, (bf16_t*)y);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }
@@ -335,12 +393,18 @@ int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float*
   const long P = (long)g->N * g->Hs * g->Ws;
   const int nb = (int)((P + WG_PIX - 1) / WG_PIX);
   HVIT_CHECK(ws && ws_elems >= (long long)nb * g->Cout * 9, "thin conv wgrad: workspace too small");
-  if (dt == HVIT_BF16)
-    hipLaunchKernelGGL((c1_wgrad_kernel<bf16_t>), dim3(nb), dim3(256), 0, st, (const bf16_t*)g->src1,
+  const size_t smem = sizeof(float) * strip_floats(WG_PIX, g->Ws);
+  HVIT_CHECK(smem + sizeof(float) * 4 * 256 * 9 <= 160 * 1024, "thin conv wgrad: W=%d too wide for the LDS strip",
+             g->Ws);
+  if (dt == HVIT_BF16) {
+    allow_lds(c1_wgrad_kernel<bf16_t>, smem);
+    hipLaunchKernelGGL((c1_wgrad_kernel<bf16_t>), dim3(nb), dim3(256), smem, st, (const bf16_t*)g->src1,
                        (const bf16_t*)dz, ws, g->N, g->Hs, g->Ws, g->Cout);
-  else
-    hipLaunchKernelGGL((c1_wgrad_kernel<float>), dim3(nb), dim3(256), 0, st, (const float*)g->src1,
+  } else {
+    allow_lds(c1_wgrad_kernel<float>, smem);
+    hipLaunchKernelGGL((c1_wgrad_kernel<float>), dim3(nb), dim3(256), smem, st, (const float*)g->src1,
                        (const float*)dz, ws, g->N, g->Hs, g->Ws, g->Cout);
+  }
   HVIT_LAUNCH_CHECK();
   return hvit_sum_slabs(ws, nb, (long long)g->Cout * 9, dw, st);
 }

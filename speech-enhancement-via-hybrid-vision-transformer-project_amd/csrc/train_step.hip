@@ -180,11 +180,11 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
 
 // ------------------------------------------------------- clip + AdamW ------
 constexpr int MT_MAX = 40;      // tensors per launch (kernel arguments by value)
-constexpr int SUMSQ_GRID = 512; // partials per sum-of-squares launch
+constexpr int SUMSQ_GRID = 1024; // partials per sum-of-squares launch
 
 struct SumsqArgs {
   int count;
-  long start[MT_MAX + 1];  // prefix sums of 4-element units
+  long start[MT_MAX + 1];  // prefix sums of 4-element units (sum of squares: of SQ_TILE-unit tiles)
   long n[MT_MAX];
   const float* g[MT_MAX];
 };
@@ -200,18 +200,37 @@ __device__ __forceinline__ f32x4 load_unit(const float* p, long u, long n) {
   return v;
 }
 
+// multi-tensor chunking: the tensors' 4-element units are cut into tiles of
+// SQ_TILE units (a tensor's last tile may be short); blocks take tiles
+// round-robin and find a tile's tensor in the tile prefix table (a uniform
+// scalar walk), each thread keeping SQ_TILE / 256 independent loads in flight
+constexpr int SQ_TILE = 1024;
+__device__ __forceinline__ float sq4(f32x4 v) { return v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]; }
+
 __global__ __launch_bounds__(256) void sumsq_kernel(SumsqArgs a, float* __restrict__ part) {
   __shared__ float red[4];
-  const long total = a.start[a.count];
+  const long tiles = a.start[a.count];  // start[] holds tile prefix sums here
   int j = 0;
-  float s = 0.f;
-  for (long u = (long)blockIdx.x * 256 + threadIdx.x; u < total; u += (long)gridDim.x * 256) {
-    while (u >= a.start[j + 1]) ++j;
-    const f32x4 v = load_unit(a.g[j], u - a.start[j], a.n[j]);
-    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  float s[SQ_TILE / 256] = {};
+  for (long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    while (t >= a.start[j + 1]) ++j;
+    const float* g = a.g[j];
+    const long n = a.n[j];
+    const long u0 = (t - a.start[j]) * SQ_TILE + threadIdx.x;
+    f32x4 v[SQ_TILE / 256];
+#pragma unroll
+    for (int k = 0; k < SQ_TILE / 256; ++k) {
+      const long u = u0 + k * 256;
+      v[k] = 4 * u < n ? load_unit(g, u, n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < SQ_TILE / 256; ++k) s[k] += sq4(v[k]);
   }
-  s = block_sum256(s, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = s;
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < SQ_TILE / 256; ++k) tot += s[k];
+  tot = block_sum256(tot, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
 // out[0] = total norm, out[1] = min(max_norm / (norm + 1e-6), 1)
@@ -374,7 +393,7 @@ extern "C" long long hvit_clip_ws_elems(int count) {
   return count <= 0 ? 0 : (long long)cdiv(count, MT_MAX) * SUMSQ_GRID;
 }
 
-static int fill_sumsq(SumsqArgs& a, const hvit_tensor_t* t, int base, int count) {
+static int fill_sumsq(SumsqArgs& a, const hvit_tensor_t* t, int base, int count, long per = 1) {
   a.count = count;
   a.start[0] = 0;
   for (int k = 0; k < count; ++k) {
@@ -382,7 +401,8 @@ static int fill_sumsq(SumsqArgs& a, const hvit_tensor_t* t, int base, int count)
     HVIT_CHECK(x.ptr && x.numel >= 0, "hvit: tensor %d: null pointer or negative numel", base + k);
     a.g[k] = (const float*)x.ptr;
     a.n[k] = (long)x.numel;
-    a.start[k + 1] = a.start[k] + (long)((x.numel + 3) / 4);
+    const long units = (long)((x.numel + 3) / 4);
+    a.start[k + 1] = a.start[k] + (units + per - 1) / per;  // per = units per table entry
   }
   return HVIT_OK;
 }
@@ -395,7 +415,7 @@ extern "C" int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_n
   int nparts = 0;
   for (int base = 0; base < count; base += MT_MAX) {
     SumsqArgs a;
-    if (int rc = fill_sumsq(a, grads, base, std::min(MT_MAX, count - base))) return rc;
+    if (int rc = fill_sumsq(a, grads, base, std::min(MT_MAX, count - base), SQ_TILE)) return rc;
     hipLaunchKernelGGL(sumsq_kernel, dim3(SUMSQ_GRID), dim3(256), 0, st, a, ws + nparts);
     HVIT_LAUNCH_CHECK();
     nparts += SUMSQ_GRID;

@@ -88,10 +88,11 @@ def test_linear_fwd_epilogues(hv, dt):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-def test_linear_dgrad_gelu_bwd(hv, dt):
+@pytest.mark.parametrize("M", [300, 512])  # 512: full tiles -> the compile-time GELU_BWD epilogue (h prefetch)
+def test_linear_dgrad_gelu_bwd(hv, dt, M):
     l = L(hv)
     HF = __import__("hvit_amd.functional", fromlist=["x"])
-    M, N, K = 300, 256, 512
+    N, K = 256, 512
     dy = torch.randn(M, N, device=DEV).to(tdt(dt))
     w = (torch.randn(N, K, device=DEV) / N ** 0.5).to(tdt(dt))
     hpre = torch.randn(M, K, device=DEV).to(tdt(dt))
@@ -170,6 +171,7 @@ CONV_CASES = [
     (2, 8, 8, 256, 128, 2, 128, 3),
     (1, 9, 7, 32, 16, 2, 16, 3),
     (2, 33, 47, 1, 0, 1, 8, 3),
+    (3, 20, 256, 1, 0, 1, 64, 3),  # Cin = 1 strips spanning images (enc0 shape class)
     (2, 12, 10, 64, 0, 1, 1, 3),
 ]
 
