@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--mode", default="train", choices=["train", "infer"],
+                    help="infer: BASELINE config 2 (forward only, eval, no grad)")
+    ap.add_argument("--variant", default="default", choices=["default", "large"],
+                    help="large: BASELINE config 5 shape (D=768, 12 heads, 12 layers; bf16, not fp8)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing loop (used for rocprofv3 --pmc passes)")
     return ap.parse_args()
@@ -146,7 +150,8 @@ def main():
     from hvit_amd.dp import GradAllReducer, broadcast_module
 
     torch.manual_seed(1234)
-    model = hv.HybridViT(precision=args.precision).cuda().train()
+    arch = dict(embed_dim=768, num_heads=12, num_layers=12) if args.variant == "large" else {}
+    model = hv.HybridViT(precision=args.precision, **arch).cuda().train()
     reducer = None
     if world > 1:
         broadcast_module(model)
@@ -158,7 +163,13 @@ def main():
     noisy, clean = noisy.cuda(), clean.cuda()
     torch.manual_seed(1000 + rank)
 
+    if args.mode == "infer":
+        model.eval()
+
     def step():
+        if args.mode == "infer":
+            with torch.no_grad():
+                return model(noisy).float().mean()
         y = model(noisy)
         loss = crit(y, clean)
         loss.backward()
@@ -194,10 +205,11 @@ def main():
     if rank == 0:
         roof = dominant_kernel_roofline(hv, args.batch)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.mode == "train" and args.variant == "default":
             cpu = cpu_baseline(args.batch, args.cpu_seconds)
         out = {
-            "metric": "spectrogram-frames/sec/GPU (fwd+bwd) on 256x256 mag-spec, batch 32; 1/2/4/8 GPU",
+            "metric": ("spectrogram-frames/sec/GPU (fwd+bwd) on 256x256 mag-spec, batch 32; 1/2/4/8 GPU"
+                       if args.mode == "train" else "spectrogram-frames/sec/GPU (fwd only, eval) on 256x256 mag-spec"),
             "value": round(value, 1),
             "unit": "spectrogram-frames/s",
             "n_gpus": world,
@@ -209,8 +221,11 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (harmonic+noise 16 kHz waveforms, host STFT 512/128 hann, min-max, 256x256)",
-            "config": {"workload": "HybridViT default (enc 64/128/256, 6x8-head d512 ViT, dec 256/128/64/1) train "
-                                   "step: fwd + CombinedLoss + bwd + clip + AdamW",
+            "config": {"workload": (("HybridViT default (enc 64/128/256, 6x8-head d512 ViT, dec 256/128/64/1)"
+                                     if args.variant == "default" else
+                                     "HybridViT large (enc 64/128/256, 12x12-head d768 ViT, dec 256/128/64/1)")
+                                    + (" train step: fwd + CombinedLoss + bwd + clip + AdamW" if args.mode == "train"
+                                       else " inference forward (eval, no grad)")),
                        "global_batch": world * args.batch, "seq_len": 256, "input": [args.batch, 1, 256, 256],
                        "parallelism": f"dp{world}"},
             "spectrograms_per_s": round(spectros, 2),

@@ -9,6 +9,8 @@
 //     components.py:275-280, with the [B,N,D] token layout written directly).
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "gemm.h"
 
 using namespace hvit;
@@ -59,7 +61,10 @@ int check_epi(const hvit_epilogue_t* e) {
 // >= 4 K-stages)
 int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64) {
   long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
-  const long target = bm * bn <= 64 * 64 ? 512 : 256;  // small tiles: two per CU
+  // small tiles: two per CU.  HVIT_WG_TARGET overrides the 128x128 target
+  // (A/B measurements only)
+  static const long big = getenv("HVIT_WG_TARGET") ? atol(getenv("HVIT_WG_TARGET")) : 256;
+  const long target = bm * bn <= 64 * 64 ? 512 : big;
   long want = (target + tiles - 1) / tiles;
   long maxs = K / (4 * bk);
   if (want > maxs) want = maxs;

@@ -193,6 +193,36 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
 // partial[blk][co][tap] = sum over the block's pixels of dz[p][co] * x[p + tap]
 // (pixel chunks sized for >= 4 workgroups per CU at the model's shapes)
 constexpr int WG_PIX = 2048;   // Cin = 1 wgrad (2M pixels at B=32)
+constexpr int C1_WG_PF = 4;    // dz prefetch depth (pixels per thread)
+
+// 8 consecutive elements kept raw in registers until used
+template <typename T>
+struct Raw8 {
+  u32x4 u;
+  __device__ __forceinline__ void load(const T* p) { u = *(const u32x4*)p; }
+  __device__ __forceinline__ void to_f(float* f) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(u[i] << 16);
+      f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+};
+template <>
+struct Raw8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *(const f32x4*)p;
+    b = *(const f32x4*)(p + 4);
+  }
+  __device__ __forceinline__ void to_f(float* f) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[i] = a[i];
+      f[4 + i] = b[i];
+    }
+  }
+};
 constexpr int WG_PIX_O1 = 256; // Cout = 1 wgrad (131k pixels at B=32)
 template <typename T>
 __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
@@ -211,22 +241,32 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, 
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
-  // dz for the next pixel is loaded before the current one is accumulated
+  // dz loads run C1_WG_PF pixels ahead of the accumulation (a ring of raw
+  // 16/32-byte registers): one load in flight per thread left the loop
+  // latency-bound at this occupancy
   PixCursor pc(pbeg + pl, H, W);
   int p = pbeg + pl;
-  float dn[8];
-  if (p < pend) Vec8<T>::load(dz + (size_t)p * Cout + cc * 8, dn);
-  for (; p < pend; p += lanes, pc.advance(lanes, H, W)) {
-    float d[8];
+  Raw8<T> q[C1_WG_PF];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) d[e] = dn[e];
-    if (p + lanes < pend) Vec8<T>::load(dz + (size_t)(p + lanes) * Cout + cc * 8, dn);
-    float xv[9];
-    taps9(xs + (p - base), pc.y, pc.x, H, W, xv);
+  for (int k = 0; k < C1_WG_PF; ++k)
+    if (p + k * lanes < pend) q[k].load(dz + (size_t)(p + k * lanes) * Cout + cc * 8);
+  while (p < pend) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int k = 0; k < C1_WG_PF; ++k) {
+      if (p >= pend) break;
+      float d[8];
+      q[k].to_f(d);
+      const int pn = p + C1_WG_PF * lanes;
+      if (pn < pend) q[k].load(dz + (size_t)pn * Cout + cc * 8);
+      float xv[9];
+      taps9(xs + (p - base), pc.y, pc.x, H, W, xv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[t][e] += d[e] * xv[t];
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[t][e] += d[e] * xv[t];
+      p += lanes;
+      pc.advance(lanes, H, W);
+    }
   }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll

@@ -1,0 +1,83 @@
+"""CPU: the host side of the enhancement path (BASELINE
+config 1): STFT -> magnitude normalisation -> model -> iSTFT with the noisy
+phase (inference/enhancer.py:57-135), WAV I/O, checkpoint loading
+(enhancer.py:258-290).  The model is a stand-in here (identity), so no GPU
+work runs; tests/test_gpu_enhancer.py runs the HybridViT itself."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+
+class Identity(nn.Module):
+    def forward(self, x):
+        return x
+
+
+def test_identity_model_reconstructs_audio(hv):
+    from hvit_amd import enhancer as E
+
+    clip = E.synthetic_clip(0.5, seed=3)
+    enh = E.AudioEnhancer(Identity(), device="cpu")
+    out = enh.enhance(clip)
+    assert out.shape == clip.shape and out.dtype == np.float32
+    assert np.abs(out - clip).max() < 1e-5 * np.abs(clip).max()
+    out2 = enh.enhance(clip, normalize=False)
+    assert np.abs(out2 - clip).max() < 1e-5 * np.abs(clip).max()
+
+
+def test_spectrogram_shape_matches_reference_settings(hv):
+    from hvit_amd import enhancer as E
+
+    enh = E.AudioEnhancer(Identity(), device="cpu")
+    spec = enh.stft(np.zeros(32000, dtype=np.float32))
+    assert tuple(spec.shape) == (257, 251)  # 2 s at 16 kHz: the config-1 clip [1, 1, 257, 251]
+
+
+def test_silence_is_passed_through(hv):
+    from hvit_amd import enhancer as E
+
+    out = E.AudioEnhancer(Identity(), device="cpu").enhance(np.zeros(4000, dtype=np.float32))
+    assert np.all(out == 0)
+
+
+def test_wav_round_trip(hv, tmp_path):
+    from hvit_amd import enhancer as E
+
+    clip = E.synthetic_clip(0.25, seed=1)
+    p = tmp_path / "a.wav"
+    E.write_wav(p, clip, 16000)
+    assert np.array_equal(E.read_wav(p, 16000), clip)
+    with pytest.raises(ValueError):
+        E.read_wav(p, 8000)
+
+
+def test_enhance_file_and_directory(hv, tmp_path):
+    from hvit_amd import enhancer as E
+
+    d_in, d_out = tmp_path / "in", tmp_path / "out"
+    d_in.mkdir()
+    for i in range(2):
+        E.write_wav(d_in / f"n{i}.wav", E.synthetic_clip(0.2, seed=i), 16000)
+    E.AudioEnhancer(Identity(), device="cpu").enhance_directory(d_in, d_out)
+    for i in range(2):
+        a = E.read_wav(d_out / f"n{i}.wav", 16000)
+        b = E.read_wav(d_in / f"n{i}.wav", 16000)
+        assert np.abs(a - b).max() < 1e-5
+
+
+def test_load_model_for_inference_trainer_checkpoint(hv, tmp_path):
+    from hvit_amd import enhancer as E
+
+    kw = dict(encoder_channels=[8, 16, 32], embed_dim=64, num_heads=4, num_layers=2, decoder_channels=[32, 16, 8, 1])
+    torch.manual_seed(0)
+    src = hv.HybridViT(**kw)
+    ck = tmp_path / "best_model.pth"
+    torch.save({"epoch": 3, "model_state_dict": src.state_dict(), "best_val_loss": 0.5}, ck)  # trainer.py:350-380
+    dst = E.load_model_for_inference(ck, hv.HybridViT(**kw), device="cpu")
+    assert not dst.training
+    for (k, a), b in zip(src.state_dict().items(), dst.state_dict().values()):
+        assert torch.equal(a, b), k
+    torch.save(src.state_dict(), tmp_path / "bare.pth")
+    E.load_model_for_inference(tmp_path / "bare.pth", hv.HybridViT(**kw), device="cpu")
