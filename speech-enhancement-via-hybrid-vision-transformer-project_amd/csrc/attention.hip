@@ -16,6 +16,8 @@
 // Backward (FlashAttention-2 style recompute from lse): a dQ kernel over query
 // tiles and a dK/dV kernel over key tiles, both recomputing P; delta =
 // rowsum(dO * O) is produced by a small pre-pass.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace hvit {
@@ -502,10 +504,11 @@ __device__ __forceinline__ void v2_stage(char* dst, const bf16_t* src, long pitc
 // source address (lane L fetches logical chunk (L%8) ^ row&7 of row 8p + L/8).
 // Rows >= n re-read row n-1 (finite data; every use of those rows is masked or
 // multiplied by an exact zero).  `rows` is a multiple of 8.
+template <int WAVES>
 __device__ __forceinline__ void v2_stage_glds(char* dst, const bf16_t* src, long pitch, int n, int rows) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rl = lane >> 3, cp = lane & 7;
-  for (int pc = w; pc < (rows >> 3); pc += AT_THREADS / 64) {
+  for (int pc = w; pc < (rows >> 3); pc += WAVES) {
     const int row = pc * 8 + rl;
     const int srow = row < n ? row : n - 1;
     const bf16_t* g = src + (long)srow * pitch + ((cp ^ rl) << 3);
@@ -571,8 +574,11 @@ __device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uin
   return k;
 }
 
-// forward: workgroup = (b, h, 64 queries); wave = 16 queries x all keys
-__global__ __launch_bounds__(AT_THREADS) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+// forward: workgroup = (b, h, 16*WAVES queries); wave = 16 queries x all keys.
+// WAVES = 16 covers all N <= 256 queries of a (b, h) in one workgroup, so K
+// and V are staged into LDS once per (b, h) instead of once per 64 queries.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int N, int H, float scale,
                                                          uint32_t thr, float dscale, unsigned long long seed,
                                                          uint32_t site) {
@@ -588,13 +594,13 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_fwd_v2(const bf16_t* __restri
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
   const int NK = (N + 15) & ~15;
   const int nkt = NK >> 4;
-  const int q = blockIdx.x * AT_TILE + w * 16 + frow;  // this lane's query
+  const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;  // this lane's query
   u32x4 qf[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
     qf[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
-  v2_stage_glds(Ks, base + D, pitch, N, NK);
-  v2_stage_glds(Vs, base + 2 * D, pitch, N, NK);
+  v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK);
+  v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK);
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
   // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q), log2 units
@@ -661,8 +667,9 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_fwd_v2(const bf16_t* __restri
 }
 
 // dQ (+ delta = rowsum(dO * O), written for the dK/dV kernel):
-// workgroup = (b, h, 64 queries); K, V images in LDS
-__global__ __launch_bounds__(AT_THREADS) void mhsa_dq_v2(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+// workgroup = (b, h, 16*WAVES queries); K, V images in LDS
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                         const bf16_t* __restrict__ dout,
                                                         const float* __restrict__ lse, float* __restrict__ delta,
                                                         bf16_t* __restrict__ dqkv, int N, int H, float scale,
@@ -680,7 +687,7 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dq_v2(const bf16_t* __restric
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
   const int NK = (N + 15) & ~15;
   const int nkt = NK >> 4;
-  const int q = blockIdx.x * AT_TILE + w * 16 + frow;
+  const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;
   const bool qv = q < N;
   const uint64_t bh = (uint64_t)b * H + h;
   u32x4 qf[2], df[2];
@@ -702,8 +709,8 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dq_v2(const bf16_t* __restric
   dl += __shfl_xor(dl, 32, 64);
   if (qv && fq == 0) delta[bh * N + q] = dl;
   const float lse2 = qv ? lse[bh * N + q] * 1.4426950408889634f : 0.f;
-  v2_stage_glds(Ks, base + D, pitch, N, NK);
-  v2_stage_glds(Vs, base + 2 * D, pitch, N, NK);
+  v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK);
+  v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK);
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
   f32x4 dq[4];
@@ -741,9 +748,10 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dq_v2(const bf16_t* __restric
   }
 }
 
-// dK, dV: workgroup = (b, h, 64 keys); wave = 16 keys x all queries;
+// dK, dV: workgroup = (b, h, 16*WAVES keys); wave = 16 keys x all queries;
 // Q, dO images + lse, delta of all queries in LDS
-__global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_v2(const bf16_t* __restrict__ qkv,
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restrict__ qkv,
                                                          const bf16_t* __restrict__ dout,
                                                          const float* __restrict__ lse,
                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -763,7 +771,7 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_v2(const bf16_t* __restri
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
   const int NQ = (N + 15) & ~15;
   const int nqt = NQ >> 4;
-  const int key = blockIdx.x * AT_TILE + w * 16 + frow;  // this lane's key (B operand column)
+  const int key = blockIdx.x * WAVES * 16 + w * 16 + frow;  // this lane's key (B operand column)
   const bool kv = key < N;
   const uint64_t bh = (uint64_t)b * H + h;
   u32x4 kf[2], vf[2];
@@ -772,9 +780,9 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_v2(const bf16_t* __restri
     kf[s2] = kv ? *(const u32x4*)(base + D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
     vf[s2] = kv ? *(const u32x4*)(base + 2 * D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
   }
-  v2_stage_glds(Qs, base, pitch, N, NQ);
-  v2_stage_glds(Ds, dout + (long)b * N * D + h * 64, D, N, NQ);
-  for (int i = threadIdx.x; i < NQ; i += AT_THREADS) {
+  v2_stage_glds<WAVES>(Qs, base, pitch, N, NQ);
+  v2_stage_glds<WAVES>(Ds, dout + (long)b * N * D + h * 64, D, N, NQ);
+  for (int i = threadIdx.x; i < NQ; i += WAVES * 64) {
     Ls[i] = i < N ? lse[bh * N + i] * 1.4426950408889634f : 0.f;
     Dl[i] = i < N ? delta[bh * N + i] : 0.f;
   }
@@ -843,6 +851,11 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_v2(const bf16_t* __restri
 }
 
 static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 && N <= V2_KMAX && N % 4 == 0; }
+// waves per v2 workgroup (HVIT_ATTN_WAVES = 4 / 8 / 16 overrides; A/B only)
+static int v2_waves() {
+  static const int w = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
+  return w;
+}
 
 // ------------------------------------------------------------------- host ---
 template <typename T, int HD>
@@ -913,8 +926,14 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
     const hvit_dropout_t* dr = dropout;
     const uint32_t thr = dr ? drop_threshold(dr->p) : 0;
     const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-    hipLaunchKernelGGL(mhsa_fwd_v2, dim3(cdiv(N, AT_TILE), H, B), dim3(AT_THREADS), 0, st, (const bf16_t*)qkv,
-                       (bf16_t*)o, lse, N, H, scale, thr, ds, dr ? dr->seed : 0ull, dr ? dr->site : 0u);
+    const int wv = v2_waves();
+    auto go = [&](auto kern, int waves) {
+      hipLaunchKernelGGL(kern, dim3(cdiv(N, 16 * waves), H, B), dim3(64 * waves), 0, st, (const bf16_t*)qkv,
+                         (bf16_t*)o, lse, N, H, scale, thr, ds, dr ? dr->seed : 0ull, dr ? dr->site : 0u);
+    };
+    if (wv == 16) go(mhsa_fwd_v2<16>, 16);
+    else if (wv == 8) go(mhsa_fwd_v2<8>, 8);
+    else go(mhsa_fwd_v2<4>, 4);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
@@ -937,12 +956,17 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
     const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
     const unsigned long long seed = dr ? dr->seed : 0ull;
     const uint32_t site = dr ? dr->site : 0u;
-    dim3 g(cdiv(N, AT_TILE), H, B);
-    hipLaunchKernelGGL(mhsa_dq_v2, g, dim3(AT_THREADS), 0, st, (const bf16_t*)qkv, (const bf16_t*)o,
-                       (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
-    HVIT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(mhsa_dkv_v2, g, dim3(AT_THREADS), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                       (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+    auto go = [&](auto dqk, auto dkvk, int waves) {
+      dim3 g(cdiv(N, 16 * waves), H, B);
+      hipLaunchKernelGGL(dqk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout,
+                         lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+      hipLaunchKernelGGL(dkvk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
+                         (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+    };
+    const int wv = v2_waves();
+    if (wv == 16) go(mhsa_dq_v2<16>, mhsa_dkv_v2<16>, 16);
+    else if (wv == 8) go(mhsa_dq_v2<8>, mhsa_dkv_v2<8>, 8);
+    else go(mhsa_dq_v2<4>, mhsa_dkv_v2<4>, 4);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
