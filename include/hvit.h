@@ -187,8 +187,12 @@ typedef struct {
   int cout, cin, ks;
 } hvit_wprep_item_t;
 int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void* stream);
+long long hvit_dropout_colsum_ws_elems(int N);
 int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, const hvit_dropout_t* dropout,
-                       const float* rowscale, int rows_per_sample, void* out, int out_dt, void* stream);
+                       const float* rowscale, int rows_per_sample, void* out, int out_dt, float* colsum, float* ws,
+                       long long ws_elems, void* stream);  /* colsum (nullable, f32 [N]) += column sums of out
+                       (the bias gradient of the GEMM that consumes out); ws: hvit_dropout_colsum_ws_elems(N)
+                       floats of per-workgroup partials (NULL: a slower two-pass fallback) */
 int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long long n, void* dz, int dz_dt, void* stream);
 int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate, float* out,
                      void* stream);                                     /* out[n] (+)= sum_m x[m*ld+n] */

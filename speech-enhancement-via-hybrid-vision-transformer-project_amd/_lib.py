@@ -99,7 +99,8 @@ _SIGS = {
     "hvit_bilinear_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "hvit_upsample_split_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp], i32),
     "hvit_cast": ([vp, i32, vp, i32, i64, vp], i32),
-    "hvit_dropout_scale": ([vp, i32, i64, i32, P(Dropout), vp, i32, vp, i32, vp], i32),
+    "hvit_dropout_scale": ([vp, i32, i64, i32, P(Dropout), vp, i32, vp, i32, vp, vp, i64, vp], i32),
+    "hvit_dropout_colsum_ws_elems": ([i32], i64),
     "hvit_tanh_bwd": ([vp, i32, vp, i64, vp, i32, vp], i32),
     "hvit_reduce_rows": ([vp, i32, i64, i64, i64, i32, vp, vp], i32),
     "hvit_sum_slabs": ([vp, i32, i64, vp, vp], i32),

@@ -100,6 +100,74 @@ __global__ void dropout_scale4_kernel(const void* g, int gdt, void* out, int odt
   }
 }
 
+// dropout_scale4 + column sums of the output (the bias gradient of the GEMM
+// that consumes it): a thread's 4 columns never change (grid stride is a
+// multiple of N/4, host-checked: (N/4) divides 256), so the sums stay in
+// registers; threads of a block sharing columns fold through LDS and the
+// block writes its N partial sums to part[block][N] (no same-address atomics:
+// with a few hundred workgroups those serialised the pass 3x), which one
+// column reduction adds into the caller's colsum.
+constexpr int DSC_THREADS = 256, DSC_BLOCKS = 1024;
+__global__ __launch_bounds__(DSC_THREADS) void dropout_scale4_colsum_kernel(const void* g, int gdt, void* out, int odt, int M,
+                                                                    int N, uint32_t thr, float ds,
+                                                                    unsigned long long seed, uint32_t site,
+                                                                    const float* rowscale, int rps,
+                                                                    float* __restrict__ part) {
+  __shared__ f32x4 red[DSC_THREADS];
+  const int total4 = M * (N / 4);
+  const int stride = gridDim.x * blockDim.x;
+  f32x4 cs = {0.f, 0.f, 0.f, 0.f};
+  // DS_UNROLL independent 16-byte loads in flight per thread (few, long-lived
+  // workgroups keep the atomics per column low)
+  constexpr int DS_UNROLL = 8;
+  for (int base = blockIdx.x * blockDim.x + threadIdx.x; base < total4; base += DS_UNROLL * stride) {
+    f32x4 v[DS_UNROLL];
+#pragma unroll
+    for (int k = 0; k < DS_UNROLL; ++k) {
+      const int i = (base + k * stride) * 4;
+      v[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (base + k * stride < total4) {
+        if (gdt == HVIT_F32) {
+          v[k] = *(const f32x4*)((const float*)g + i);
+        } else {
+          uint2 u = *(const uint2*)((const bf16_t*)g + i);
+          v[k] = (f32x4){__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                         __uint_as_float(u.y & 0xffff0000u)};
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DS_UNROLL; ++k) {
+      if (base + k * stride >= total4) break;
+      const int i = (base + k * stride) * 4;
+      if (thr) {
+        const uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ (((uint64_t)i >> 2) * 0xD6E8FEB86659FD93ull));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= thr) ? v[k][e] * ds : 0.f;
+      }
+      if (rowscale) v[k] *= rowscale[(i / N) / rps];
+      cs += v[k];
+      if (odt == HVIT_F32) {
+        *(f32x4*)((float*)out + i) = v[k];
+      } else {
+        uint2 u;
+        u.x = f2bf2(v[k][0], v[k][1]);
+        u.y = f2bf2(v[k][2], v[k][3]);
+        *(uint2*)((bf16_t*)out + i) = u;
+      }
+    }
+  }
+  red[threadIdx.x] = cs;
+  __syncthreads();
+  const int n4 = N / 4;
+  if ((int)threadIdx.x < n4) {
+    f32x4 t = red[threadIdx.x];
+    for (int k = threadIdx.x + n4; k < DSC_THREADS; k += n4) t += red[k];
+    const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % n4) * 4;
+    *(f32x4*)(part + (long)blockIdx.x * N + c) = t;  // every block writes all N partials
+  }
+}
+
 __global__ void tanh_bwd_kernel(const void* dy, int dydt, const float* y, void* dz, int dzdt, long n) {
   GRID_STRIDE(i, n) {
     float t = y[i];
@@ -287,15 +355,33 @@ extern "C" int hvit_conv_weight_unpack(const float* dw_packed, int Cout, int Cin
   return HVIT_OK;
 }
 
+extern "C" long long hvit_dropout_colsum_ws_elems(int N) { return (long long)DSC_BLOCKS * (N > 0 ? N : 0); }
+
 extern "C" int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, const hvit_dropout_t* dropout,
-                                  const float* rowscale, int rows_per_sample, void* out, int out_dt,
-                                  void* stream) {
+                                  const float* rowscale, int rows_per_sample, void* out, int out_dt, float* colsum,
+                                  float* ws, long long ws_elems, void* stream) {
   HVIT_CHECK(g && out, "hvit_dropout_scale: null pointer");
   HVIT_CHECK(!rowscale || rows_per_sample > 0, "hvit_dropout_scale: rows_per_sample");
   uint32_t thr = dropout ? drop_threshold(dropout->p) : 0;
   float ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
   long total = (long)M * N;
   if (total <= 0) return HVIT_OK;
+  if (colsum) {
+    if (N % 4 == 0 && N / 4 <= 256 && 256 % (N / 4) == 0 && total < (1L << 31) && aligned16(g) && aligned16(out) &&
+        ws && aligned16(ws) && ws_elems >= hvit_dropout_colsum_ws_elems(N)) {
+      hipLaunchKernelGGL(dropout_scale4_colsum_kernel, dim3(DSC_BLOCKS), dim3(DSC_THREADS), 0,
+                         (hipStream_t)stream, g, g_dt, out, out_dt, (int)M, N, thr, ds,
+                         dropout ? dropout->seed : 0ull, dropout ? dropout->site : 0u, rowscale, rows_per_sample,
+                         ws);
+      HVIT_LAUNCH_CHECK();
+      return hvit_reduce_rows(ws, HVIT_F32, DSC_BLOCKS, N, N, 1, colsum, stream);
+    }
+    // other widths / no workspace: the plain pass, then a column reduction of its output
+    if (int rc = hvit_dropout_scale(g, g_dt, M, N, dropout, rowscale, rows_per_sample, out, out_dt, nullptr, nullptr,
+                                    0, stream))
+      return rc;
+    return hvit_reduce_rows(out, out_dt, M, N, N, 1, colsum, stream);
+  }
   if (N % 4 == 0 && total < (1L << 31) && aligned16(g) && aligned16(out)) {
     hipLaunchKernelGGL(dropout_scale4_kernel, dim3(grid_for(total, 4)), dim3(256), 0, (hipStream_t)stream, g,
                        g_dt, out, out_dt, (int)M, N, thr, ds, dropout ? dropout->seed : 0ull,

@@ -54,7 +54,9 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
     if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return HVIT_OK;
   }
-  const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK;
+  // HVIT_NO_RS=1: bias grad by a separate column reduction (A/B measurements only)
+  static const bool no_rs = getenv("HVIT_NO_RS") && atoi(getenv("HVIT_NO_RS"));
+  const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK && !no_rs;
   Epi ep;
   ep.out_dt = HVIT_F32;
   ep.ldo = K;

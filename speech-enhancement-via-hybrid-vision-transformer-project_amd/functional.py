@@ -196,6 +196,17 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False):
     return (dw, db) if bias else dw
 
 
+def dropout_scale(g, M, N, drop, rowscale, rps, out, colsum=None):
+    """out = rowscale * dropout(g) in out's dtype; colsum (f32 [N], zeroed)
+    += column sums of it (per-workgroup partials in a scratch slab)."""
+    ws, ws_n = None, 0
+    if colsum is not None:
+        ws_n = L.lib().hvit_dropout_colsum_ws_elems(N)
+        ws = torch.empty(ws_n, dtype=torch.float32, device=g.device)
+    call("hvit_dropout_scale", g.data_ptr(), L.dt_of(g), M, N, drop, ptr(rowscale), rps, out.data_ptr(),
+         L.dt_of(out), ptr(colsum), ptr(ws), ws_n, stream_ptr())
+
+
 def epilogue(act=L.ACT_NONE, out2=None, aux=None, drop=None, resid=None, rowscale=None, rps=1, rowadd=None,
              rowadd_rows=1, colsum=None):
     e = L.Epilogue()
@@ -367,9 +378,8 @@ class PatchEmbedFn(torch.autograd.Function):
         dx0 = dx0.contiguous()
         M = N * Nt
         gd = _empty((M, D), dt, dev)
-        call("hvit_dropout_scale", dx0.data_ptr(), L.dt_of(dx0), M, D, dr, None, 1, gd.data_ptr(), dt, s)
-        db = ctx.zs.take(dev)
-        call("hvit_reduce_rows", gd.data_ptr(), dt, M, D, D, 1, db.data_ptr(), s)
+        db = ctx.zs.take(dev)  # patch-embed bias grad: column sums fused into the dropout pass
+        dropout_scale(dx0, M, D, dr, None, 1, gd, db)
         dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
         call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
         g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
@@ -459,7 +469,9 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.save_for_backward(n1w, n2w)
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
-        ctx.zs = (_zs(ctx, 2 * D), _zs(ctx, 2 * D), _zs(ctx, hid))  # LN1, LN2 (dgamma|dbeta), fc1 bias grad
+        # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
+        # the GELU-backward epilogue and the two dropout passes)
+        ctx.zs = (_zs(ctx, 2 * D), _zs(ctx, 2 * D), _zs(ctx, hid), _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
         if want_probs:
             ctx.mark_non_differentiable(probs)
         return x2.view(B, Nt, D), probs
@@ -476,11 +488,12 @@ class ViTBlockFn(torch.autograd.Function):
         if dx2.dtype != torch.float32:
             dx2 = dx2.float()
         # MLP branch
+        zln1, zln2, zf1b, zf2b, zpb, zqb = ctx.zs
         g2 = _empty((M, D), dt, dev)
-        call("hvit_dropout_scale", dx2.data_ptr(), F32, M, D, drf2, ptr(rs2), Nt, g2.data_ptr(), dt, s)
-        df2w, df2b = linear_wgrad(dt, g2, a, M, D, hid, bias=True)
+        df2b = zf2b.take(dev)
+        dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
+        df2w = linear_wgrad(dt, g2, a, M, D, hid)
         dh = _empty((M, hid), dt, dev)
-        zln1, zln2, zf1b = ctx.zs
         df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
         call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
              epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1, colsum=df1b), s)
@@ -490,15 +503,20 @@ class ViTBlockFn(torch.autograd.Function):
         dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2, zln2)
         # attention branch
         g1 = _empty((M, D), dt, dev)
-        call("hvit_dropout_scale", dx1.data_ptr(), F32, M, D, drp, ptr(rs1), Nt, g1.data_ptr(), dt, s)
-        dpw, dpb = linear_wgrad(dt, g1, o, M, D, D, bias=True)
+        dpb = zpb.take(dev)
+        dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
+        dpw = linear_wgrad(dt, g1, o, M, D, D)
         do = _empty((M, D), dt, dev)
         call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H, D // H,
              scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
-        dqkvw, dqkvb = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, bias=True)
+        # qkv bias grad by a column reduction: the wgrad GEMM variant with fused
+        # A-row sums spills at 128x128 (rocprof: 42 -> 28 us class without it)
+        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D)
+        dqkvb = zqb.take(dev)
+        call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None, s)
         dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)

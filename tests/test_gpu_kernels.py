@@ -87,6 +87,27 @@ def test_linear_fwd_epilogues(hv, dt):
     assert rel(y, exp) < tol(dt)
 
 
+@pytest.mark.parametrize("N", [512, 96])  # 96: N/4 does not divide 256 -> plain pass + column reduction
+@pytest.mark.parametrize("odt", ["f32", "bf16"])
+def test_dropout_scale_colsum(hv, N, odt):
+    l = L(hv)
+    M, Nt = 1000, 250
+    g = torch.randn(M, N, device=DEV)
+    rs = torch.rand(M // Nt, device=DEV) + 0.5
+    out = torch.empty(M, N, device=DEV, dtype=tdt(odt))
+    cs = torch.zeros(N, device=DEV)
+    dr = l.dropout(0.2, 11, 5)
+    ws_n = l.lib().hvit_dropout_colsum_ws_elems(N)
+    ws = torch.empty(ws_n, device=DEV)
+    l.call("hvit_dropout_scale", g.data_ptr(), l.F32, M, N, dr, rs.data_ptr(), Nt, out.data_ptr(), l.dt_of(out),
+           cs.data_ptr(), ws.data_ptr(), ws_n, s())
+    mask = torch.as_tensor(keep_mask(11, 5, M * N, 0.2).reshape(M, N), device=DEV)
+    ref = g * mask / 0.8 * rs.repeat_interleave(Nt)[:, None]
+    assert rel(out.float(), ref) < tol(odt)
+    # fused path (N = 512) sums the f32 values; the N = 96 fallback reduces the stored output
+    assert rel(cs, ref.sum(0)) < (1e-4 if N == 512 or odt == "f32" else 1e-2)
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("M", [300, 512])  # 512: full tiles -> the compile-time GELU_BWD epilogue (h prefetch)
 def test_linear_dgrad_gelu_bwd(hv, dt, M):
