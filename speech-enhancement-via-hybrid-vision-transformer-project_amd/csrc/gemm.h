@@ -337,7 +337,7 @@ enum EpiAct { ACT_NONE = 0, ACT_GELU_DUAL = 1, ACT_TANH = 2, ACT_GELU_BWD = 3 };
 // column sums) and for split-K slabs; everything else takes the generic one
 // and for the three fused ViT epilogues (fc1 GELU, residual adds, GELU
 // backward), which are only chosen when every tile is full and vector-aligned
-enum EpiKind { EK_GEN = 0, EK_STORE = 1, EK_SLAB = 2, EK_GELU_DUAL = 3, EK_RESID = 4, EK_GELU_BWD = 5 };
+enum EpiKind { EK_GEN = 0, EK_STORE = 1, EK_SLAB = 2, EK_GELU_DUAL = 3, EK_RESID = 4, EK_GELU_BWD = 5, EK_PATCH = 6 };
 
 struct Epi {
   int mode = EPI_STORE;
@@ -995,6 +995,24 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
 #pragma unroll
           for (int e = 0; e < 4; ++e) csum[e] += v[e];
         }
+      } else if constexpr (EK == EK_PATCH) {
+        // col2im scatter of the patch-embedding dgrad: m = token (b, py, px),
+        // n = (ky*P + kx)*C + c.  The host guarantees C % 4 == 0 (a thread's
+        // 4 columns share one tap), so the column part of the NHWC offset is
+        // per-thread constant and each row is one vector store
+        const int tap = n / ep.pC, cch = n - tap * ep.pC;
+        const int ky = tap / ep.pP, kx = tap - ky * ep.pP;
+        const long colpart = ((long)ky * ep.pW + kx) * ep.pC + cch;
+        const int hw = ep.pHp * ep.pWp;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = r0 + i * RSTEP;
+          const int m = mbase + row;
+          const int b = m / hw, rem = m - b * hw;
+          const int py = rem / ep.pWp, px = rem - py * ep.pWp;
+          const long o = (((long)b * ep.pH + py * ep.pP) * ep.pW + px * ep.pP) * ep.pC + colpart;
+          store4v<true>(ep.out, o, *(const f32x4*)(Cs + row * CP + c4 * 4), 4, ep.out_dt);
+        }
       } else {
         EpiIn in[NR];
 #pragma unroll
@@ -1134,6 +1152,11 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
     const bool full_tiles = ep.vec_ok && M % bm == 0 && N % bn == 0 && ep.mode == EPI_STORE && !ep.rowadd &&
                             !ep.stats;
     const bool drop_ok = ep.drop_thr ? N % 4 == 0 : ep.drop_scale == 1.f;
+    // lean col2im scatter for the patch-embedding dgrad (no bias / act / dropout)
+    const bool patch_lean = ep.mode == EPI_PATCH && ep.pC % 4 == 0 && M % bm == 0 && N % bn == 0 && !ep.bias &&
+                            ep.act == ACT_NONE && !ep.drop_thr && ep.drop_scale == 1.f && !ep.resid && !ep.rowadd &&
+                            !ep.stats && !ep.colsum && ((uintptr_t)ep.out & 15) == 0;
+    if (IsDenseKC<LA>::value && ek == EK_GEN && patch_lean) ek = EK_PATCH;
     if (IsDenseKC<LA>::value && ek == EK_GEN && full_tiles && drop_ok) {
       if (ep.act == ACT_GELU_DUAL && !ep.resid) ek = EK_GELU_DUAL;
       else if (ep.act == ACT_NONE && ep.resid && ep.resid != ep.out) ek = EK_RESID;
@@ -1182,6 +1205,9 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
       break;
     case EK_GELU_BWD:
       if constexpr (IsDenseKC<LA>::value) go(std::integral_constant<int, EK_GELU_BWD>());
+      break;
+    case EK_PATCH:
+      if constexpr (IsDenseKC<LA>::value) go(std::integral_constant<int, EK_PATCH>());
       break;
     default: go(std::integral_constant<int, EK_GEN>()); break;
   }
