@@ -317,6 +317,8 @@ extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, con
 #undef LNB
   HVIT_LAUNCH_CHECK();
   if (slab) {
+    if (dbeta == dgamma + D)  // [dgamma | dbeta] contiguous: one column reduction of the [nblk][2D] slab
+      return hvit_reduce_rows(ws, HVIT_F32, nblk, 2 * D, 2 * D, (flags & HVIT_ACC_ZEROED) ? 1 : 0, dgamma, stream);
     hipLaunchKernelGGL(ln_slab_sum_kernel, dim3(cdiv(2 * D, 64)), dim3(256), 0, st, ws, nblk, D, dgamma, dbeta);
     HVIT_LAUNCH_CHECK();
   }

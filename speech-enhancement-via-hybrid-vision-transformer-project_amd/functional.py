@@ -401,15 +401,21 @@ def _ln(x2d, gw, gb, dt):
     return y, mean, rstd
 
 
+_LN_SLAB = bool(int(__import__("os").environ.get("HVIT_LN_SLAB", "1")))
+
+
 def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):
     """zs: a zslot(2 * D) registered in the forward (dgamma | dbeta)."""
     M, D = x.shape
     dx = torch.empty((M, D), dtype=torch.float32, device=x.device)
     acc = zs.take(x.device)
     dgw, dgb = acc[:D], acc[D:2 * D]
-    # atomic dgamma/dbeta partials (measured faster than the slab + reduce form at B*N = 8192)
+    ws, ws_n = None, 0
+    if _LN_SLAB:  # per-workgroup dgamma/dbeta slab + one column reduction (no same-address atomics)
+        ws_n = L.lib().hvit_layernorm_bwd_ws_elems(M, D)
+        ws = torch.empty(ws_n, dtype=torch.float32, device=x.device)
     call("hvit_layernorm_bwd", dy.data_ptr(), L.dt_of(dy), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-         gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), None, 0, L.ACC_ZEROED,
+         gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), ptr(ws), ws_n, L.ACC_ZEROED,
          stream_ptr())
     return dx, dgw, dgb
 

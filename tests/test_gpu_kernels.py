@@ -387,6 +387,14 @@ def test_layernorm(hv, dt, M, D):
            l.ACC_ZEROED, s())
     assert rel(acc[:D], g.grad) < 1e-4
     assert rel(acc[D:], b.grad) < 1e-4
+    # slab path with contiguous [dgamma | dbeta]: one column reduction of the slab
+    acc.zero_()
+    l.call("hvit_layernorm_bwd", dy.data_ptr(), l.F32, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+           g.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), acc.data_ptr(), acc[D:].data_ptr(), ws.data_ptr(),
+           ws_n, l.ACC_ZEROED, s())
+    assert rel(dx - resid, x.grad) < 1e-4
+    assert rel(acc[:D], g.grad) < 1e-4
+    assert rel(acc[D:], b.grad) < 1e-4
 
 
 # ------------------------------------------------------------- batchnorm ---
