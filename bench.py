@@ -138,8 +138,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU over RCCL; HVIT_DIST_BACKEND=gloo (with ranks sharing the
+        # visible GPUs round-robin) only rehearses the DP path on a one-GPU box
+        backend = os.environ.get("HVIT_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     import hvit_amd_loader
 
     hv = hvit_amd_loader.load()
