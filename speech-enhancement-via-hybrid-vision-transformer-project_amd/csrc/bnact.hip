@@ -252,6 +252,118 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
   }
 }
 
+// backward reduce pass (training): per-channel sums of the routed gradient g
+// and of g * xhat over full pooling windows.  Software-pipelined: the next
+// window's z taps and dy are loaded (raw) before the current one is reduced,
+// so every thread keeps two windows of loads in flight.
+template <typename T>
+__device__ __forceinline__ float raw_elem(const u32x4& u, int e) {
+  if constexpr (sizeof(T) == 2) return __uint_as_float((e & 1) ? (u[e >> 1] & 0xffff0000u) : (u[e >> 1] << 16));
+  else return __uint_as_float(u[e]);
+}
+
+template <typename T, typename TD>
+__global__ __launch_bounds__(256) void bnact_sums_kernel(const T* __restrict__ z, const TD* __restrict__ dy,
+                                                        BnArgs a, float* __restrict__ sums) {
+  constexpr int CV = V16<T>::N;
+  constexpr int MAXW = 4;  // pool <= 2
+  __shared__ float red[2][256][CV];
+  const int G = a.C / CV;
+  const int P = a.pool;
+  const int Ho = a.H / P, Wo = a.W / P;
+  const int total = a.N * Ho * Wo * G;  // full windows only
+  const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
+  float sc[CV], sh[CV], mu[CV], is[CV], acc1[CV], acc2[CV];
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    mu[e] = a.mean[c + e];
+    is[e] = a.invstd[c + e];
+    sc[e] = is[e] * a.gamma[c + e];
+    sh[e] = a.beta[c + e] - mu[e] * sc[e];
+    acc1[e] = acc2[e] = 0.f;
+  }
+  struct Item {
+    u32x4 zr[MAXW];
+    float d[CV];
+    int n;
+  };
+  auto load = [&](int i, Item& it) {
+    if (i >= total) return;
+    int t = i / G;
+    const int wx = t % Wo;
+    t /= Wo;
+    const int wy = t % Ho;
+    it.n = t / Ho;
+#pragma unroll
+    for (int q = 0; q < MAXW; ++q)
+      if (q < P * P)
+        it.zr[q] = *(const u32x4*)(z + ((size_t)(it.n * a.H + wy * P + (q >> 1)) * a.W + wx * P + (q & 1)) * a.C + c);
+    const TD* dp = dy + ((size_t)(it.n * Ho + wy) * Wo + wx) * a.C + c;
+    if constexpr (sizeof(TD) == sizeof(T)) {
+      V16<TD>::load(dp, it.d);
+    } else {
+#pragma unroll
+      for (int e = 0; e < CV; ++e) it.d[e] = Elem<TD>::to_f(dp[e]);
+    }
+  };
+  auto reduce = [&](const Item& it) {
+    float m[CV];
+    drop_mask<CV>(a, it.n, c, m);
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      float zs = raw_elem<T>(it.zr[0], e);
+      float best = fmaxf(zs * sc[e] + sh[e], 0.f);
+#pragma unroll
+      for (int q = 1; q < MAXW; ++q) {
+        if (q >= P * P) break;
+        const float zq = raw_elem<T>(it.zr[q], e);
+        const float v = fmaxf(zq * sc[e] + sh[e], 0.f);
+        if (v > best) {  // first maximum wins ties (torch's max-pool routing)
+          best = v;
+          zs = zq;
+        }
+      }
+      const float gv = best > 0.f ? it.d[e] * m[e] : 0.f;
+      acc1[e] += gv;
+      acc2[e] += gv * ((zs - mu[e]) * is[e]);
+    }
+  };
+  const int stride = gridDim.x * blockDim.x;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  Item cur;
+  load(i, cur);
+  for (; i < total; i += stride) {
+    Item nxt;
+    load(i + stride, nxt);
+    reduce(cur);
+    cur = nxt;
+  }
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    red[0][threadIdx.x][e] = acc1[e];
+    red[1][threadIdx.x][e] = acc2[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    float t1[CV], t2[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) t1[e] = t2[e] = 0.f;
+    for (int k = threadIdx.x; k < 256; k += G)
+#pragma unroll
+      for (int e = 0; e < CV; ++e) {
+        t1[e] += red[0][k][e];
+        t2[e] += red[1][k][e];
+      }
+    float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+    const int cc = threadIdx.x * CV;
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      atomicAdd(slot + cc + e, t1[e]);
+      atomicAdd(slot + a.C + cc + e, t2[e]);
+    }
+  }
+}
+
 // sums[0 .. 2C) = sum over the BN_SLOTS slot copies that follow it
 __global__ void bn_slots_reduce_kernel(float* sums, int n2) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -324,8 +436,10 @@ static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* su
   if (total <= 0) return HVIT_OK;
   dim3 g(grid_for(total, BN_GRID_SUMS)), ga(grid_for(total, BN_GRID_APPLY));
   if (training) {
-    hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, false>), g, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
-                       training, (T*)dz);
+    const long tsum = (long)a.N * (a.H / P) * (a.W / P) * (a.C / cv);
+    if (tsum > 0)
+      hipLaunchKernelGGL((bnact_sums_kernel<T, TD>), dim3(grid_for(tsum, BN_GRID_SUMS)), dim3(256), 0, st,
+                         (const T*)z, (const TD*)dy, a, sums);
     HVIT_LAUNCH_CHECK();
     hipLaunchKernelGGL(bn_slots_reduce_kernel, dim3(cdiv(2 * a.C, 256)), dim3(256), 0, st, sums, 2 * a.C);
     HVIT_LAUNCH_CHECK();
