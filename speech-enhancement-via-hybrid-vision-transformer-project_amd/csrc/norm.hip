@@ -50,10 +50,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     int c = lane * 4 + i * 256;
-    if (c < D)
+    if (c < D) {  // D % 4 == 0: one vector load of gamma / beta, one vector store
+      const f32x4 gv = *(const f32x4*)(g + c), bv = *(const f32x4*)(b + c);
+      f32x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        y[(long)row * D + c + e] = Elem<TY>::from_f((v[i][e] - mean) * rstd * g[c + e] + b[c + e]);
+      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * gv[e] + bv[e];
+      if constexpr (sizeof(TY) == 4) {
+        *(f32x4*)((float*)y + (long)row * D + c) = o;
+      } else {
+        uint2 u;
+        u.x = f2bf2(o[0], o[1]);
+        u.y = f2bf2(o[2], o[3]);
+        *(uint2*)((bf16_t*)y + (long)row * D + c) = u;
+      }
+    }
   }
   if (lane == 0) {
     mean_out[row] = mean;
@@ -270,7 +280,8 @@ extern "C" int hvit_layernorm_fwd(const float* x, const float* gamma, const floa
                                   float eps, void* y, int y_dt, float* mean, float* rstd, void* stream) {
   HVIT_CHECK(x && gamma && beta && y && mean && rstd, "hvit_layernorm_fwd: null pointer");
   HVIT_CHECK(D % 4 == 0 && D <= 1024 && D > 0, "hvit_layernorm_fwd: D=%d must be a multiple of 4, <= 1024", D);
-  HVIT_CHECK(aligned16(x), "hvit_layernorm_fwd: x must be 16-byte aligned");
+  HVIT_CHECK(aligned16(x) && aligned16(gamma) && aligned16(beta) && aligned16(y),
+             "hvit_layernorm_fwd: x, gamma, beta, y must be 16-byte aligned");
   if (M <= 0) return HVIT_OK;
   hipStream_t st = (hipStream_t)stream;
   dim3 g(cdiv(M, 4));
