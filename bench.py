@@ -11,11 +11,14 @@ one spectrogram = 256 frames.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Rank 0 prints one JSON line.  ``roofline`` times the dominant kernel (the
-bf16 MLP fc1 GEMM with its fused GELU/dropout epilogue, the largest MFMA
-launch of the step) with HIP events on the stream it runs on;
-``cpu_baseline`` times the CPU oracle (oracle/, fp32 PyTorch restatement of
-the reference) on a bounded sample of the same step, on this host's cores.
+Rank 0 prints one JSON line.  After the timed steps, an instrumented repeat
+of the same steps records HIP events around every launch of each op class
+(functional.timed) on the stream it runs on; ``op_table`` lists each class's
+GPU time per step and algorithmic FLOP/s (or bytes/s) against its roofline,
+and ``roofline`` is the class with the most GPU time (the ViT linear
+weight-gradient GEMMs at the default config).  ``cpu_baseline`` times the CPU
+oracle (oracle/, fp32 PyTorch restatement of the reference) on a bounded
+sample of the same step, on this host's cores.
 """
 
 import argparse
@@ -53,53 +56,93 @@ def parse():
     return ap.parse_args()
 
 
-def dominant_kernel_roofline(hv, batch):
-    """fc1 of one ViT block: [B*256, 512] x [512, 2048]^T + bias, GELU (dual
-    output) + dropout, bf16 MFMA.  2*M*N*K algorithmic FLOPs per launch."""
-    L = hv._lib
+PEAKS = {"mfma": (PEAK_BF16_TFLOPS, "TFLOP/s", 1e12), "hbm": (PEAK_HBM_GBS, "GB/s", 1e9)}
+# op class (functional.timed tag) -> roofline that bounds it
+OP_BOUND = {"vit_linear_wgrad": "mfma", "vit_linear_fwd": "mfma", "vit_linear_dgrad": "mfma", "linear_wgrad": "mfma",
+            "attn_fwd": "mfma", "attn_bwd": "mfma", "conv_fwd": "mfma", "conv_dgrad": "mfma", "conv_wgrad": "mfma",
+            "bn_act_fwd": "hbm", "bn_act_bwd": "hbm"}
+
+
+def op_table(times, steps):
+    """Per op class: launches and GPU ms per step, algorithmic work / time vs
+    its roofline (HIP event pairs recorded on the launch stream in-step)."""
+    rows = {}
+    for name, recs in times.items():
+        t = sum(e0.elapsed_time(e1) for e0, e1, _ in recs) / 1e3  # s
+        work = sum(w for _, _, w in recs)
+        bound = OP_BOUND.get(name, "mfma")
+        peak, unit, scale = PEAKS[bound]
+        ach = work / t / scale if t > 0 else 0.0
+        rows[name] = {"bound": bound, "ms_per_step": round(t / steps * 1e3, 4), "launches_per_step": len(recs) // steps,
+                      "avg_launch_us": round(t / len(recs) * 1e6, 2), "achieved": round(ach, 2), "peak": peak,
+                      "unit": unit, "frac": round(ach / peak, 4), "work_per_launch": work / len(recs)}
+    return dict(sorted(rows.items(), key=lambda kv: -kv[1]["ms_per_step"]))
+
+
+def roofline_of(table):
+    """The dominant op class (most GPU time per step) in the roofline format."""
+    name, r = next(iter(table.items()))
+    return {"kernel": name, "bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
+            "frac": r["frac"], "traffic": measured_traffic(name), "avg_launch_us": r["avg_launch_us"],
+            "launches_per_step": r["launches_per_step"],
+            ("flops_per_launch" if r["bound"] == "mfma" else "bytes_per_launch"): r["work_per_launch"],
+            "measured": "HIP events around each launch of this op class on its stream, inside an instrumented "
+                        "repeat of the timed steps"}
+
+
+def roofline_loop(hv, batch, reps=50):
+    """The dominant op class alone (ViT linear weight gradients of one block:
+    fc2, fc1, proj, qkv shapes, split-K bf16 GEMM + slab reduction), for
+    rocprofv3 --kernel-trace / --pmc passes (bench.py --roofline-only)."""
     HF = sys.modules["hvit_amd.functional"]
-    M, N, K = batch * 256, 2048, 512
-    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
-    b = torch.zeros(N, device="cuda")
-    h = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    a = torch.empty_like(h)
-    e = HF.epilogue(act=L.ACT_GELU_DUAL, out2=a, drop=L.dropout(0.1, 1, 1))
-    st = torch.cuda.current_stream()
-    args = (L.BF16, x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, h.data_ptr(), L.BF16, e, st.cuda_stream)
-    for _ in range(5):
-        L.call("hvit_linear_fwd", *args)
-    reps = 50
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
+    M, D, hid = batch * 256, 512, 2048
+    shapes = [(D, hid), (hid, D), (D, D), (3 * D, D)]  # (N, K): dw[N, K] = dy[M, N]^T x[M, K]
+    ops = [(torch.randn(M, n, device="cuda").to(torch.bfloat16), torch.randn(M, k, device="cuda").to(torch.bfloat16),
+            n, k) for n, k in shapes]
+    for _ in range(3):
+        for dy, x, n, k in ops:
+            HF.linear_wgrad(hv._lib.BF16, dy, x, M, n, k)
+    torch.cuda.synchronize()
+    HF.OP_TIMES = {}
     for _ in range(reps):
-        L.call("hvit_linear_fwd", *args)
-    e1.record(st)
-    e1.synchronize()
-    sec = e0.elapsed_time(e1) / 1e3 / reps
-    flops = 2.0 * M * N * K
-    achieved = flops / sec / 1e12
-    return {"kernel": "hvit gemm_kernel<bf16,128,128,LdDense,LdDense> (fc1 + GELU_DUAL epilogue)",
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": measured_traffic(),
-            "flops_per_launch": flops, "avg_launch_us": round(sec * 1e6, 2)}
+        for dy, x, n, k in ops:
+            HF.linear_wgrad(hv._lib.BF16, dy, x, M, n, k, tag="vit_linear_wgrad")
+    torch.cuda.synchronize()
+    t = op_table(HF.OP_TIMES, reps)
+    HF.OP_TIMES = None
+    return roofline_of(t)
 
 
-def measured_traffic():
-    """HBM bytes per launch of the roofline kernel from the committed PMC pass
+def measured_traffic(name):
+    """HBM bytes per launch of op class ``name`` from the committed PMC pass
     (profiles/roofline_pmc.json, written by tools/pmc_summary.py from
-    rocprofv3 --pmc FETCH_SIZE WRITE_SIZE on ``bench.py --roofline-only``;
-    FETCH_SIZE doubled per the gfx950 correction).  None when absent."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over ``bench.py
+    --roofline-only``; FETCH_SIZE doubled per the gfx950 correction).  None
+    when absent or recorded for another op."""
     p = os.path.join(ROOT, "profiles", "roofline_pmc.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch") if d.get("op") == name else None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(batch, budget_s):
     """Oracle (fp32 PyTorch CPU restatement of the reference) train step:
-    fwd + CombinedLoss + bwd + AdamW, same shapes, bounded by ``budget_s``."""
+    fwd + CombinedLoss + bwd + clip + AdamW on the same synthetic
+    spectrograms, bounded by ``budget_s``."""
+    from hvit_amd.data import spectrogram_batch
     from oracle import closed_form as CF
     from oracle import hvit_oracle as O
 
@@ -109,8 +152,7 @@ def cpu_baseline(batch, budget_s):
     sd = O.make_state(shapes, CF.weights(shapes), requires_grad=True)
     params = [v for k, v in sd.items() if v.requires_grad]
     opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=0.01)
-    x = torch.rand(batch, 1, 256, 256)
-    t = torch.rand(batch, 1, 256, 256)
+    x, t = spectrogram_batch(batch, seed=1234)
 
     def step():
         y = O.forward(sd, x, cfg, training=True)
@@ -127,9 +169,9 @@ def cpu_baseline(batch, budget_s):
         n += 1
     dt = (time.perf_counter() - t0) / n
     return {"value": round(batch * FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", "cpu": cpu_model(),
             "sample": f"oracle/hvit_oracle.py fp32 train step (fwd+CombinedLoss+bwd+clip+AdamW), B={batch}, "
-                      f"1x256x256, 1 warmup + {n} timed steps, {dt:.2f} s/step"}
+                      f"1x256x256 synthetic spectrograms, 1 warmup + {n} timed steps, {dt:.2f} s/step"}
 
 
 def main():
@@ -151,7 +193,7 @@ def main():
 
     hv = hvit_amd_loader.load()
     if args.roofline_only:
-        print(json.dumps(dominant_kernel_roofline(hv, args.batch)), flush=True)
+        print(json.dumps(roofline_loop(hv, args.batch)), flush=True)
         return
     from hvit_amd.data import spectrogram_batch
     from hvit_amd.dp import GradAllReducer, broadcast_module
@@ -208,9 +250,27 @@ def main():
     if not torch.isfinite(loss).item():
         raise RuntimeError("non-finite loss")
 
+    # host enqueue cost of one step while the GPU queue is busy (no sync inside)
+    HF = sys.modules["hvit_amd.functional"]
+    step()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        step()
+    host_ms = (time.perf_counter() - t1) / 3 * 1e3
+    torch.cuda.synchronize()
+    # instrumented repeat of the timed steps: HIP events around every launch of
+    # each op class (functional.timed), for the per-op roofline table
+    isteps = min(args.steps, 10)
+    HF.OP_TIMES = {}
+    for _ in range(isteps):
+        step()
+    torch.cuda.synchronize()
+    table = op_table(HF.OP_TIMES, isteps)
+    HF.OP_TIMES = None
+
     out = None
     if rank == 0:
-        roof = dominant_kernel_roofline(hv, args.batch)
+        roof = roofline_of(table)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.mode == "train" and args.variant == "default":
             cpu = cpu_baseline(args.batch, args.cpu_seconds)
@@ -237,8 +297,11 @@ def main():
                        "parallelism": f"dp{world}"},
             "spectrograms_per_s": round(spectros, 2),
             "frames_per_s_per_gpu": round(value / world, 1),
+            "value_is": "aggregate spectrogram frames/s over all n_gpus (per-GPU figure: frames_per_s_per_gpu)",
+            "host_enqueue_ms_per_step": round(host_ms, 3),
             "final_loss": round(loss.item(), 6),
             "roofline": roof,
+            "op_table": {k: {kk: vv for kk, vv in v.items() if kk != "work_per_launch"} for k, v in table.items()},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

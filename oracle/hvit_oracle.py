@@ -292,15 +292,35 @@ def forward(sd: Dict[str, torch.Tensor], x: torch.Tensor, cfg: HViTConfig,
     return x
 
 
-def combined_loss(pred, target, l1_weight=1.0, stoi_weight=0.1):
-    """CombinedLoss.forward (training/losses.py:330-387) with the default weights
-    of create_loss_function (:390-408): l1·L1 + stoi·mean(1 - cos(flat(p), flat(t)))
-    (STOILoss :109-141)."""
-    l1 = (pred - target).abs().mean()
-    pn = F.normalize(pred.flatten(1), dim=1)
-    tn = F.normalize(target.flatten(1), dim=1)
-    stoi = (1.0 - (pn * tn).sum(1)).mean()
-    return l1_weight * l1 + stoi_weight * stoi
+def combined_loss(pred, target, l1_weight=1.0, stoi_weight=0.1, mse_weight=0.0, perceptual_weight=0.0,
+                  use_log_compression=False, return_components=False):
+    """CombinedLoss.forward (training/losses.py:330-387); defaults are those of
+    create_loss_function (:390-408).  l1·L1 + mse·MSE on log(x + 1e-8) when
+    use_log_compression (:319-321, :344-346), + stoi·mean(1 - cos(flat(p),
+    flat(t))) (STOILoss :109-141, on the uncompressed inputs) + perceptual·L1
+    (PerceptualLoss :270-283, placeholder L1 on the uncompressed inputs)."""
+    pi, ti = (torch.log(pred + 1e-8), torch.log(target + 1e-8)) if use_log_compression else (pred, target)
+    total = 0.0
+    comps = {}
+    if l1_weight > 0:
+        l1 = (pi - ti).abs().mean()
+        comps["l1"] = l1
+        total = total + l1_weight * l1
+    if mse_weight > 0:
+        mse = ((pi - ti) ** 2).mean()
+        comps["mse"] = mse
+        total = total + mse_weight * mse
+    if stoi_weight > 0:
+        pn = F.normalize(pred.flatten(1), dim=1)
+        tn = F.normalize(target.flatten(1), dim=1)
+        stoi = (1.0 - (pn * tn).sum(1)).mean()
+        comps["stoi"] = stoi
+        total = total + stoi_weight * stoi
+    if perceptual_weight > 0:
+        perc = (pred - target).abs().mean()
+        comps["perceptual"] = perc
+        total = total + perceptual_weight * perc
+    return (total, comps) if return_components else total
 
 
 def is_buffer(key: str) -> bool:

@@ -3,19 +3,38 @@
 The reference has no distributed code; the build adds the one
 exchange the path has: the gradient all-reduce of a batch-sharded step.  One
 process per GPU, ``torch.distributed`` with the RCCL backend ("nccl" on ROCm)
-over xGMI; gloo works for CPU tests.
+over xGMI; gloo works for CPU tests and for ranks that share one GPU.
 
-Gradients are bucketed (default 25 MB) in reverse registration order, which is
-roughly the order backward produces them; a bucket's all-reduce is launched
-from a post-accumulate-grad hook as soon as its last gradient lands, so
-communication overlaps the rest of the backward.  BatchNorm statistics stay
-per replica (no SyncBN in the reference).  ``pos_encoding.pos_embed`` only has
-non-zero gradient in its first N rows (N patches), so only that slice is
-reduced: 18 % fewer bytes for the default model, bit-identical result.
+* Gradients are bucketed (default 25 MB) in reverse registration order, which
+  is roughly the order backward produces them.  A bucket's all-reduce is
+  launched from a post-accumulate-grad hook as soon as its last gradient lands,
+  so communication overlaps the rest of the backward.
+* Every bucket owns two persistent flat buffers used on alternate steps.
+  Gradients are copied into the step's buffer once (the launch), and after the
+  reduction each parameter's ``.grad`` becomes a view of the averaged buffer:
+  no per-step concatenation buffer and no copy-back.  Alternating keeps a
+  launch from ever reducing in place under a ``.grad`` view that a later
+  accumulating backward still writes (``zero_grad(set_to_none=False)``).
+* Gradient accumulation (trainer.py:72, :164-183: several backward passes
+  before one optimizer step) is exact: a bucket whose gradients change after
+  its all-reduce was launched is marked stale and re-reduced from the current
+  ``.grad`` in ``finish()``.  ``no_sync()`` skips the wasted early launches.
+* ``sliced={"pos_encoding.pos_embed": R}`` reduces only the first R rows of a
+  parameter whose gradient is zero beyond the token count (the 10 000-row
+  positional table; 18 % of the default model's gradient bytes at N = 256).
+  R must bound the token count of every forward on every rank; the model's
+  ``last_num_tokens`` is checked against it in ``finish()`` and a larger count
+  raises.  Without ``sliced`` the whole table is reduced (exact for any N).
+* BatchNorm statistics are computed per replica (local BN, as DDP without
+  SyncBN; the reference has no distributed code to match).  With
+  ``broadcast_buffers`` (default, as DDP) rank 0's running statistics are
+  broadcast to every rank in ``finish()`` (one coalesced broadcast), so replicas
+  never diverge and any rank's ``state_dict`` equals rank 0's.
 """
 
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, List, Optional
 
 import torch
@@ -24,13 +43,17 @@ import torch.distributed as dist
 
 class GradAllReducer:
     def __init__(self, model: torch.nn.Module, bucket_mb: float = 25.0, group=None,
-                 sliced: Optional[Dict[str, int]] = None):
+                 sliced: Optional[Dict[str, int]] = None, broadcast_buffers: bool = True):
+        self.model = model
         self.group = group
         self.world = dist.get_world_size(group)
         self.sliced = dict(sliced or {})
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         self.params = [p for _, p in named]
         self.names = {id(p): n for n, p in named}
+        for n in self.sliced:
+            if n not in dict(named):
+                raise KeyError(f"hvit GradAllReducer: no parameter {n!r} to slice")
         cap = int(bucket_mb * 1024 * 1024)
         self.buckets: List[List[torch.nn.Parameter]] = []
         cur, size = [], 0
@@ -44,61 +67,132 @@ class GradAllReducer:
         if cur:
             self.buckets.append(cur)
         self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
+        self.offsets = []
+        for ps in self.buckets:
+            offs, o = [], 0
+            for p in ps:
+                offs.append(o)
+                o += self._numel(p)
+            self.offsets.append((offs, o))
+        self.flats: List[List[Optional[torch.Tensor]]] = [[None, None] for _ in self.buckets]
+        self._gen = 0
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._fwd_hook = model.register_forward_hook(self._on_forward)
+        self._syncing = True
+        self.broadcast_buffers = broadcast_buffers
+        self._bufs = [b for b in model.buffers() if b.is_floating_point()]
+        self._max_tokens = 0
         self.reset()
 
+    # ------------------------------------------------------------ helpers --
+    def _rows(self, p):
+        return self.sliced.get(self.names[id(p)])
+
     def _numel(self, p):
-        rows = self.sliced.get(self.names[id(p)])
+        rows = self._rows(p)
         return p[:, :rows].numel() if rows is not None else p.numel()
 
     def _view(self, p):
-        rows = self.sliced.get(self.names[id(p)])
-        g = p.grad
-        return g[:, :rows] if rows is not None else g
+        rows = self._rows(p)
+        return p.grad[:, :rows] if rows is not None else p.grad
+
+    def _on_forward(self, module, args, out):
+        n = getattr(module, "last_num_tokens", None)
+        if n is not None:
+            self._max_tokens = max(self._max_tokens, int(n))
 
     def set_rows(self, name: str, rows: int):
-        self.sliced[name] = rows
+        """Change a sliced parameter's row bound (bucket sizes follow)."""
+        if name not in self.sliced:
+            raise KeyError(name)
+        self.remove()
+        self.__init__(self.model, group=self.group, sliced={**self.sliced, name: rows},
+                      broadcast_buffers=self.broadcast_buffers)
 
     def reset(self):
-        self.pending = [len(b) for b in self.buckets]
+        self.seen = [set() for _ in self.buckets]
         self.works = [None] * len(self.buckets)
-        self.flats = [None] * len(self.buckets)
+        self.stale = [False] * len(self.buckets)
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulation micro-steps: gradients accumulate locally, no bucket
+        is launched (DDP's no_sync); the step after the context syncs."""
+        prev, self._syncing = self._syncing, False
+        try:
+            yield
+        finally:
+            self._syncing = prev
+
+    # ------------------------------------------------------------ the hook --
     def _on_grad(self, p):
+        if not self._syncing:
+            return
         b = self.where[id(p)]
-        self.pending[b] -= 1
-        if self.pending[b] == 0:
+        if self.works[b] is not None:  # another backward changed an already-launched bucket
+            self.stale[b] = True
+            return
+        self.seen[b].add(id(p))
+        if len(self.seen[b]) == len(self.buckets[b]):
             self._launch(b)
 
     def _launch(self, b):
-        flat = torch.cat([self._view(p).reshape(-1) for p in self.buckets[b]])
-        self.flats[b] = flat
+        ps = self.buckets[b]
+        offs, total = self.offsets[b]
+        flat = self.flats[b][self._gen]
+        if flat is None or flat.device != ps[0].grad.device:
+            flat = self.flats[b][self._gen] = torch.empty(total, dtype=torch.float32, device=ps[0].grad.device)
+        for p, o in zip(ps, offs):
+            v = self._view(p)
+            dst = flat[o:o + v.numel()].view_as(v)
+            if dst.data_ptr() != v.data_ptr():
+                dst.copy_(v)
         self.works[b] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish(self):
         """Wait for every bucket (launching any whose hooks did not fire, e.g.
-        unused parameters), write averaged gradients back, reset for the next
-        step."""
+        unused parameters or a step taken under no_sync, and re-launching stale
+        ones), install the averaged gradients, broadcast rank 0's buffers, and
+        reset for the next step."""
+        for name, rows in self.sliced.items():
+            if self._max_tokens > rows:
+                raise RuntimeError(f"hvit GradAllReducer: a forward used {self._max_tokens} tokens but only "
+                                   f"{rows} rows of {name} are reduced; raise sliced[{name!r}]")
         for b, ps in enumerate(self.buckets):
-            if self.works[b] is None:
-                for p in ps:
-                    if p.grad is None:
-                        p.grad = torch.zeros_like(p)
-                self._launch(b)
+            if self.works[b] is not None and not self.stale[b]:
+                continue
+            if self.works[b] is not None:
+                self.works[b].wait()
+            for p in ps:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            self._launch(b)
         for b, ps in enumerate(self.buckets):
             self.works[b].wait()
-            flat = self.flats[b].div_(self.world)
-            off = 0
-            for p in ps:
-                v = self._view(p)
-                n = v.numel()
-                v.copy_(flat[off:off + n].view_as(v))
-                off += n
+            flat = self.flats[b][self._gen].div_(self.world)
+            offs, _ = self.offsets[b]
+            for p, o in zip(ps, offs):
+                if self._rows(p) is not None:
+                    v = self._view(p)
+                    v.copy_(flat[o:o + v.numel()].view_as(v))
+                else:
+                    p.grad = flat[o:o + p.numel()].view_as(p)
+        if self.broadcast_buffers and self.world > 1 and self._bufs:
+            with torch.no_grad():
+                fb = torch.cat([t.reshape(-1).float() for t in self._bufs])
+                dist.broadcast(fb, 0, group=self.group)
+                o = 0
+                for t in self._bufs:
+                    t.copy_(fb[o:o + t.numel()].view_as(t))
+                    o += t.numel()
+        self._max_tokens = 0
+        self._gen ^= 1
         self.reset()
 
     def remove(self):
         for h in self._hooks:
             h.remove()
+        self._fwd_hook.remove()
 
 
 def broadcast_module(model: torch.nn.Module, src: int = 0, group=None):
@@ -106,3 +200,15 @@ def broadcast_module(model: torch.nn.Module, src: int = 0, group=None):
     with torch.no_grad():
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, src, group=group)
+
+
+def save_on_rank0(obj, path: str, group=None) -> bool:
+    """torch.save(obj, path) on rank 0 only (Trainer.save_checkpoint,
+    trainer.py:350-380, under DP), then a barrier so no rank reads the file
+    before it is complete.  Returns True on the rank that wrote."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if rank == 0:
+        torch.save(obj, path)
+    if dist.is_initialized():
+        dist.barrier(group=group)
+    return rank == 0

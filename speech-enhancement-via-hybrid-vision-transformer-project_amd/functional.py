@@ -24,6 +24,46 @@ from ._lib import call, ptr, stream_ptr
 F32, BF16 = L.F32, L.BF16
 
 
+# ---------------------------------------------------------------------------
+# In-step op timing (measurement only; off unless a caller installs a table).
+# bench.py installs OP_TIMES = {} around its timed region: every instrumented
+# op records a HIP event pair on the stream it launches on, so an op's GPU
+# duration is measured inside the real training step.  Off, `timed` is a no-op.
+OP_TIMES = None
+
+
+class _Timed:
+    __slots__ = ("name", "work", "e0")
+
+    def __init__(self, name, work):
+        self.name, self.work = name, work
+
+    def __enter__(self):
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e0.record()
+
+    def __exit__(self, *exc):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        OP_TIMES.setdefault(self.name, []).append((self.e0, e1, self.work))
+
+
+class _Untimed:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_UNTIMED = _Untimed()
+
+
+def timed(name: str, work: float):
+    """Context for one op launch sequence; ``work`` = algorithmic FLOPs or bytes."""
+    return _UNTIMED if OP_TIMES is None else _Timed(name, work)
+
+
 def _empty(shape, dt, dev):
     return torch.empty(shape, dtype=L.torch_dtype(dt), device=dev)
 
@@ -183,7 +223,7 @@ def col_sum(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
     return out
 
 
-def linear_wgrad(dt, dy, x, M, N, K, bias=False):
+def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad"):
     """dw [N, K] = dy^T x (f32); with ``bias`` also db [N] = colsum(dy), which
     the bf16 path fuses into the GEMM (db stored right after dw)."""
     buf = torch.empty(N * K + (N if bias else 0), dtype=torch.float32, device=dy.device)
@@ -191,8 +231,9 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False):
     db = buf[N * K:] if bias else None
     ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
-    call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db), ws.data_ptr(), ws_n,
-         stream_ptr())
+    with timed(tag, 2.0 * M * N * K):
+        call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db), ws.data_ptr(),
+             ws_n, stream_ptr())
     return (dw, db) if bias else dw
 
 
@@ -234,7 +275,9 @@ def conv_wgrad(dt, g: L.ConvGeom, dz, wshape) -> torch.Tensor:
     dwp = torch.empty(co * ci * ks * ks, dtype=torch.float32, device=dz.device)
     ws_n = L.lib().hvit_conv_wgrad_workspace(g)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dz.device)
-    call("hvit_conv_wgrad", dt, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, stream_ptr())
+    P = dz.numel() // co  # output pixels
+    with timed("conv_wgrad", 2.0 * P * co * ci * ks * ks):
+        call("hvit_conv_wgrad", dt, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, stream_ptr())
     return unpack_conv(dwp, wshape)
 
 
@@ -283,22 +326,27 @@ class ConvBNActFn(torch.autograd.Function):
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
         mean = torch.empty(Cout, dtype=torch.float32, device=dev)
         invstd = torch.empty_like(mean)
+        P = N * H * W
+        es = 4 if dt == F32 else 2
+        cflops = 2.0 * P * Cout * Cin * KS * KS
         if training:
-            P = N * H * W
             tr = L.lib().hvit_conv_bn_tile_rows(C.byref(g))  # rows per BN partial tile
             nt = (P + tr - 1) // tr
             part = torch.empty((nt, Cout, 2), dtype=torch.float32, device=dev)
-            call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, part.data_ptr(), None, s)
+            with timed("conv_fwd", cflops):
+                call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, part.data_ptr(), None, s)
             call("hvit_bn_finalize", part.data_ptr(), nt, tr, P, Cout, mean.data_ptr(), invstd.data_ptr(),
                  ptr(rmean), ptr(rvar), ptr(nbt), momentum, eps, s)
         else:
-            call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, None, None, s)
+            with timed("conv_fwd", cflops):
+                call("hvit_conv_fwd", dt, g, wp.data_ptr(), None, z.data_ptr(), dt, None, None, s)
             call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
                  invstd.data_ptr(), s)
         y = _empty((N, H // pool, W // pool, Cout), dt, dev)
         dr = drop.c() if training else L.dropout()
-        call("hvit_bn_act_fwd", dt, z.data_ptr(), N, H, W, Cout, mean.data_ptr(), invstd.data_ptr(),
-             gamma.data_ptr(), beta.data_ptr(), dr, pool, y.data_ptr(), dt, s)
+        with timed("bn_act_fwd", float(P * Cout * es * (1 + 1.0 / (pool * pool)))):  # read z, write y
+            call("hvit_bn_act_fwd", dt, z.data_ptr(), N, H, W, Cout, mean.data_ptr(), invstd.data_ptr(),
+                 gamma.data_ptr(), beta.data_ptr(), dr, pool, y.data_ptr(), dt, s)
         ctx.save_for_backward(x1, x2, w, gamma, beta)
         ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
         ctx.meta = (U, pool, training, dr, dt)
@@ -319,9 +367,10 @@ class ConvBNActFn(torch.autograd.Function):
         dy = dy.contiguous()
         dz = _empty(z.shape, dt, dev)
         sums = ctx.zs.take(dev)
-        call("hvit_bn_act_bwd", dt, z.data_ptr(), N, H, W, Cout, ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
-             gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
-             dz.data_ptr(), dt, sums.data_ptr(), L.ACC_ZEROED, s)
+        with timed("bn_act_bwd", float(2 * z.numel() * z.element_size() + dy.numel() * dy.element_size())):
+            call("hvit_bn_act_bwd", dt, z.data_ptr(), N, H, W, Cout, ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
+                 gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
+                 dz.data_ptr(), dt, sums.data_ptr(), L.ACC_ZEROED, s)
         dbeta, dgamma = sums[:Cout], sums[Cout:2 * Cout]
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
         dw = conv_wgrad(dt, g, dz, w.shape)
@@ -329,7 +378,8 @@ class ConvBNActFn(torch.autograd.Function):
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             wd = pack_conv(w, 1, dt)
             du = _empty((N, H, W, C1 + C2), dt, dev)
-            call("hvit_conv_dgrad", dt, g, dz.data_ptr(), wd.data_ptr(), du.data_ptr(), dt, s)
+            with timed("conv_dgrad", 2.0 * N * H * W * Cout * (C1 + C2) * KS * KS):
+                call("hvit_conv_dgrad", dt, g, dz.data_ptr(), wd.data_ptr(), du.data_ptr(), dt, s)
             if U == 1 and C2 == 0:
                 dx1 = du
             else:
@@ -451,27 +501,32 @@ class ViTBlockFn(torch.autograd.Function):
         xn1, m1, r1 = _ln(x2d, n1w, n1b, dt)
         Wqkv = cast(qkvw, dt)
         qkv = _empty((M, 3 * D), dt, dev)
-        call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
-             qkv.data_ptr(), dt, None, s)
+        with timed("vit_linear_fwd", 2.0 * M * 3 * D * D):
+            call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
+                 qkv.data_ptr(), dt, None, s)
         o = _empty((M, D), dt, dev)
         lse = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         probs = torch.empty((B, H, Nt, Nt), dtype=torch.float32, device=dev) if want_probs else None
-        call("hvit_mhsa_fwd", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(), lse.data_ptr(),
-             ptr(probs), s)
+        with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
+            call("hvit_mhsa_fwd", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(), lse.data_ptr(),
+                 ptr(probs), s)
         Wp = cast(pw, dt)
         x1 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D, x1.data_ptr(), F32,
-             epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), s)
+        with timed("vit_linear_fwd", 2.0 * M * D * D):
+            call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D, x1.data_ptr(), F32,
+                 epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), s)
         xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
         W1 = cast(f1w, dt)
         h = _empty((M, hid), dt, dev)
         a = _empty((M, hid), dt, dev)
-        call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, h.data_ptr(), dt,
-             epilogue(act=L.ACT_GELU_DUAL, out2=a, drop=d_fc1.c()), s)
+        with timed("vit_linear_fwd", 2.0 * M * hid * D):
+            call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, h.data_ptr(), dt,
+                 epilogue(act=L.ACT_GELU_DUAL, out2=a, drop=d_fc1.c()), s)
         W2 = cast(f2w, dt)
         x2 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid, x2.data_ptr(), F32,
-             epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
+        with timed("vit_linear_fwd", 2.0 * M * D * hid):
+            call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid, x2.data_ptr(), F32,
+                 epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
         ctx.save_for_backward(n1w, n2w)
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
@@ -498,33 +553,39 @@ class ViTBlockFn(torch.autograd.Function):
         g2 = _empty((M, D), dt, dev)
         df2b = zf2b.take(dev)
         dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
-        df2w = linear_wgrad(dt, g2, a, M, D, hid)
+        df2w = linear_wgrad(dt, g2, a, M, D, hid, tag="vit_linear_wgrad")
         dh = _empty((M, hid), dt, dev)
         df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
-        call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
-             epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1, colsum=df1b), s)
-        df1w = linear_wgrad(dt, dh, xn2, M, hid, D)
+        with timed("vit_linear_dgrad", 2.0 * M * D * hid):
+            call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
+                 epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1, colsum=df1b), s)
+        df1w = linear_wgrad(dt, dh, xn2, M, hid, D, tag="vit_linear_wgrad")
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
+        with timed("vit_linear_dgrad", 2.0 * M * hid * D):
+            call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
         dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2, zln2)
         # attention branch
         g1 = _empty((M, D), dt, dev)
         dpb = zpb.take(dev)
         dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
-        dpw = linear_wgrad(dt, g1, o, M, D, D)
+        dpw = linear_wgrad(dt, g1, o, M, D, D, tag="vit_linear_wgrad")
         do = _empty((M, D), dt, dev)
-        call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
+        with timed("vit_linear_dgrad", 2.0 * M * D * D):
+            call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
-        call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H, D // H,
-             scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
+        with timed("attn_bwd", 8.0 * B * H * Nt * Nt * (D // H)):
+            call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H, D // H,
+                 scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
         # qkv bias grad by a column reduction: the wgrad GEMM variant with fused
         # A-row sums spills at 128x128 (rocprof: 42 -> 28 us class without it)
-        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D)
+        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, tag="vit_linear_wgrad")
         dqkvb = zqb.take(dev)
         call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None, s)
+        with timed("vit_linear_dgrad", 2.0 * M * 3 * D * D):
+            call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None,
+                 s)
         dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
                 None, None, None, None, None, None)

@@ -184,6 +184,20 @@ class VisionTransformer(nn.Module):
         self.norm = nn.LayerNorm(embed_dim)
 
 
+def _on_input_device(fn):
+    """Run a forward entry point under a device guard for its input tensor."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(self, x, *a, **k):
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            with torch.cuda.device(x.device):
+                return fn(self, x, *a, **k)
+        return fn(self, x, *a, **k)
+
+    return run
+
+
 # ------------------------------------------------------------------ model ---
 class HybridViT(nn.Module):
     """HybridViT (models/hybrid_vit.py:21-489) on the gfx950 HIP path."""
@@ -223,6 +237,7 @@ class HybridViT(nn.Module):
         self.num_heads = num_heads
         self.dropout_p = dropout
         self.precision = precision
+        self.last_num_tokens = 0  # patch tokens N of the latest forward (dp.GradAllReducer checks it)
 
         self.encoder = nn.ModuleList()
         in_ch = input_channels
@@ -285,6 +300,9 @@ class HybridViT(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("hvit: the HIP path needs GPU tensors (call .to('cuda')); there is no CPU path")
         lib = L.lib()  # noqa: F841  (fails loudly when libhvit.so is missing)
+        for n, t in self.named_parameters():
+            if t.device != x.device:
+                raise RuntimeError(f"hvit: input on {x.device} but parameter {n} on {t.device}")
 
     def _seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
@@ -338,6 +356,7 @@ class HybridViT(nn.Module):
         pe = self.patch_embed.projection
         t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, self.pos_encoding.pos_embed, P,
                                   HF.Drop(self.dropout_p, seed, 200), self.training, dt)
+        self.last_num_tokens = t.shape[1]
         return t, (feat.shape[1] // P, feat.shape[2] // P)
 
     def _vit(self, t, dt, seed, want_attn=False):
@@ -375,6 +394,7 @@ class HybridViT(nn.Module):
         raise RuntimeError("hvit: decoder has no final layer")
 
     # -------------------------------------------------------- reference API --
+    @_on_input_device
     def forward_encoder(self, x: torch.Tensor) -> Tuple[torch.Tensor, List[torch.Tensor]]:
         """hybrid_vit.py:286-307.  Returns NCHW views (channels-last storage)."""
         self._check_device(x)
@@ -383,12 +403,14 @@ class HybridViT(nn.Module):
         HF.zflush(x.device)
         return self._nchw(h), [self._nchw(s) for s in skips]
 
+    @_on_input_device
     def forward_transformer(self, x: torch.Tensor, spatial_shape: Tuple[int, int]) -> torch.Tensor:
         """hybrid_vit.py:309-350: patch tokens [B, N, D] (without pos-enc) -> [B, C, H, W]."""
         self._check_device(x)
         dt = self._dt()
         seed = self._seed()
         B, N, D = x.shape
+        self.last_num_tokens = N
         pos = self.pos_encoding.pos_embed[:, :N, :]
         t = x.float() + pos
         if self.training and self.dropout_p > 0:
@@ -398,6 +420,7 @@ class HybridViT(nn.Module):
         HF.zflush(x.device)
         return self._nchw(out)
 
+    @_on_input_device
     def forward_decoder(self, x: torch.Tensor, skip_features: List[torch.Tensor]) -> torch.Tensor:
         """hybrid_vit.py:352-394 (output before the final resize)."""
         self._check_device(x)
@@ -414,8 +437,14 @@ class HybridViT(nn.Module):
         return self._nchw(out)
 
     def forward(self, x: torch.Tensor, return_attentions: bool = False):
-        """hybrid_vit.py:396-469."""
+        """hybrid_vit.py:396-469.  Kernels are launched on ``x``'s device (a
+        device guard, so a model on cuda:1 works while cuda:0 is current; the
+        autograd engine runs the backward on the same device)."""
         self._check_device(x)
+        with torch.cuda.device(x.device):
+            return self._forward(x, return_attentions)
+
+    def _forward(self, x: torch.Tensor, return_attentions: bool):
         if x.dim() != 4:
             raise ValueError(f"hvit: expected [B, C, F, T], got {tuple(x.shape)}")
         dt = self._dt()

@@ -104,6 +104,12 @@ class FusedAdamW(torch.optim.Optimizer):
                 raise RuntimeError("hvit FusedAdamW: sparse gradients are not supported")
             if not p.is_cuda or p.dtype != torch.float32:
                 raise TypeError("hvit FusedAdamW: parameters must be float32 GPU tensors")
+            # the kernel walks p, grad, exp_avg and exp_avg_sq as flat arrays: all
+            # four must share one dense layout (a channels_last parameter with a
+            # contiguous grad would pair the wrong elements)
+            if not p.is_contiguous() or p.grad.stride() != p.stride():
+                raise ValueError("hvit FusedAdamW: parameters and their gradients must be contiguous "
+                                 "(a strided / channels_last parameter is not supported)")
         coef = None
         if self.max_grad_norm is not None:
             coef = _clip_coef([p.grad for p in live], self.max_grad_norm)
@@ -124,11 +130,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 by_step.setdefault(float(st["step"]), []).append(p)
             for step, ps in by_step.items():
                 items = (L.AdamWItem * len(ps))()
-                keep = []  # contiguous copies of strided grads live until the launch
                 for i, p in enumerate(ps):
                     st = self.state[p]
-                    g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                    keep.append(g)
+                    g = p.grad
                     sh = HF.shadow_of(p)
                     items[i] = L.AdamWItem(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
                                            st["exp_avg_sq"].data_ptr(), sh.data_ptr() if sh is not None else None,

@@ -43,6 +43,8 @@ class Toy(torch.nn.Module):
 
     def forward(self, x):  # x [B, N, 8], N <= 50
         n = x.shape[1]
+        self.last_num_tokens = n
+        self.running.add_(1.0)  # a per-replica buffer update (like BN running stats)
         h = x + self.pos_embed[:, :n]
         h = h * self.shared
         h = self.fc2(torch.nn.functional.gelu(self.fc1(h)))
@@ -111,7 +113,82 @@ def test_grad_allreduce_matches_full_batch(bucket_mb):
     for rank, err, tail, running, wsum, nb in out:
         assert err < 1e-6, (rank, err)
         assert tail == 0.0
-        assert running == 1.0  # buffers broadcast from rank 0
+        assert running == 3.0  # rank 0's buffers (1, then +1 per forward) broadcast by finish()
     assert out[0][4] == out[1][4]  # identical parameters after broadcast
     if bucket_mb < 0.01:
         assert out[0][5] > 1  # several buckets exercised
+
+
+def _worker_accum(rank, world, port, mode, q):
+    """Gradient accumulation (trainer.py:164-183): two micro-batches per step,
+    with hooks live on both (mode 'hooks': stale buckets re-reduced) or the
+    first under no_sync() (mode 'no_sync'); zero_grad with set_to_none False
+    (grads stay views of the reducer's buffers) or True."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import importlib
+
+        import hvit_amd_loader
+
+        hvit_amd_loader.load()
+        dp = importlib.import_module("hvit_amd.dp")
+        torch.manual_seed(3)
+        model = Toy()
+        dp.broadcast_module(model)
+        torch.manual_seed(9)
+        xs = [torch.randn(4 * world, 12, 8) for _ in range(6)]
+        red = dp.GradAllReducer(model, bucket_mb=0.0005, sliced={"pos_embed": 16})
+        to_none = mode.endswith("none")
+        errs = []
+        for step in range(3):
+            model.zero_grad(set_to_none=to_none)
+            a, b = xs[2 * step], xs[2 * step + 1]
+            if mode.startswith("no_sync"):
+                with red.no_sync():
+                    model(a[rank * 4:(rank + 1) * 4]).backward()
+            else:
+                model(a[rank * 4:(rank + 1) * 4]).backward()
+            model(b[rank * 4:(rank + 1) * 4]).backward()
+            red.finish()
+            ref = Toy()
+            ref.load_state_dict(model.state_dict())
+            grads = {n: torch.zeros_like(p) for n, p in ref.named_parameters()}
+            for r in range(world):
+                for xx in (a, b):
+                    ref.zero_grad(set_to_none=True)
+                    ref(xx[r * 4:(r + 1) * 4]).backward()
+                    for n, p in ref.named_parameters():
+                        if p.grad is not None:
+                            grads[n] += p.grad / world
+            errs.append(max(((p.grad if p.grad is not None else torch.zeros_like(p)) - grads[n]).abs().max().item()
+                            for n, p in model.named_parameters()))
+        # token bound: a forward with more tokens than the sliced rows raises
+        raised = False
+        model.zero_grad(set_to_none=True)
+        model(torch.randn(4, 20, 8)).backward()
+        try:
+            red.finish()
+        except RuntimeError:
+            raised = True
+        q.put((rank, max(errs), raised))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["hooks_none", "hooks_keep", "no_sync_none", "no_sync_keep"])
+def test_grad_accumulation(mode):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_accum, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, raised in out:
+        assert err < 1e-6, (mode, rank, err)
+        assert raised

@@ -1,0 +1,111 @@
+"""GPU: the data-parallel HybridViT step (BASELINE config 4) with
+the real HIP model on every rank.  Two ranks share cuda:0 over gloo (RCCL
+refuses two ranks on one device; the 8-GPU RCCL run is the driver's).  Each
+rank runs the tiny HybridViT (fp32, dropout off, train-mode BN = local BN per
+replica) on its batch shard under GradAllReducer; the reduced gradients must
+equal the mean of the per-shard gradients computed single-process, replicas
+must stay bit-identical through FusedAdamW steps, and rank 0's BN statistics
+must be broadcast.  The input has N = 260 > 256 patch tokens, so pos_embed rows
+beyond 256 carry gradient (reduced through ``sliced`` rows = 320)."""
+
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KW = dict(encoder_channels=[8, 16, 32], embed_dim=64, num_heads=4, num_layers=2, decoder_channels=[32, 16, 8, 1],
+          dropout=0.0, attn_dropout=0.0, drop_path_rate=0.0, precision="fp32")
+SHAPE = (2, 1, 64, 1040)   # per rank; N = (64/16) * (1040/16) = 4 * 65 = 260 tokens
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import copy
+        import importlib
+
+        import hvit_amd_loader
+
+        hv = hvit_amd_loader.load()
+        dp = importlib.import_module("hvit_amd.dp")
+        torch.cuda.set_device(0)
+        torch.manual_seed(11 + rank)  # ranks start different: broadcast_module aligns them
+        model = hv.HybridViT(**KW).cuda().train()
+        dp.broadcast_module(model)
+        ref = copy.deepcopy(model)
+        g = torch.Generator().manual_seed(5)
+        x = torch.rand((world * SHAPE[0],) + SHAPE[1:], generator=g)
+        t = torch.rand(x.shape, generator=g)
+        crit = hv.CombinedLoss()
+        red = dp.GradAllReducer(model, bucket_mb=0.05, sliced={"pos_encoding.pos_embed": 320})
+        sl = slice(rank * SHAPE[0], (rank + 1) * SHAPE[0])
+        crit(model(x[sl].cuda()), t[sl].cuda()).backward()
+        red.finish()
+        ntok = model.last_num_tokens
+        # single-process reference: mean of the per-shard gradients (local BN per shard)
+        acc = {n: torch.zeros_like(p) for n, p in ref.named_parameters()}
+        for r in range(world):
+            m = copy.deepcopy(ref)
+            s2 = slice(r * SHAPE[0], (r + 1) * SHAPE[0])
+            crit(m(x[s2].cuda()), t[s2].cuda()).backward()
+            for n, p in m.named_parameters():
+                acc[n] += p.grad / world
+        err = max(((p.grad - acc[n]).norm() / acc[n].norm().clamp_min(1e-20)).item()
+                  for n, p in model.named_parameters())
+        pos_tail = model.pos_encoding.pos_embed.grad[0, 256:ntok].abs().max().item()
+        beyond = model.pos_encoding.pos_embed.grad[0, ntok:].abs().max().item()
+        bn = model.encoder[0].bn.running_mean.clone()
+        bn0 = bn.clone()
+        dist.broadcast(bn0, 0)
+        # replicas stay identical through optimizer steps
+        opt = hv.FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        for _ in range(2):
+            crit(model(x[sl].cuda()), t[sl].cuda()).backward()
+            red.finish()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        csum = torch.stack([p.detach().double().sum() for p in model.parameters()]).cpu()
+        q.put((rank, err, pos_tail, beyond, ntok, torch.equal(bn, bn0), csum))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_hybridvit_two_ranks_on_one_gpu():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, pos_tail, beyond, ntok, bn_same, _ in out:
+        assert ntok == 260
+        assert err < 1e-5, (rank, err)
+        assert pos_tail > 0.0      # rows 256..259 carry gradient and were reduced
+        assert beyond == 0.0
+        assert bn_same             # rank 0's running statistics on every rank
+    assert torch.equal(out[0][6], out[1][6])  # bit-identical replicas after 3 optimizer steps

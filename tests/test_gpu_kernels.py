@@ -470,3 +470,64 @@ def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
         assert rel(dxb.float(), refb) < 2e-2
         l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, dxb.data_ptr(), l.BF16, 1, s())
         assert rel(dxb.float(), 2 * refb) < 2e-2
+
+
+# --------------------------------------------------------------- DropPath ---
+@pytest.mark.parametrize("p", [0.02, 0.1, 0.5])
+def test_droppath_scale_mask_and_rate(hv, p):
+    """hvit_droppath_scale (DropPath components.py:407-427: per-sample
+    x.div(keep) * floor(keep + U)): each sample's scale is 0 or 1/keep, bit-exact
+    against the numpy mirror of the counter hash, and the kept fraction is
+    within 4 sigma of keep = 1 - p."""
+    l = L(hv)
+    B = 65536
+    out = torch.empty(B, device=DEV)
+    l.call("hvit_droppath_scale", B, l.dropout(p, 1234567, 2), out.data_ptr(), s())
+    kept = torch.as_tensor(keep_mask(1234567, 2, B, p), device=DEV)
+    ds = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))  # the kernel's f32 1 / (1 - p)
+    assert torch.equal(out, torch.where(kept, torch.full_like(out, ds), torch.zeros_like(out)))
+    rate = kept.float().mean().item()
+    sigma = (p * (1 - p) / B) ** 0.5
+    assert abs(rate - (1 - p)) < 4 * sigma
+
+def test_vit_block_droppath_matches_torch(hv):
+    """A whole TransformerEncoderBlock (attention.py:176-213) in train mode with
+    drop_path = 0.5 and dropout off, against torch ops on the same weights with
+    the per-sample DropPath masks taken from the hash mirror: dropped samples
+    keep their residual, kept ones get the branch scaled by 1/keep; gradients too."""
+    import sys
+    HF = sys.modules["hvit_amd.functional"]
+    torch.manual_seed(5)
+    B, N, D, H = 16, 64, 64, 4
+    blk = hv.hybrid_vit.TransformerEncoderBlock(D, H, 4.0, True, 0.0, 0.0, 0.5).to(DEV)
+    for prm in blk.parameters():
+        prm.data.normal_(0, 0.1)
+    x = torch.randn(B, N, D, device=DEV, requires_grad=True)
+    seed = 4242
+    drops = (HF.Drop(), HF.Drop(), HF.Drop(), HF.Drop(), seed)
+    a, m = blk.attn, blk.mlp.net
+    y, _ = HF.ViTBlockFn.apply(x, blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias, a.proj.weight,
+                               a.proj.bias, blk.norm2.weight, blk.norm2.bias, m[0].weight, m[0].bias, m[3].weight,
+                               m[3].bias, H, drops, 0.5, True, hv._lib.F32, False)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    k1 = torch.as_tensor(keep_mask(seed, 1, B, 0.5), device=DEV).float() / 0.5
+    k2 = torch.as_tensor(keep_mask(seed, 2, B, 0.5), device=DEV).float() / 0.5
+    assert 0 < k1.count_nonzero() < B and 0 < k2.count_nonzero() < B  # both outcomes occur
+
+    xr = x.detach().clone().requires_grad_(True)
+    P = {n: q.detach().clone().requires_grad_(True) for n, q in blk.named_parameters()}
+    h = F.layer_norm(xr, (D,), P["norm1.weight"], P["norm1.bias"], 1e-5)
+    qkv = F.linear(h, P["attn.qkv.weight"], P["attn.qkv.bias"]).reshape(B, N, 3, H, D // H).permute(2, 0, 3, 1, 4)
+    att = ((qkv[0] @ qkv[1].transpose(-2, -1)) * (D // H) ** -0.5).softmax(-1)
+    o = F.linear((att @ qkv[2]).transpose(1, 2).reshape(B, N, D), P["attn.proj.weight"], P["attn.proj.bias"])
+    x1 = xr + o * k1.view(B, 1, 1)
+    h = F.layer_norm(x1, (D,), P["norm2.weight"], P["norm2.bias"], 1e-5)
+    f = F.linear(F.gelu(F.linear(h, P["mlp.net.0.weight"], P["mlp.net.0.bias"])), P["mlp.net.3.weight"],
+                 P["mlp.net.3.bias"])
+    yr = x1 + f * k2.view(B, 1, 1)
+    (yr * g).sum().backward()
+    assert rel(y.detach(), yr.detach()) < 1e-5
+    assert rel(x.grad, xr.grad) < 1e-4
+    for n, q in blk.named_parameters():
+        assert rel(q.grad, P[n].grad) < 1e-4, n

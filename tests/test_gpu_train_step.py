@@ -174,3 +174,27 @@ def test_train_step_matches_torch_optimizer(hv):
     for (k, pa), pb in zip(ma.named_parameters(), mb.parameters()):
         err = (pa.detach() - pb.detach()).abs().max().item()
         assert err <= 1e-4 * pb.detach().abs().max().item() + 1e-3 * 1e-3 * 3, k
+
+
+def test_combined_loss_reference_fixture(hv):
+    """hvit CombinedLoss against the reference's own CombinedLoss outputs
+    (tests/golden/loss_cases.npz, from training/losses.py:286-387 by
+    tools/gen_golden.py): loss, components and d loss / d pred."""
+    import numpy as np
+    from conftest import golden
+    g = golden("loss_cases")
+    ncase = len({k.split(".")[0] for k in g})
+    for i in range(ncase):
+        kw = {k.split(".")[-1]: float(v) for k, v in g.items() if k.startswith(f"c{i}.kw.")}
+        if "use_log_compression" in kw:
+            kw["use_log_compression"] = bool(kw["use_log_compression"])
+        p = torch.as_tensor(g[f"c{i}.pred"], device=DEV).requires_grad_(True)
+        loss, comps = hv.CombinedLoss(**kw)(p, torch.as_tensor(g[f"c{i}.target"], device=DEV), return_components=True)
+        loss.backward()
+        ref = float(g[f"c{i}.loss"])
+        assert abs(loss.item() - ref) <= 1e-5 * max(1.0, abs(ref)), i
+        assert rel(p.grad.cpu(), torch.as_tensor(g[f"c{i}.dpred"])) < 1e-4, i
+        for k, v in comps.items():
+            if k != "total":
+                assert abs(v.item() - float(g[f"c{i}.comp.{k}"])) < 1e-5, (i, k)
+        assert abs(comps["total"].item() - float(g[f"c{i}.comp.total"])) < 1e-5

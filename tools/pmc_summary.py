@@ -1,40 +1,64 @@
-"""Per-launch PMC summary of the roofline kernel from rocprofv3 --pmc csv
-output (one or more pass directories).  Writes profiles/roofline_pmc.json.
+"""Per-kernel PMC summary from rocprofv3 --pmc csv passes (tools/pmc_pass.sh).
 
-    python tools/pmc_summary.py OUT.json DIR [DIR ...]
+    python tools/pmc_summary.py OUT.json DIR [DIR ...] [--op NAME]
 
-HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (KiB units -> bytes): on gfx950
-FETCH_SIZE counts half of the bytes of wide coalesced reads
-(MI355X_MICROARCH.md, HBM section)."""
+Kernels are grouped by (short name, grid); per group: launches and the mean
+per-launch counters.  HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes):
+on gfx950 FETCH_SIZE counts half of the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM section).  SQ_VALU_MFMA_BUSY_CYCLES is summed over
+the chip; mfma_busy_frac = it / (SQ_BUSY_CYCLES * 4 SIMDs * ... ) is not
+derived here (no gfx950 derived-counter formulas ship with ROCm 7.2): the raw
+per-launch values are kept.  With --op NAME (the bench's dominant op class),
+hbm_bytes_per_launch of the whole op (all of its kernels per op launch) is
+also written for bench.py's roofline ``traffic``."""
 
 import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
-KERNEL = "gemm_kernel<unsigned short, 128, 128, hvit::LdDense<unsigned short, true>, hvit::LdDense<unsigned short, true>, 3"
+
+def short(name):
+    name = re.sub(r"\(.*", "", name).replace("void ", "").replace("hvit::", "").replace("unsigned short", "bf16")
+    return name[:150]
 
 
 def main():
-    out, dirs = sys.argv[1], sys.argv[2:]
-    vals = defaultdict(list)
+    argv = sys.argv[1:]
+    op = None
+    if "--op" in argv:
+        i = argv.index("--op")
+        op = argv[i + 1]
+        argv = argv[:i] + argv[i + 2:]
+    out, dirs = argv[0], argv[1:]
+    vals = defaultdict(lambda: defaultdict(list))
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if KERNEL not in r["Kernel_Name"]:
-                    continue
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    res = {k: sum(v) / len(v) for k, v in vals.items()}
-    summary = {"kernel": KERNEL + " (fc1: M=8192 N=2048 K=512, GELU_DUAL + dropout epilogue)",
-               "launches": {k: len(v) for k, v in vals.items()}, "counters_mean_per_launch": res}
-    if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
-        summary["hbm_bytes_per_launch"] = round((2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024)
-        summary["algorithmic_bytes_per_launch"] = 8192 * 512 * 2 + 2048 * 512 * 2 + 2 * 8192 * 2048 * 2 + 2048 * 4
+                g = f"{r.get('Grid_Size', r.get('Grid_Size_X', '?'))}"
+                key = f"{short(r['Kernel_Name'])} grid={g}"
+                vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    kernels = {}
+    for k, cs in vals.items():
+        mean = {c: sum(v) / len(v) for c, v in cs.items()}
+        row = {"launches": max(len(v) for v in cs.values()), "counters_mean_per_launch": mean}
+        if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+            row["hbm_bytes_per_launch"] = round((2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024)
+        kernels[k] = row
+    summary = {"kernels": dict(sorted(kernels.items(), key=lambda kv: -kv[1].get("hbm_bytes_per_launch", 0)))}
+    if op:
+        # the roofline loop's op = one split-K GEMM + its slab reduction per launch
+        mine = {k: r for k, r in kernels.items() if k.startswith("gemm_kernel") or k.startswith("sum_slabs")}
+        tot = sum(r.get("hbm_bytes_per_launch", 0) * r["launches"] for r in mine.values())
+        nops = sum(r["launches"] for k, r in mine.items() if k.startswith("gemm_kernel"))
+        summary["op"] = op
+        summary["hbm_bytes_per_launch"] = round(tot / max(nops, 1))
     with open(out, "w") as f:
         json.dump(summary, f, indent=1)
-    print(json.dumps(summary, indent=1))
+    print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in kernels.items()}, indent=1))
 
 
 if __name__ == "__main__":
