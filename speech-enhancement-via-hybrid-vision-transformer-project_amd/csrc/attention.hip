@@ -554,8 +554,14 @@ __device__ __forceinline__ f32x4 v2_mma32(u32x4 a, u32x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, a), __builtin_bit_cast(s16x8, b), c, 0,
                                                  0, 0);
 }
-__device__ __forceinline__ f32x4 v2_mma16(v4s_t a, v4s_t b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+// 16x16x32 operand from two transposed 4-row reads (tiles jj and jj + 1):
+// k = 8g + e  <->  row 16*(jj + e/4) + 4g + e%4
+__device__ __forceinline__ u32x4 v2_cat(v4s_t lo, v4s_t hi) {
+  const uint2 a = __builtin_bit_cast(uint2, lo), b = __builtin_bit_cast(uint2, hi);
+  return (u32x4){a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ u32x4 v2_trj2(const char* img, const V2Lane& L, int jj, int t) {
+  return v2_cat(v2_trj(img, L, jj, t), v2_trj(img, L, jj + 1, t));
 }
 __device__ __forceinline__ v4s_t v2_pack(f32x4 v) {
   uint2 u;
@@ -594,13 +600,14 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
   const int NK = (N + 15) & ~15;
   const int nkt = NK >> 4;
+  const int NK32 = (N + 31) & ~31;  // staged rows: whole tile pairs
   const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;  // this lane's query
   u32x4 qf[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
     qf[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
-  v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK);
-  v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK);
+  v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK32);
+  v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK32);
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
   // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q), log2 units
@@ -639,18 +646,25 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   sum += __shfl_xor(sum, 32, 64);
   const float inv = 1.f / sum;
   const uint64_t bh = (uint64_t)b * H + h;
-  // O^T[d][q] += V^T[d][keys] P^T[keys][q]   (4 d-blocks of 16)
+  // O^T[d][q] += V^T[d][keys] P^T[keys][q]   (4 d-blocks of 16), two key tiles
+  // per 16x16x32 MFMA: the B operand is this lane's P of tiles 2jp, 2jp + 1
+  // (keys 16(2jp + e/4) + 4fq + e%4), the A operand the matching transposed
+  // reads of V.  A missing odd tile is P = 0 against staged (finite) V rows.
   f32x4 ot[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < V2_KMAX / 16; ++j) {
-    if (j < nkt) {
-      f32x4 p = st[j] * inv;
-      if (thr) p *= v2_keep(bh, N, q < N ? q : 0, 16 * j + 4 * fq, thr, dscale, seed, site);
-      const v4s_t pb = v2_pack(p);
+  for (int jp = 0; jp < V2_KMAX / 32; ++jp) {
+    if (2 * jp < nkt) {
+      f32x4 p0 = st[2 * jp] * inv;
+      f32x4 p1 = (2 * jp + 1 < nkt) ? st[2 * jp + 1] * inv : (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (thr) {
+        p0 *= v2_keep(bh, N, q < N ? q : 0, 32 * jp + 4 * fq, thr, dscale, seed, site);
+        if (2 * jp + 1 < nkt) p1 *= v2_keep(bh, N, q < N ? q : 0, 32 * jp + 16 + 4 * fq, thr, dscale, seed, site);
+      }
+      const u32x4 pb = v2_cat(v2_pack(p0), v2_pack(p1));
 #pragma unroll
-      for (int t = 0; t < 4; ++t) ot[t] = v2_mma16(v2_trj(Vs, LN, j, t), pb, ot[t]);
+      for (int t = 0; t < 4; ++t) ot[t] = v2_mma32(v2_trj2(Vs, LN, 2 * jp, t), pb, ot[t]);
     }
   }
   if (q < N) {
@@ -709,32 +723,39 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
   dl += __shfl_xor(dl, 32, 64);
   if (qv && fq == 0) delta[bh * N + q] = dl;
   const float lse2 = qv ? lse[bh * N + q] * 1.4426950408889634f : 0.f;
-  v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK);
-  v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK);
+  const int NK32 = (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite, P = 0)
+  v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK32);
+  v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK32);
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
   f32x4 dq[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dq[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int j = 0; j < nkt; ++j) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
-    s = v2_mma32(v2_fragj(Ks, LN, j, 0), qf[0], s);
-    s = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], s);
-    dp = v2_mma32(v2_fragj(Vs, LN, j, 0), df[0], dp);
-    dp = v2_mma32(v2_fragj(Vs, LN, j, 1), df[1], dp);
-    const f32x4 keep = thr ? v2_keep(bh, N, qv ? q : 0, 16 * j + 4 * fq, thr, dscale, seed, site)
-                           : (f32x4){1.f, 1.f, 1.f, 1.f};
-    f32x4 ds;
+  // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q]: two key tiles per 16x16x32 MFMA
+#pragma unroll 2
+  for (int j0 = 0; j0 < nkt; j0 += 2) {
+    f32x4 ds2[2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool valid = qv && (16 * j + 4 * fq + r < N);
-      const float p = valid ? exp2f(s[r] * c2 - lse2) : 0.f;
-      ds[r] = p * (dp[r] * keep[r] - dl);
+    for (int u = 0; u < 2; ++u) {
+      const int j = j0 + u;
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+      s = v2_mma32(v2_fragj(Ks, LN, j, 0), qf[0], s);
+      s = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], s);
+      dp = v2_mma32(v2_fragj(Vs, LN, j, 0), df[0], dp);
+      dp = v2_mma32(v2_fragj(Vs, LN, j, 1), df[1], dp);
+      const f32x4 keep = thr ? v2_keep(bh, N, qv ? q : 0, (16 * j + 4 * fq) < N ? 16 * j + 4 * fq : 0, thr,
+                                       dscale, seed, site)
+                             : (f32x4){1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = qv && (16 * j + 4 * fq + r < N);
+        const float p = valid ? exp2f(s[r] * c2 - lse2) : 0.f;
+        ds2[u][r] = p * (dp[r] * keep[r] - dl);
+      }
     }
-    const v4s_t db = v2_pack(ds);
+    const u32x4 db = v2_cat(v2_pack(ds2[0]), v2_pack(ds2[1]));
 #pragma unroll
-    for (int t = 0; t < 4; ++t) dq[t] = v2_mma16(v2_trj(Ks, LN, j, t), db, dq[t]);
+    for (int t = 0; t < 4; ++t) dq[t] = v2_mma32(v2_trj2(Ks, LN, j0, t), db, dq[t]);
   }
   if (qv) {
     bf16_t* dp_out = dqkv + ((long)b * N + q) * pitch + h * 64;
@@ -780,9 +801,10 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
     kf[s2] = kv ? *(const u32x4*)(base + D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
     vf[s2] = kv ? *(const u32x4*)(base + 2 * D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
   }
-  v2_stage_glds<WAVES>(Qs, base, pitch, N, NQ);
-  v2_stage_glds<WAVES>(Ds, dout + (long)b * N * D + h * 64, D, N, NQ);
-  for (int i = threadIdx.x; i < NQ; i += WAVES * 64) {
+  const int NQ32 = (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite, P = 0)
+  v2_stage_glds<WAVES>(Qs, base, pitch, N, NQ32);
+  v2_stage_glds<WAVES>(Ds, dout + (long)b * N * D + h * 64, D, N, NQ32);
+  for (int i = threadIdx.x; i < NQ32; i += WAVES * 64) {
     Ls[i] = i < N ? lse[bh * N + i] * 1.4426950408889634f : 0.f;
     Dl[i] = i < N ? delta[bh * N + i] : 0.f;
   }
@@ -793,46 +815,52 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
 #pragma unroll
   for (int t = 0; t < 4; ++t) dkt[t] = dvt[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-  for (int j = 0; j < nqt; ++j) {
-    // S^T-free form: S[q][key] with m = queries 16j + 4fq + r, n = key (lane)
-    f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
-    s = v2_mma32(v2_fragj(Qs, LN, j, 0), kf[0], s);
-    s = v2_mma32(v2_fragj(Qs, LN, j, 1), kf[1], s);
-    dp = v2_mma32(v2_fragj(Ds, LN, j, 0), vf[0], dp);
-    dp = v2_mma32(v2_fragj(Ds, LN, j, 1), vf[1], dp);
-    // dropout: lane (quad position c = key & 3) hashes query row 16j+4fq+c of
-    // its key group; the quad exchanges the 16-bit slices (4 queries x 4 keys)
-    uint32_t hlo = 0u, hhi = 0u;
-    if (thr) {
-      const int qc = 16 * j + 4 * fq + (frow & 3);
-      const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
-      const uint64_t hv = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
-      hlo = (uint32_t)hv;
-      hhi = (uint32_t)(hv >> 32);
-    }
-    f32x4 pd, ds;
+  for (int j0 = 0; j0 < nqt; j0 += 2) {
+    f32x4 pd2[2], ds2[2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qi = 16 * j + 4 * fq + r;
-      const bool valid = kv && qi < N;
-      const float p = valid ? exp2f(s[r] * c2 - Ls[qi]) : 0.f;
-      float kp = 1.f;
+    for (int u = 0; u < 2; ++u) {
+      const int j = j0 + u;
+      // S^T-free form: S[q][key] with m = queries 16j + 4fq + r, n = key (lane)
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+      s = v2_mma32(v2_fragj(Qs, LN, j, 0), kf[0], s);
+      s = v2_mma32(v2_fragj(Qs, LN, j, 1), kf[1], s);
+      dp = v2_mma32(v2_fragj(Ds, LN, j, 0), vf[0], dp);
+      dp = v2_mma32(v2_fragj(Ds, LN, j, 1), vf[1], dp);
+      // dropout: lane (quad position c = key & 3) hashes query row 16j+4fq+c of
+      // its key group; the quad exchanges the 16-bit slices (4 queries x 4 keys)
+      uint32_t hlo = 0u, hhi = 0u;
       if (thr) {
-        const int src = (lane & ~3) | r;
-        const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
-        const uint32_t word = (key & 2) ? hi : lo;
-        const uint32_t u16 = (key & 1) ? (word >> 16) : (word & 0xffffu);
-        kp = (valid && u16 >= thr) ? dscale : 0.f;
+        const int qc = 16 * j + 4 * fq + (frow & 3);
+        const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
+        const uint64_t hv = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
+        hlo = (uint32_t)hv;
+        hhi = (uint32_t)(hv >> 32);
       }
-      pd[r] = p * kp;
-      ds[r] = p * (dp[r] * kp - Dl[qi]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = 16 * j + 4 * fq + r;
+        const bool valid = kv && qi < N;
+        const float p = valid ? exp2f(s[r] * c2 - Ls[qi]) : 0.f;
+        float kp = 1.f;
+        if (thr) {
+          const int src = (lane & ~3) | r;
+          const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
+          const uint32_t word = (key & 2) ? hi : lo;
+          const uint32_t u16 = (key & 1) ? (word >> 16) : (word & 0xffffu);
+          kp = (valid && u16 >= thr) ? dscale : 0.f;
+        }
+        pd2[u][r] = p * kp;
+        ds2[u][r] = p * (dp[r] * kp - Dl[qi]);
+      }
     }
     // dV^T[d][key] += dO^T[d][q] P~[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
-    const v4s_t pb = v2_pack(pd), sb = v2_pack(ds);
+    // (two query tiles per 16x16x32 MFMA)
+    const u32x4 pb = v2_cat(v2_pack(pd2[0]), v2_pack(pd2[1]));
+    const u32x4 sb = v2_cat(v2_pack(ds2[0]), v2_pack(ds2[1]));
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      dvt[t] = v2_mma16(v2_trj(Ds, LN, j, t), pb, dvt[t]);
-      dkt[t] = v2_mma16(v2_trj(Qs, LN, j, t), sb, dkt[t]);
+      dvt[t] = v2_mma32(v2_trj2(Ds, LN, j0, t), pb, dvt[t]);
+      dkt[t] = v2_mma32(v2_trj2(Qs, LN, j0, t), sb, dkt[t]);
     }
   }
   if (kv) {

@@ -370,6 +370,7 @@ struct Epi {
   float* rs_ptr = nullptr;  // row sums of the A operand (wgrad bias grad): rs_ptr[z * rs_stride + m]
   long rs_stride = 0;
   bool vec_ok = false;      // N % 4 == 0, every operand 16-B aligned with ld % 4 == 0
+  int xcd_remap = 1;        // XCD-aware block order (see tile_of); 0 = hardware order
   // EPI_PATCH: m = token (b, py, px) of Hp x Wp, n = (ky*P + kx)*C + c
   int pP = 0, pC = 0, pHp = 0, pWp = 0, pH = 0, pW = 0;
 };
@@ -785,6 +786,32 @@ extern __device__ unsigned long long g_gemm_stamps[65536 * 4];
 #ifndef HVIT_BIG_OCC
 #define HVIT_BIG_OCC 2
 #endif
+// XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs
+// (block b and b + 8 share one XCD's 4 MiB L2), so in hardware order every
+// XCD sees tiles from all over the output and re-fetches the same A rows / B
+// columns from HBM.  Here the hardware block b is given logical tile
+// base(b % 8) + b / 8: each XCD owns one contiguous range of the logical order
+// (split-K slice major, then M tiles, N tiles fastest), i.e. a compact block of
+// output tiles of one K slice whose operand panels stay L2-resident.  The
+// mapping is a bijection for any grid size (q = nwg / 8 blocks per XCD, the
+// first nwg % 8 XCDs one more).
+struct TileId {
+  int mt, nt, z;
+};
+__device__ __forceinline__ TileId tile_of(int remap) {
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  if (!remap) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const int nwg = gx * gy * gz;
+  const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xcd = b & 7, slot = b >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  const int per = gx * gy;
+  const int z = lid / per, rem = lid - z * per;
+  const int mt = rem / gy;
+  return {mt, rem - mt * gy, z};
+}
+
 template <typename T, int BM, int BN, class LA, class LB, int EK, bool RS = false>
 __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
                                                                                             int K, int kps, Epi ep) {
@@ -798,9 +825,10 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * kps;
+  const TileId tid3 = tile_of(ep.xcd_remap);
+  const int m0 = tid3.mt * BM;
+  const int n0 = tid3.nt * BN;
+  const int kbeg = tid3.z * kps;
   const int kend = min(K, kbeg + kps);
   const int frow = lane & 15, fq = lane >> 4;
 
@@ -845,7 +873,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
   GEMM_STAMP(0);
   const bool interior = m0 + BM <= M && n0 + BN <= N && ((kend - kbeg) % C::BK) == 0 && la.fast() && lb.fast();
   float rsacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bool rs_on = RS && blockIdx.y == 0;
+  const bool rs_on = RS && tid3.nt == 0;
   if (interior) C::template run<false, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
   else C::template run<true, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
   if constexpr (RS) {
@@ -858,7 +886,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
       if (tid < BM && m0 + tid < M) {
         float sum = 0.f;
         for (int k = 0; k < C::RS_KG; ++k) sum += red[k * BM + tid];
-        ep.rs_ptr[(long)blockIdx.z * ep.rs_stride + m0 + tid] = sum;
+        ep.rs_ptr[(long)tid3.z * ep.rs_stride + m0 + tid] = sum;
       }
       __syncthreads();
     }
@@ -909,7 +937,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
           const int m = mbase + row;
           if (PRED && (m >= M || !nok)) continue;
           const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
-          float* slab = (float*)ep.out + (long)blockIdx.z * ep.slab_stride + (long)m * ep.ldo + n;
+          float* slab = (float*)ep.out + (long)tid3.z * ep.slab_stride + (long)m * ep.ldo + n;
           if (!PRED || (full && (ep.ldo & 3) == 0)) *(f32x4*)slab = v;
           else store4_slow(slab, 0, v, nv, HVIT_F32);
         }
@@ -1119,6 +1147,8 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
                 int force_tile = 0) {
   Epi ep = ep_in;
   if (ep.slab_stride == 0) ep.slab_stride = (long)M * ep.ldo;
+  static const int remap = getenv("HVIT_XCD_REMAP") ? atoi(getenv("HVIT_XCD_REMAP")) : 1;  // A/B only
+  ep.xcd_remap = remap;
   auto vok = [](const void* p, long ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
   ep.vec_ok = N % 4 == 0 && vok(ep.out, ep.ldo) && vok(ep.out2, ep.ldo2) && vok(ep.aux, ep.ldaux) &&
               vok(ep.resid, ep.ldr) && vok(ep.rowadd, ep.rowadd_ld);

@@ -67,6 +67,10 @@ int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64) {
   const long target = bm * bn <= 64 * 64 ? 512 : big;
   long want = (target + tiles - 1) / tiles;
   long maxs = K / (4 * bk);
+  // a multiple of 8 slices: with the XCD-aware tile order (gemm.h tile_of)
+  // each XCD then reduces whole K slices, whose operand rows stay in its L2
+  static const bool split8 = !getenv("HVIT_SPLIT8") || atoi(getenv("HVIT_SPLIT8"));  // A/B only
+  if (split8 && want > 4 && maxs >= 8) want = std::min((want + 7) / 8 * 8, maxs / 8 * 8);
   if (want > maxs) want = maxs;
   if (want > 256) want = 256;
   if (want < 1) want = 1;

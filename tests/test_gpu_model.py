@@ -19,17 +19,20 @@ LARGE = dict(embed_dim=768, num_heads=12, num_layers=12)   # BASELINE config 5 a
 
 
 def grad_tol(name, key):
-    """Relative-L2 bar for a parameter gradient.  f32 gradients that pass
-    through train-mode BN + ReLU + max-pool backward are ill-conditioned:
-    argmax / ReLU-mask routing flips on 1e-7 forward differences.  Measured
-    (tools/diag_dump.py, default_clip): a 1e-7 relative input perturbation of
-    the same build moves the encoder conv weight grads by 3e-3 relative L2.
-    So the conv/BN/skip parameters of the 28M-parameter configs get 3e-2;
-    every ViT, patch-embedding, positional and head gradient (no routing
-    discontinuity on their own path) and every tiny-config gradient 5e-3."""
-    if name.startswith("tiny"):
-        return 5e-3
-    return 3e-2 if key.split(".")[0] in ("encoder", "decoder", "skip_projections") else 5e-3
+    """Relative-L2 bar for a parameter gradient of a whole-model train step.
+
+    fp32 gradients of the 28M-parameter configs are ill-conditioned through
+    the BatchNorm + ReLU (+ max-pool) stages: one ReLU whose input is within
+    the forward's 1e-6 rounding difference of zero flips its mask and moves the
+    gradient by ~1/sqrt(elements) of the routed tensor.  Measured
+    (tools/grad_trace.py): the gradient w.r.t. the decoder-2 block output
+    agrees with the oracle to 1.6e-6, the gradient w.r.t. the decoder-1 output
+    (after decoder-2's ReLU routing) to 4e-3 (default_256) / 1.2e-2
+    (default_clip), and every upstream gradient (ViT, patch embedding, encoder)
+    inherits that.  So the whole-model bars are 3e-2 on the 28M configs, 5e-3
+    on the tiny ones; the ViT backward is pinned separately, with the same
+    upstream gradient on both sides, at 1e-4 (test_vit_backward_isolated)."""
+    return 5e-3 if name.startswith("tiny") else 3e-2
 
 
 def rel(a, b):
@@ -259,3 +262,49 @@ def test_batch32_train_step_bf16_vs_oracle_loss(hv):
     assert abs(loss.item() - lo) < 2e-2 * abs(lo)
     for k, p in m.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+@pytest.mark.parametrize("kw", [{}, LARGE], ids=["default", "large"])
+def test_vit_backward_isolated(hv, kw):
+    """The transformer path alone (pos-embed add, every ViT block, final
+    LayerNorm, to_feature_map; hybrid_vit.py:309-350, attention.py:176-300) in
+    fp32 train mode with dropout off, driven by the SAME upstream gradient on
+    the HIP side (forward_transformer) and the oracle side: no ReLU routing
+    upstream, so every ViT / head / pos-embed gradient and the token gradient
+    are pinned at 1e-4 relative L2."""
+    import torch.nn.functional as F
+    cfg = O.HViTConfig(**kw)
+    cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
+    shapes = O.state_dict_shapes(cfg)
+    W = CF.weights(shapes)
+    D, C, B, Hp, Wp = cfg.embed_dim, cfg.encoder_channels[-1], 2, 16, 16
+    gen = torch.Generator().manual_seed(21)
+    tok = torch.randn(B, Hp * Wp, D, generator=gen)
+    G = torch.randn(B, C, Hp, Wp, generator=gen)
+    m = build(hv, kw, "fp32", True).train()
+    tk = tok.cuda().requires_grad_(True)
+    out = m.forward_transformer(tk, (Hp, Wp))
+    (out * G.cuda()).sum().backward()
+    sd = O.make_state(shapes, W, requires_grad=True)
+    to = tok.clone().requires_grad_(True)
+    t = to + sd["pos_encoding.pos_embed"][:, :Hp * Wp]
+    dpr = [v.item() for v in torch.linspace(0, cfg.drop_path_rate, cfg.num_layers)]
+    for l in range(cfg.num_layers):
+        t, _ = O.vit_block(sd, f"transformer.blocks.{l}", t, cfg, dpr[l], True)
+    t = F.layer_norm(t, (D,), sd["transformer.norm.weight"], sd["transformer.norm.bias"], 1e-5)
+    f = F.linear(t, sd["to_feature_map.weight"], sd["to_feature_map.bias"])
+    ref = f.transpose(1, 2).reshape(B, C, Hp, Wp)
+    (ref * G).sum().backward()
+    assert rel(out.detach().cpu(), ref.detach()) < 1e-5
+    assert relnorm(tk.grad.cpu(), to.grad) < 1e-4
+    n = 0
+    for k, p in m.named_parameters():
+        if not (k.startswith("transformer") or k.startswith("to_feature_map") or k.startswith("pos_encoding")):
+            continue
+        r = sd[k].grad
+        got = p.grad.detach().cpu()
+        if k == "pos_encoding.pos_embed":
+            got, r = got[:, :Hp * Wp], r[:, :Hp * Wp]
+        assert relnorm(got, r) < 1e-4, k
+        n += 1
+    assert n == 12 * cfg.num_layers + 5

@@ -5,7 +5,7 @@
 GradScaler.scale / unscale_ / step / update, torch.nn.utils.clip_grad_norm_,
 gradient accumulation, optimizer.zero_grad(), a CosineAnnealingLR scheduler,
 then the Trainer checkpoint dict saved with torch.save and restored into fresh
-objects, which must continue bit-identically."""
+objects, which must continue identically (to float-atomic rounding)."""
 
 import copy
 import io
@@ -61,7 +61,8 @@ def test_trainer_loop_amp_scaler_accum_checkpoint(hv):
     losses = _train_steps(m, opt, sched, scaler, crit, _batches(4, 1))
     assert all(torch.isfinite(torch.tensor(losses)))
     moved = [k for k, v in m.state_dict().items() if v.is_floating_point() and not torch.equal(v, before[k])]
-    assert len(moved) > 100  # parameters and BN running stats all updated
+    still = [k for k, v in m.state_dict().items() if v.is_floating_point() and k not in moved]
+    assert not still, (scaler.get_scale(), still)  # every parameter and BN running statistic updated
     assert set(m.state_dict()) == set(before)
     assert all(float(opt.state[p]["step"]) == 2.0 for p in m.parameters())  # 4 micro-batches / accum 2
     assert opt.param_groups[0]["lr"] < 1e-3  # scheduler stepped
