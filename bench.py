@@ -43,17 +43,22 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 32; 16 for --variant large)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--mode", default="train", choices=["train", "infer"],
                     help="infer: BASELINE config 2 (forward only, eval, no grad)")
     ap.add_argument("--variant", default="default", choices=["default", "large"],
-                    help="large: BASELINE config 5 shape (D=768, 12 heads, 12 layers; bf16, not fp8)")
+                    help="large: BASELINE config 5 shape (D=768, 12 heads, 12 layers)")
+    ap.add_argument("--attn", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: e4m3 MFMA attention forward (BASELINE config 5), bf16 attention backward")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing loop (used for rocprofv3 --pmc passes)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 16 if a.variant == "large" else 32
+    return a
 
 
 PEAKS = {"mfma": (PEAK_BF16_TFLOPS, "TFLOP/s", 1e12), "hbm": (PEAK_HBM_GBS, "GB/s", 1e9)}
@@ -200,7 +205,8 @@ def main():
 
     torch.manual_seed(1234)
     arch = dict(embed_dim=768, num_heads=12, num_layers=12) if args.variant == "large" else {}
-    model = hv.HybridViT(precision=args.precision, **arch).cuda().train()
+    model = hv.HybridViT(precision=args.precision, attention_precision="fp8" if args.attn == "fp8" else None,
+                         **arch).cuda().train()
     reducer = None
     if world > 1:
         broadcast_module(model)
@@ -286,7 +292,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.precision,
+            "dtype": args.precision + ("+fp8-attention" if args.attn == "fp8" else ""),
             "data": "synthetic (harmonic+noise 16 kHz waveforms, host STFT 512/128 hann, min-max, 256x256)",
             "config": {"workload": (("HybridViT default (enc 64/128/256, 6x8-head d512 ViT, dec 256/128/64/1)"
                                      if args.variant == "default" else

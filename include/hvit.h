@@ -128,6 +128,14 @@ int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int hd, float sc
                   const hvit_dropout_t* dropout, void* o, float* lse, float* probs, void* stream);
 int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
                   int hd, float scale, const hvit_dropout_t* dropout, void* dqkv, float* delta_ws, void* stream);
+/* fp8 (OCP e4m3) forward of the same core for BASELINE config 5: bf16 qkv / o,
+ * per-(b, h) power-of-two scales for K and V and per-query scales for Q
+ * (e4m3 range from the absolute maxima), QK^T on v_mfma_f32_16x16x32_fp8_fp8,
+ * PV on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4.  hd = 64, N <= 256.
+ * The dropout mask and lse match hvit_mhsa_fwd's, so hvit_mhsa_bwd (bf16) is
+ * its backward. */
+int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
+                      void* o, float* lse, void* stream);
 
 /* ---- LayerNorm eps (attention.py:152-153, :271): x f32 [M, D] -> y; saves
  * mean / rstd [M].  Backward: dx = resid + dLN (resid may be NULL or alias dx),

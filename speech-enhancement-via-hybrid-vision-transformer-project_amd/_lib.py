@@ -85,6 +85,7 @@ _SIGS = {
     "hvit_conv_weight_pack": ([vp, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_conv_weight_unpack": ([vp, i32, i32, i32, vp, vp], i32),
     "hvit_mhsa_fwd": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
+    "hvit_mhsa_fwd_fp8": ([vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_layernorm_fwd": ([vp, vp, vp, i32, i32, f32, vp, i32, vp, vp, vp], i32),
     "hvit_layernorm_bwd_ws_elems": ([i32, i32], i64),

@@ -879,8 +879,12 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
 }
 
 static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 && N <= V2_KMAX && N % 4 == 0; }
-// waves per v2 workgroup (HVIT_ATTN_WAVES = 4 / 8 / 16 overrides; A/B only)
-static int v2_waves() {
+// waves per v2 workgroup: 16 = all queries (keys) of a (b, h) in one
+// workgroup, K/V (Q/dO) staged once.  Measured: two 8-wave workgroups per
+// (b, h) are slower both at B*H = 256 (default, B=32) and at B*H = 192
+// (config 5, B=16: 20.6 -> 21.5 us per layer); HVIT_ATTN_WAVES = 4 / 8 / 16
+// overrides (A/B only)
+static int v2_waves(int) {
   static const int w = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
   return w;
 }
@@ -954,7 +958,7 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
     const hvit_dropout_t* dr = dropout;
     const uint32_t thr = dr ? drop_threshold(dr->p) : 0;
     const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-    const int wv = v2_waves();
+    const int wv = v2_waves(B * H);
     auto go = [&](auto kern, int waves) {
       hipLaunchKernelGGL(kern, dim3(cdiv(N, 16 * waves), H, B), dim3(64 * waves), 0, st, (const bf16_t*)qkv,
                          (bf16_t*)o, lse, N, H, scale, thr, ds, dr ? dr->seed : 0ull, dr ? dr->site : 0u);
@@ -991,7 +995,7 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
       hipLaunchKernelGGL(dkvk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
                          (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
     };
-    const int wv = v2_waves();
+    const int wv = v2_waves(B * H);
     if (wv == 16) go(mhsa_dq_v2<16>, mhsa_dkv_v2<16>, 16);
     else if (wv == 8) go(mhsa_dq_v2<8>, mhsa_dkv_v2<8>, 8);
     else go(mhsa_dq_v2<4>, mhsa_dkv_v2<4>, 4);

@@ -1,0 +1,253 @@
+// FP8 (OCP e4m3) multi-head self-attention forward for gfx950: the
+// "fp8 MFMA attention path" of BASELINE config 5 (D=768, 12 heads, hd 64),
+// restating MultiHeadSelfAttention's core (models/attention.py:91-107:
+// softmax(q k^T * scale) -> dropout -> @ v) with fp8 matrix operands.
+//
+// One workgroup per (b, h), 16 waves x 16 queries (N <= 256).  The head's K
+// and V are read once (bf16, the qkv Linear output in place), scaled by a
+// power of two chosen from their absolute maximum so that e4m3's range is
+// used (448 / amax, rounded down to 2^e), converted to e4m3 and staged in LDS:
+//   K   [key][64 d]  (80-B rows: conflict-free 8-byte fragment reads),
+//   V^T [d][256 keys] (264-B rows), keys >= N zero.
+// Each query row gets its own power-of-two scale the same way.
+//   S^T = K Q^T        v_mfma_f32_16x16x32_fp8_fp8 (2 per 16-key tile)
+//   softmax            f32, exactly as the bf16 kernel (running max, exp2)
+//   O^T = V^T P^T      v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3), one
+//                      per 128 keys and 16 d: twice the bf16 MFMA rate.  P in
+//                      [0, 1] is stored as 256 * P in e4m3 and the MFMA's
+//                      block scales undo both the P and the V scaling exactly
+//                      (E8M0 exponents).
+// The dropout mask is the bf16 kernel's (same hash, same indices), so the
+// backward -- bf16, recomputing P from the saved lse (FlashAttention-3's fp8
+// recipe: fp8 forward, bf16 backward) -- sees the forward's mask.
+#include "common.h"
+
+namespace hvit {
+namespace {
+
+constexpr int F8_KMAX = 256;
+constexpr int F8_KP = 80;         // K image row pitch (64 fp8 + 16 pad)
+constexpr int F8_VP = 256 + 8;    // V^T image row pitch (256 fp8 keys + 8 pad)
+constexpr float F8_MAX = 448.f;   // e4m3 largest finite
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float clamp8(float x) { return fminf(fmaxf(x, -F8_MAX), F8_MAX); }
+// 4 floats -> 4 e4m3 bytes (byte i = value i)
+__device__ __forceinline__ uint32_t f8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(clamp8(a), clamp8(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(clamp8(c), clamp8(d), w, true);
+  return (uint32_t)w;
+}
+// power-of-two exponent e with amax * 2^e <= 448 (0 for an all-zero block)
+__device__ __forceinline__ int pow2_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  const float r = F8_MAX / amax;
+  int e = (int)((__float_as_uint(r) >> 23) & 0xff) - 127;  // floor(log2(r)) for normal r
+  return e < -60 ? -60 : (e > 60 ? 60 : e);
+}
+__device__ __forceinline__ float exp2i(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+__device__ __forceinline__ float absmax8(const u32x4& u) {
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    m = fmaxf(m, fmaxf(fabsf(__uint_as_float(u[e] << 16)), fabsf(__uint_as_float(u[e] & 0xffff0000u))));
+  return m;
+}
+// 8 bf16 (u32x4) * s -> 8 e4m3 bytes
+__device__ __forceinline__ uint2 to_f8(const u32x4& u, float s) {
+  uint2 r;
+  r.x = f8x4(__uint_as_float(u[0] << 16) * s, __uint_as_float(u[0] & 0xffff0000u) * s,
+             __uint_as_float(u[1] << 16) * s, __uint_as_float(u[1] & 0xffff0000u) * s);
+  r.y = f8x4(__uint_as_float(u[2] << 16) * s, __uint_as_float(u[2] & 0xffff0000u) * s,
+             __uint_as_float(u[3] << 16) * s, __uint_as_float(u[3] & 0xffff0000u) * s);
+  return r;
+}
+// dropout multipliers of keys kj..kj+3 of query qi (the bf16 kernel's v2_keep)
+__device__ __forceinline__ f32x4 keep4q(uint64_t bh, int N, int qi, int kj, uint32_t thr, float dscale,
+                                       unsigned long long seed, uint32_t site) {
+  const uint64_t idx = (bh * N + qi) * (uint64_t)N + kj;
+  const uint64_t hv = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
+  f32x4 k;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) k[e] = ((uint32_t)(hv >> (16 * e)) & 0xffffu) >= thr ? dscale : 0.f;
+  return k;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* __restrict__ qkv,
+                                                                  bf16_t* __restrict__ o, float* __restrict__ lse,
+                                                                  int N, int H, float scale, uint32_t thr,
+                                                                  float dscale, unsigned long long seed,
+                                                                  uint32_t site) {
+  constexpr int NT = WAVES * 64;
+  constexpr int PER = F8_KMAX * 8 / NT;  // 16-byte chunks of K (and of V) per thread
+  __shared__ __attribute__((aligned(16))) char Ks[F8_KMAX * F8_KP];
+  __shared__ __attribute__((aligned(16))) char Vt[64 * F8_VP];
+  __shared__ float red[2][WAVES];
+  const int D = H * 64;
+  const long pitch = 3L * D;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+  const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
+  const uint64_t bh = (uint64_t)b * H + h;
+
+  // ---- K, V (bf16) -> registers, block absmax
+  u32x4 kr[PER], vr[PER];
+  float mk = 0.f, mv = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = tid + i * NT, key = c >> 3, dc = c & 7;
+    kr[i] = vr[i] = (u32x4){0u, 0u, 0u, 0u};
+    if (key < N) {
+      kr[i] = *(const u32x4*)(base + D + (long)key * pitch + dc * 8);
+      vr[i] = *(const u32x4*)(base + 2 * D + (long)key * pitch + dc * 8);
+    }
+    mk = fmaxf(mk, absmax8(kr[i]));
+    mv = fmaxf(mv, absmax8(vr[i]));
+  }
+  // this lane's query row (2 x 8 d per lane), its own scale
+  const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;
+  u32x4 qb[2];
+  float mq = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    qb[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+    mq = fmaxf(mq, absmax8(qb[s2]));
+  }
+  mq = fmaxf(mq, __shfl_xor(mq, 16, 64));
+  mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
+  mk = wave_max(mk);
+  mv = wave_max(mv);
+  if (lane == 0) {
+    red[0][w] = mk;
+    red[1][w] = mv;
+  }
+  __syncthreads();
+  mk = mv = 0.f;
+#pragma unroll
+  for (int i = 0; i < WAVES; ++i) {
+    mk = fmaxf(mk, red[0][i]);
+    mv = fmaxf(mv, red[1][i]);
+  }
+  const int ek = pow2_exp(mk), ev = pow2_exp(mv), eq = pow2_exp(mq);
+  const float sk = exp2i(ek), sv = exp2i(ev), sq = exp2i(eq);
+  // ---- e4m3 images: K row-major, V transposed (keys >= N are zero)
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = tid + i * NT, key = c >> 3, dc = c & 7;
+    *(uint2*)(Ks + key * F8_KP + dc * 8) = to_f8(kr[i], sk);
+    const uint2 v8 = to_f8(vr[i], sv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      Vt[(dc * 8 + e) * F8_VP + key] = (char)(((e < 4 ? v8.x : v8.y) >> (8 * (e & 3))) & 0xffu);
+  }
+  long q8[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) q8[s2] = __builtin_bit_cast(long, to_f8(qb[s2], sq));
+  __syncthreads();
+
+  const int nkt = (N + 15) >> 4;
+  // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q) in log2 units
+  const float c2 = scale * 1.4426950408889634f / (sq * sk);
+  f32x4 st[F8_KMAX / 16];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < F8_KMAX / 16; ++j) {
+    if (j < nkt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const long kf = *(const long*)(Ks + (16 * j + frow) * F8_KP + 32 * s2 + 8 * fq);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(kf, q8[s2], a, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = (16 * j + 4 * fq + r < N) ? a[r] * c2 : -INFINITY;
+        a[r] = v;
+        mx = fmaxf(mx, v);
+      }
+      st[j] = a;
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < F8_KMAX / 16; ++j) {
+    if (j < nkt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(st[j][r] - mx);
+        st[j][r] = p;
+        sum += p;
+      }
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  // O^T[d][q] = V^T[d][keys] (256 P^T[keys][q]) per 128-key block; lane (q, g)
+  // supplies keys 128kb + 16m + 4g + r (m = 0..7, r = 0..3) for both operands
+  f32x4 ot[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int qq = q < N ? q : 0;
+#pragma unroll
+  for (int kb = 0; kb < F8_KMAX / 128; ++kb) {
+    if (128 * kb < N) {
+      i32x8 pb;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int j = 8 * kb + m;
+        f32x4 p = (j < nkt) ? st[j] * 256.f : (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (thr && j < nkt) p *= keep4q(bh, N, qq, 16 * j + 4 * fq, thr, dscale, seed, site);
+        pb[m] = (int)f8x4(p[0], p[1], p[2], p[3]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const char* vrow = Vt + (16 * t + frow) * F8_VP + 128 * kb + 4 * fq;
+        i32x8 va;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) va[m] = *(const int*)(vrow + 16 * m);
+        // scale_a = 2^-ev (undo V's scale), scale_b = 2^-8 (undo 256 P)
+        ot[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(va, pb, ot[t], 0, 0, 0, 127 - ev, 0, 127 - 8);
+      }
+    }
+  }
+  if (q < N) {
+    bf16_t* op = o + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint2 u;
+      u.x = f2bf2(ot[t][0] * inv, ot[t][1] * inv);
+      u.y = f2bf2(ot[t][2] * inv, ot[t][3] * inv);
+      *(uint2*)(op + 16 * t + 4 * fq) = u;
+    }
+    if (fq == 0) lse[bh * N + q] = (mx + log2f(sum)) * 0.6931471805599453f;
+  }
+}
+
+}  // namespace
+}  // namespace hvit
+
+using namespace hvit;
+
+extern "C" int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, float scale,
+                                 const hvit_dropout_t* dropout, void* o, float* lse, void* stream) {
+  HVIT_CHECK(qkv && o && lse, "hvit_mhsa_fwd_fp8: null pointer");
+  HVIT_CHECK(B > 0 && N > 0 && H > 0, "hvit_mhsa_fwd_fp8: bad shape B=%d N=%d H=%d", B, N, H);
+  HVIT_CHECK(hd == 64, "hvit_mhsa_fwd_fp8: head_dim %d unsupported (64)", hd);
+  HVIT_CHECK(N <= F8_KMAX, "hvit_mhsa_fwd_fp8: N=%d exceeds %d tokens", N, F8_KMAX);
+  HVIT_CHECK(aligned16(qkv) && aligned16(o), "hvit_mhsa_fwd_fp8: qkv/o must be 16-byte aligned");
+  const uint32_t thr = dropout ? drop_threshold(dropout->p) : 0;
+  const float ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
+  // one 16-wave workgroup per (b, h) (measured faster than two 8-wave ones at
+  // config 5's B*H = 192: 24.4 vs 26.4 us per layer)
+  constexpr int WAVES = 16;
+  hipLaunchKernelGGL(mhsa_fwd_fp8_kernel<WAVES>, dim3(cdiv(N, 16 * WAVES), H, B), dim3(64 * WAVES), 0,
+                     (hipStream_t)stream, (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds,
+                     dropout ? dropout->seed : 0ull, dropout ? dropout->site : 0u);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}

@@ -486,7 +486,7 @@ class ViTBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, H, drops, dpr, training,
-                dt, want_probs):
+                dt, want_probs, attn_fp8=False):
         B, Nt, D = x.shape
         M = B * Nt
         hd = D // H
@@ -507,9 +507,18 @@ class ViTBlockFn(torch.autograd.Function):
         o = _empty((M, D), dt, dev)
         lse = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         probs = torch.empty((B, H, Nt, Nt), dtype=torch.float32, device=dev) if want_probs else None
-        with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
-            call("hvit_mhsa_fwd", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(), lse.data_ptr(),
-                 ptr(probs), s)
+        if attn_fp8 and not want_probs:
+            # fp8 (e4m3) QK^T / PV forward (BASELINE config 5); the backward
+            # below is the bf16 kernel, recomputing P from this lse
+            if dt != BF16:
+                raise ValueError("hvit: the fp8 attention path runs inside the bf16 model (precision='bf16')")
+            with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
+                call("hvit_mhsa_fwd_fp8", qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
+                     lse.data_ptr(), s)
+        else:
+            with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
+                call("hvit_mhsa_fwd", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
+                     lse.data_ptr(), ptr(probs), s)
         Wp = cast(pw, dt)
         x1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_fwd", 2.0 * M * D * D):
@@ -588,7 +597,7 @@ class ViTBlockFn(torch.autograd.Function):
                  s)
         dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 class HeadFn(torch.autograd.Function):

@@ -14,7 +14,10 @@ Precision: ``precision="fp32"`` runs the exact-f32 MFMA path (parity with the
 reference within 1e-3 rel); ``"bf16"`` runs bf16 MFMA with f32 accumulation, f32
 residual stream / statistics / weight gradients; ``"auto"`` (default) picks bf16
 inside a CUDA autocast region (the reference's trainer.py:148 AMP context) and
-fp32 otherwise.
+fp32 otherwise.  ``attention_precision="fp8"`` (an extra keyword; the
+reference's keywords and defaults are unchanged) runs the attention forward of
+the bf16 path on e4m3 MFMAs (BASELINE config 5, csrc/attention_fp8.hip) with
+the bf16 attention backward.
 """
 
 from __future__ import annotations
@@ -223,6 +226,7 @@ class HybridViT(nn.Module):
         use_skip_connections: bool = True,
         use_cls_token: bool = False,
         precision: str = "auto",
+        attention_precision: Optional[str] = None,
     ):
         super().__init__()
         if use_cls_token:
@@ -237,6 +241,11 @@ class HybridViT(nn.Module):
         self.num_heads = num_heads
         self.dropout_p = dropout
         self.precision = precision
+        if attention_precision not in (None, "fp8"):
+            raise ValueError(f"hvit: attention_precision must be None or 'fp8', got {attention_precision!r}")
+        # "fp8": e4m3 QK^T / PV MFMAs in the attention forward of the bf16 path
+        # (BASELINE config 5); the attention backward stays bf16
+        self.attention_precision = attention_precision
         self.last_num_tokens = 0  # patch tokens N of the latest forward (dp.GradAllReducer checks it)
 
         self.encoder = nn.ModuleList()
@@ -369,7 +378,8 @@ class HybridViT(nn.Module):
             t, probs = HF.ViTBlockFn.apply(t, blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias,
                                            a.proj.weight, a.proj.bias, blk.norm2.weight, blk.norm2.bias,
                                            m[0].weight, m[0].bias, m[3].weight, m[3].bias, a.num_heads, drops,
-                                           blk.dpr, self.training, dt, want_attn)
+                                           blk.dpr, self.training, dt, want_attn,
+                                           self.attention_precision == "fp8" and dt == L.BF16)
             attns.append(probs)
         return t, attns
 

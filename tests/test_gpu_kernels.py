@@ -531,3 +531,84 @@ def test_vit_block_droppath_matches_torch(hv):
     assert rel(x.grad, xr.grad) < 1e-4
     for n, q in blk.named_parameters():
         assert rel(q.grad, P[n].grad) < 1e-4, n
+
+
+# ------------------------------------------------------- fp8 attention ---
+def _f8(x):
+    """round to OCP e4m3 (float8_e4m3fn, round to nearest even) and back"""
+    return x.to(torch.float8_e4m3fn).float()
+
+
+def _pow2_scale(amax):
+    """the kernel's power-of-two scale: 2^floor(log2(448 / amax)) (1 for 0)"""
+    r = torch.where(amax > 0, 448.0 / amax.clamp_min(1e-30), torch.ones_like(amax))
+    return torch.exp2(torch.floor(torch.log2(r)))
+
+
+def _attn_fp8_emulated(q, k, v, scale, keep=None):
+    """fp32 restatement of hvit_mhsa_fwd_fp8's arithmetic: per-(b,h) K/V and
+    per-query Q power-of-two scales, e4m3 rounding of q, k, v and of 256 * P
+    (unnormalised, times the dropout multiplier ``keep``), f32 accumulation,
+    normaliser from the unrounded, undropped P."""
+    sk = _pow2_scale(k.abs().amax(dim=(2, 3), keepdim=True))
+    sv = _pow2_scale(v.abs().amax(dim=(2, 3), keepdim=True))
+    sq = _pow2_scale(q.abs().amax(dim=3, keepdim=True))
+    q8, k8, v8 = _f8(q * sq) / sq, _f8(k * sk) / sk, _f8(v * sv) / sv
+    s_ = (q8 @ k8.transpose(-2, -1)) * scale
+    p = torch.exp(s_ - s_.amax(-1, keepdim=True))
+    pk = p if keep is None else p * keep
+    o = (_f8(pk * 256.0) / 256.0) @ v8 / p.sum(-1, keepdim=True)
+    return o
+
+
+@pytest.mark.parametrize("N", [256, 240, 100])
+def test_mhsa_fwd_fp8(hv, N):
+    """e4m3 attention forward (BASELINE config 5 heads: hd 64, 12 heads) against
+    (a) an fp32 emulation of the same e4m3 roundings: tight, this pins the
+    operand layouts, the block scales and the e4m3 encoding (OCP, not fnuz);
+    (b) exact fp32 attention: the fp8 tolerance, stated here as 1e-1
+    relative L2 on the output and 5e-2 on lse (natural-log units) for unit-
+    variance q, k, v (measured 4-7e-2: e4m3 keeps 3 mantissa bits)."""
+    l = L(hv)
+    torch.manual_seed(N)
+    B, H, hd = 2, 12, 64
+    D = H * hd
+    qkv = torch.randn(B, N, 3 * D, device=DEV).to(torch.bfloat16)
+    o = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    scale = hd ** -0.5
+    l.call("hvit_mhsa_fwd_fp8", qkv.data_ptr(), B, N, H, hd, scale, l.dropout(), o.data_ptr(), lse.data_ptr(), s())
+    t = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = t[0], t[1], t[2]
+    got = o.float().view(B, N, H, hd).permute(0, 2, 1, 3)
+    emu = _attn_fp8_emulated(q, k, v, scale)
+    ref = torch.softmax(q @ k.transpose(-2, -1) * scale, -1) @ v
+    ref_lse = torch.logsumexp(q @ k.transpose(-2, -1) * scale, -1)
+    e_emu = ((got - emu).norm() / emu.norm()).item()
+    e_ref = ((got - ref).norm() / ref.norm()).item()
+    print(f"N={N}: vs e4m3 emulation {e_emu:.2e}, vs exact {e_ref:.2e}")
+    assert e_emu < 8e-3  # bf16 output rounding + accumulation order
+    assert e_ref < 1e-1
+    assert (lse - ref_lse).abs().max().item() < 5e-2
+
+
+def test_mhsa_fwd_fp8_dropout_matches_bf16_mask(hv):
+    """With attention dropout the fp8 forward applies the bf16 kernel's mask
+    (the counter hash mirrored by conftest.keep_mask, index ((b*H+h)*N+q)*N+k),
+    so that the bf16 backward recomputes the same mask: checked against the
+    e4m3 emulation with that mask."""
+    l = L(hv)
+    torch.manual_seed(3)
+    B, N, H, hd, p = 2, 128, 4, 64, 0.1
+    D = H * hd
+    qkv = torch.randn(B, N, 3 * D, device=DEV).to(torch.bfloat16)
+    o8 = torch.empty(B, N, D, device=DEV, dtype=torch.bfloat16)
+    lse8 = torch.empty(B, H, N, device=DEV)
+    l.call("hvit_mhsa_fwd_fp8", qkv.data_ptr(), B, N, H, hd, hd ** -0.5, l.dropout(p, 777, 301), o8.data_ptr(),
+           lse8.data_ptr(), s())
+    t = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    ds = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+    keep = torch.as_tensor(keep_mask(777, 301, B * H * N * N, p).reshape(B, H, N, N), device=DEV).float() * ds
+    emu = _attn_fp8_emulated(t[0], t[1], t[2], hd ** -0.5, keep)
+    got = o8.float().view(B, N, H, hd).permute(0, 2, 1, 3)
+    assert ((got - emu).norm() / emu.norm()).item() < 8e-3

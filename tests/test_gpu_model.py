@@ -308,3 +308,26 @@ def test_vit_backward_isolated(hv, kw):
         assert relnorm(got, r) < 1e-4, k
         n += 1
     assert n == 12 * cfg.num_layers + 5
+
+
+def test_large_config_fp8_attention(hv):
+    """BASELINE config 5: the D=768 / 12-head / 12-layer model in bf16 with the
+    fp8 attention forward, against the reference's fp32 golden output at the
+    bf16 bar, and one train step (bf16 attention backward) with the loss at the
+    bf16 bar and finite gradients."""
+    g = golden("large_256")
+    cfg = O.HViTConfig(**LARGE)
+    W = CF.weights(O.state_dict_shapes(cfg))
+    m = hv.HybridViT(**cfg.as_kwargs(), precision="bf16", attention_precision="fp8").cuda().eval()
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
+    with torch.no_grad():
+        y = m(torch.as_tensor(g["x"]).cuda())
+    assert rel(y.cpu(), g["eval_out"]) < BF16_TOL
+    cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
+    m = hv.HybridViT(**cfg.as_kwargs(), precision="bf16", attention_precision="fp8").cuda().train()
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
+    loss = hv.CombinedLoss()(m(torch.as_tensor(g["x"]).cuda()), torch.as_tensor(g["target"]).cuda())
+    loss.backward()
+    assert abs(loss.item() - float(g["train_loss"])) < 2e-2 * abs(float(g["train_loss"]))
+    for k, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), k
