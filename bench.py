@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--attn", default="bf16", choices=["bf16", "fp8"],
                     help="fp8: e4m3 MFMA attention forward (BASELINE config 5), bf16 attention backward")
     ap.add_argument("--roofline-only", action="store_true",
-                    help="only the dominant-kernel timing loop (used for rocprofv3 --pmc passes)")
+                    help="only the dominant op class, re-run in isolation (rocprofv3 --pmc passes)")
+    ap.add_argument("--roofline-op", default="conv_wgrad",
+                    help="op class for --roofline-only (functional.timed tag with a recorded replay)")
     a = ap.parse_args()
     if a.batch is None:
         a.batch = 16 if a.variant == "large" else 32
@@ -95,23 +97,27 @@ def roofline_of(table):
                         "repeat of the timed steps"}
 
 
-def roofline_loop(hv, batch, reps=50):
-    """The dominant op class alone (ViT linear weight gradients of one block:
-    fc2, fc1, proj, qkv shapes, split-K bf16 GEMM + slab reduction), for
-    rocprofv3 --kernel-trace / --pmc passes (bench.py --roofline-only)."""
+def roofline_loop(step, name=None, reps=20):
+    """Re-run the launches of one op class, recorded from one real train step
+    (functional.REPLAY), ``reps`` times on the same tensors: the dominant op in
+    isolation for rocprofv3 --kernel-trace / --pmc passes (bench.py
+    --roofline-only), timed with HIP events on its stream like the in-step
+    table.  ``name`` None = the weight-gradient class with the most work."""
     HF = sys.modules["hvit_amd.functional"]
-    M, D, hid = batch * 256, 512, 2048
-    shapes = [(D, hid), (hid, D), (D, D), (3 * D, D)]  # (N, K): dw[N, K] = dy[M, N]^T x[M, K]
-    ops = [(torch.randn(M, n, device="cuda").to(torch.bfloat16), torch.randn(M, k, device="cuda").to(torch.bfloat16),
-            n, k) for n, k in shapes]
-    for _ in range(3):
-        for dy, x, n, k in ops:
-            HF.linear_wgrad(hv._lib.BF16, dy, x, M, n, k)
+    HF.REPLAY = {}
+    step()
+    rec, HF.REPLAY = HF.REPLAY, None
+    if name is None or name not in rec:
+        name = max(rec, key=lambda k: sum(w for _, w in rec[k]))
+    ops = rec[name]
+    for fn, _ in ops:
+        fn()
     torch.cuda.synchronize()
     HF.OP_TIMES = {}
     for _ in range(reps):
-        for dy, x, n, k in ops:
-            HF.linear_wgrad(hv._lib.BF16, dy, x, M, n, k, tag="vit_linear_wgrad")
+        for fn, w in ops:
+            with HF.timed(name, w):
+                fn()
     torch.cuda.synchronize()
     t = op_table(HF.OP_TIMES, reps)
     HF.OP_TIMES = None
@@ -197,9 +203,6 @@ def main():
     import hvit_amd_loader
 
     hv = hvit_amd_loader.load()
-    if args.roofline_only:
-        print(json.dumps(roofline_loop(hv, args.batch)), flush=True)
-        return
     from hvit_amd.data import spectrogram_batch
     from hvit_amd.dp import GradAllReducer, broadcast_module
 
@@ -234,6 +237,11 @@ def main():
         opt.zero_grad(set_to_none=True)
         return loss
 
+    if args.roofline_only:
+        for _ in range(2):
+            step()
+        print(json.dumps(roofline_loop(step, args.roofline_op)), flush=True)
+        return
     for _ in range(args.warmup):
         step()
     if world > 1:

@@ -64,6 +64,18 @@ def timed(name: str, work: float):
     return _UNTIMED if OP_TIMES is None else _Timed(name, work)
 
 
+# Launch recorder (measurement only): bench.py installs REPLAY = {} for one
+# step; the weight-gradient ops then also store a closure that re-issues the
+# same launch on the same tensors, so the dominant op class can be re-run in
+# isolation (bench.py --roofline-only, the rocprofv3 / PMC loop).
+REPLAY = None
+
+
+def _record(name, fn):
+    if REPLAY is not None:
+        REPLAY.setdefault(name, []).append(fn)
+
+
 def _empty(shape, dt, dev):
     return torch.empty(shape, dtype=L.torch_dtype(dt), device=dev)
 
@@ -231,9 +243,14 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad"):
     db = buf[N * K:] if bias else None
     ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
-    with timed(tag, 2.0 * M * N * K):
+
+    def launch():
         call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db), ws.data_ptr(),
              ws_n, stream_ptr())
+
+    with timed(tag, 2.0 * M * N * K):
+        launch()
+    _record(tag, (launch, 2.0 * M * N * K))
     return (dw, db) if bias else dw
 
 
@@ -276,8 +293,13 @@ def conv_wgrad(dt, g: L.ConvGeom, dz, wshape) -> torch.Tensor:
     ws_n = L.lib().hvit_conv_wgrad_workspace(g)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dz.device)
     P = dz.numel() // co  # output pixels
-    with timed("conv_wgrad", 2.0 * P * co * ci * ks * ks):
+
+    def launch():
         call("hvit_conv_wgrad", dt, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, stream_ptr())
+
+    with timed("conv_wgrad", 2.0 * P * co * ci * ks * ks):
+        launch()
+    _record("conv_wgrad", (launch, 2.0 * P * co * ci * ks * ks))
     return unpack_conv(dwp, wshape)
 
 

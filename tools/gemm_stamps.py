@@ -50,7 +50,34 @@ def probe(M, N, K, tag, epi=None):
     print("   start histogram:", list(hist[0]), [round(v, 1) for v in hist[1]])
 
 
+def probe_wgrad(M, N, K, tag):
+    """dw[N, K] = dy[M, N]^T x[M, K] (split-K slabs), stamps of the GEMM launch"""
+    dy = torch.randn(M, N, device="cuda").to(BF)
+    x = torch.randn(M, K, device="cuda").to(BF)
+    dw = torch.empty(N, K, device="cuda")
+    ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
+    ws = torch.empty(max(ws_n, 1), device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        L.call("hvit_linear_wgrad", L.BF16, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), None,
+               ws.data_ptr(), ws_n, st)
+    torch.cuda.synchronize()
+    splits = ws_n // (N * K + N) if ws_n else 1
+    nblk = (N // 128) * (K // 128) * max(splits, 1)
+    s = stamps(nblk)
+    t0 = s[:, 0].min()
+    loop = (s[:, 1] - s[:, 0]) * TICK_US
+    epil = (s[:, 2] - s[:, 1]) * TICK_US
+    end = (s[:, 2] - t0) * TICK_US
+    print(f"{tag}: M={M} N={N} K={K} splits~{splits} blocks={nblk} span {end.max():.1f} us  "
+          f"loop med {np.median(loop):.1f}  epilog med {np.median(epil):.1f} us", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "wgrad":
+        for N_, K_ in [(512, 2048), (2048, 512), (512, 512), (1536, 512)]:
+            probe_wgrad(8192, N_, K_, f"wgrad {N_}x{K_}")
+        sys.exit(0)
     probe(8192, 2048, 512, "fc1 plain")
     probe(8192, 2048, 2048, "fc1 K=2048")
     probe(8192, 512, 512, "proj plain")

@@ -1,6 +1,6 @@
 """Per-kernel PMC summary from rocprofv3 --pmc csv passes (tools/pmc_pass.sh).
 
-    python tools/pmc_summary.py OUT.json DIR [DIR ...] [--op NAME]
+    python tools/pmc_summary.py OUT.json DIR [DIR ...] [--op NAME --match REGEX --oplaunches N]
 
 Kernels are grouped by (short name, grid); per group: launches and the mean
 per-launch counters.  HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes):
@@ -28,11 +28,18 @@ def short(name):
 
 def main():
     argv = sys.argv[1:]
-    op = None
-    if "--op" in argv:
-        i = argv.index("--op")
-        op = argv[i + 1]
-        argv = argv[:i] + argv[i + 2:]
+    def opt(flag, cast=str):
+        nonlocal argv
+        if flag in argv:
+            i = argv.index(flag)
+            v = cast(argv[i + 1])
+            argv = argv[:i] + argv[i + 2:]
+            return v
+        return None
+
+    op = opt("--op")
+    match = opt("--match")
+    oplaunches = opt("--oplaunches", int)
     out, dirs = argv[0], argv[1:]
     vals = defaultdict(lambda: defaultdict(list))
     for d in dirs:
@@ -51,9 +58,14 @@ def main():
     summary = {"kernels": dict(sorted(kernels.items(), key=lambda kv: -kv[1].get("hbm_bytes_per_launch", 0)))}
     if op:
         # the roofline loop's op = one split-K GEMM + its slab reduction per launch
-        mine = {k: r for k, r in kernels.items() if k.startswith("gemm_kernel") or k.startswith("sum_slabs")}
+        # --match: regex of the op's kernel names; --oplaunches: op launches in the
+        # run (every kernel launch of the op counts toward its bytes)
+        pat = re.compile(match or r"^(gemm_kernel|sum_slabs)")
+        mine = {k: r for k, r in kernels.items() if pat.search(k)}
         tot = sum(r.get("hbm_bytes_per_launch", 0) * r["launches"] for r in mine.values())
-        nops = sum(r["launches"] for k, r in mine.items() if k.startswith("gemm_kernel"))
+        nops = oplaunches or sum(r["launches"] for k, r in mine.items() if k.startswith("gemm_kernel"))
+        summary["op_kernels"] = sorted(mine)
+        summary["op_launches"] = nops
         summary["op"] = op
         summary["hbm_bytes_per_launch"] = round(tot / max(nops, 1))
     with open(out, "w") as f:

@@ -23,8 +23,8 @@ for s in $STEPS; do
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
     roofprof) timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof -o run --output-format csv -- \
-            python3 bench.py --roofline-only > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $? ;;
-    pmc) bash tools/pmc_pass.sh ${TAG}_rpmc || exit $? ;;
+            python3 bench.py --roofline-only --roofline-op conv_wgrad > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $? ;;
+    pmc) bash tools/pmc_pass.sh ${TAG}_rpmc bench.py --roofline-only --roofline-op conv_wgrad || exit $? ;;
     pmcstep) bash tools/pmc_pass.sh ${TAG}_spmc bench.py --steps 2 --warmup 2 --no-cpu-baseline || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
