@@ -73,6 +73,8 @@ def state_dict_shapes(cfg: HViTConfig) -> Dict[str, Tuple[int, ...]]:
     """The reference's state_dict keys and shapes in registration order
     (hybrid_vit.py:102-170, components.py, attention.py)."""
     s: Dict[str, Tuple[int, ...]] = {}
+    if cfg.use_cls_token:  # a parameter of HybridViT itself: first in state_dict order
+        s["cls_token"] = (1, 1, cfg.embed_dim)
     cin = cfg.input_channels
     for i, (co, k) in enumerate(zip(cfg.encoder_channels, cfg.encoder_kernel_sizes)):
         p = f"encoder.{i}.block"
@@ -84,8 +86,6 @@ def state_dict_shapes(cfg: HViTConfig) -> Dict[str, Tuple[int, ...]]:
     D, P = cfg.embed_dim, cfg.patch_size
     s["patch_embed.projection.weight"] = (D, cin, P, P)
     s["patch_embed.projection.bias"] = (D,)
-    if cfg.use_cls_token:
-        s["cls_token"] = (1, 1, D)
     s["pos_encoding.pos_embed"] = (1, 10000, D)
     hid = int(D * cfg.mlp_ratio)
     for l in range(cfg.num_layers):
@@ -254,9 +254,9 @@ def forward(sd: Dict[str, torch.Tensor], x: torch.Tensor, cfg: HViTConfig,
         attns.append(a)
     t = F.layer_norm(t, (D,), sd["transformer.norm.weight"], sd["transformer.norm.bias"],
                      1e-5)
+    cap["vit_out"] = t           # VisionTransformer output (CLS row included, as the reference module returns)
     if cfg.use_cls_token:
-        t = t[:, 1:, :]
-    cap["vit_out"] = t
+        t = t[:, 1:, :]          # hybrid_vit.py:337-338
     f = F.linear(t, sd["to_feature_map.weight"], sd["to_feature_map.bias"])
     C = f.shape[-1]
     x = f.transpose(1, 2).reshape(B, C, Hp, Wp)

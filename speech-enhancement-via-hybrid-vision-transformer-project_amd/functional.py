@@ -423,7 +423,7 @@ class PatchEmbedFn(torch.autograd.Function):
         D = w.shape[0]
         Hp, Wp = H // Pp, W // Pp
         Nt = Hp * Wp
-        if Nt > pos.shape[1]:
+        if pos is not None and Nt > pos.shape[1]:
             raise ValueError(f"hvit: {Nt} patches exceed the positional table ({pos.shape[1]})")
         dev = feat.device
         s = stream_ptr()
@@ -435,7 +435,7 @@ class PatchEmbedFn(torch.autograd.Function):
         call("hvit_conv_fwd", dt, g, wp.data_ptr(), b.data_ptr(), x0.data_ptr(), F32, None, e, s)
         ctx.save_for_backward(feat, w)
         ctx.wp = wp
-        ctx.meta = (Pp, dr, dt, Nt, pos.shape)
+        ctx.meta = (Pp, dr, dt, Nt, None if pos is None else pos.shape)
         ctx.zs = _zs(ctx, D)
         return x0
 
@@ -452,8 +452,10 @@ class PatchEmbedFn(torch.autograd.Function):
         gd = _empty((M, D), dt, dev)
         db = ctx.zs.take(dev)  # patch-embed bias grad: column sums fused into the dropout pass
         dropout_scale(dx0, M, D, dr, None, 1, gd, db)
-        dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
-        call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
+        dpos = None
+        if pshape is not None:
+            dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
+            call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
         g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
         dw = conv_wgrad(dt, g, gd, w.shape)
         dfeat = None
@@ -461,6 +463,35 @@ class PatchEmbedFn(torch.autograd.Function):
             dfeat = _empty(feat.shape, dt, dev)
             call("hvit_conv_dgrad", dt, g, gd.data_ptr(), ctx.wp.data_ptr(), dfeat.data_ptr(), dt, s)
         return dfeat, dw, db, dpos, None, None, None, None
+
+
+class PosDropFn(torch.autograd.Function):
+    """tokens + pos_embed[:, :N] and dropout (PositionalEncoding components.py:371-386)
+    on tokens handed in from outside the fused patch-embed GEMM: forward_transformer's
+    entry (hybrid_vit.py:309-333) and the CLS-token layout.  Same counter-hash mask
+    (site 200, element index over [B*N, D]) as PatchEmbedFn's epilogue.  f32 [B, N, D]."""
+
+    @staticmethod
+    def forward(ctx, x, pos, drop: Drop, training):
+        B, N, D = x.shape
+        if N > pos.shape[1]:
+            raise ValueError(f"hvit: {N} tokens exceed the positional table ({pos.shape[1]})")
+        t = x.float() + pos[:, :N]
+        dr = drop.c() if training else L.dropout()
+        out = torch.empty_like(t)
+        dropout_scale(t, B * N, D, dr, None, 1, out)
+        ctx.meta = (dr, pos.shape, N, x.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        dr, pshape, N, xdt = ctx.meta
+        B, _, D = g.shape
+        gd = torch.empty((B, N, D), dtype=torch.float32, device=g.device)
+        dropout_scale(g.contiguous(), B * N, D, dr, None, 1, gd)
+        dpos = torch.zeros(pshape, dtype=torch.float32, device=g.device)
+        call("hvit_reduce_rows", gd.data_ptr(), F32, B, N * D, N * D, 1, dpos.data_ptr(), stream_ptr())
+        return gd.to(xdt), dpos, None, None
 
 
 def _ln(x2d, gw, gb, dt):

@@ -229,9 +229,6 @@ class HybridViT(nn.Module):
         attention_precision: Optional[str] = None,
     ):
         super().__init__()
-        if use_cls_token:
-            raise NotImplementedError("hvit: use_cls_token=True is not on the hot path (never set by "
-                                      "create_hybrid_vit)")
         self.input_channels = input_channels
         self.output_channels = output_channels
         self.embed_dim = embed_dim
@@ -256,7 +253,11 @@ class HybridViT(nn.Module):
             in_ch = out_ch
         enc_out = encoder_channels[-1]
         self.patch_embed = PatchEmbedding(enc_out, embed_dim, patch_size, flatten=True)
-        self.cls_token = None
+        if use_cls_token:  # hybrid_vit.py:118-123 (never set by create_hybrid_vit; off the hot path)
+            self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+            nn.init.trunc_normal_(self.cls_token, std=0.02)
+        else:
+            self.cls_token = None
         self.pos_encoding = PositionalEncoding(embed_dim, max_len=10000, learnable=True, dropout=dropout)
         self.transformer = VisionTransformer(embed_dim, num_layers, num_heads, mlp_ratio, True, dropout,
                                              attn_dropout, drop_path_rate)
@@ -363,10 +364,22 @@ class HybridViT(nn.Module):
     def _tokens(self, feat, dt, seed):
         P = self.patch_size
         pe = self.patch_embed.projection
-        t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, self.pos_encoding.pos_embed, P,
-                                  HF.Drop(self.dropout_p, seed, 200), self.training, dt)
+        hw = (feat.shape[1] // P, feat.shape[2] // P)
+        if self.cls_token is None:  # hot path: pos-embed add and dropout fused into the GEMM epilogue
+            t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, self.pos_encoding.pos_embed, P,
+                                      HF.Drop(self.dropout_p, seed, 200), self.training, dt)
+            self.last_num_tokens = t.shape[1]
+            return t, hw
+        t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, None, P, HF.Drop(), False, dt)
+        return self._pos_tokens(t, seed), hw
+
+    def _pos_tokens(self, t, seed):
+        """[CLS +] pos_embed[:, :N] + dropout on given tokens (hybrid_vit.py:323-333,
+        components.py:371-386); same counter-hash mask (site 200) as the fused path."""
+        if self.cls_token is not None:
+            t = torch.cat([self.cls_token.expand(t.shape[0], -1, -1).float(), t.float()], 1)
         self.last_num_tokens = t.shape[1]
-        return t, (feat.shape[1] // P, feat.shape[2] // P)
+        return HF.PosDropFn.apply(t, self.pos_encoding.pos_embed, HF.Drop(self.dropout_p, seed, 200), self.training)
 
     def _vit(self, t, dt, seed, want_attn=False):
         attns = []
@@ -384,6 +397,8 @@ class HybridViT(nn.Module):
         return t, attns
 
     def _head(self, t, hw, dt):
+        if self.cls_token is not None:
+            t = t[:, 1:]  # hybrid_vit.py:337-338 (LayerNorm is per token, so dropping first is equivalent)
         n = self.transformer.norm
         return HF.HeadFn.apply(t, n.weight, n.bias, self.to_feature_map.weight, self.to_feature_map.bias, hw, dt)
 
@@ -419,13 +434,8 @@ class HybridViT(nn.Module):
         self._check_device(x)
         dt = self._dt()
         seed = self._seed()
-        B, N, D = x.shape
-        self.last_num_tokens = N
-        pos = self.pos_encoding.pos_embed[:, :N, :]
-        t = x.float() + pos
-        if self.training and self.dropout_p > 0:
-            t = torch.nn.functional.dropout(t, self.dropout_p)
-        t, _ = self._vit(t.contiguous(), dt, seed)
+        t = self._pos_tokens(x, seed)
+        t, _ = self._vit(t, dt, seed)
         out = self._head(t, spatial_shape, dt)
         HF.zflush(x.device)
         return self._nchw(out)

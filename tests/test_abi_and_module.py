@@ -49,7 +49,8 @@ def test_wgrad_workspace_query(hv):
     assert n >= 0 and n % (512 * 512 + 512) == 0
 
 
-@pytest.mark.parametrize("kw", [{}, O.TINY, dict(num_layers=12, num_heads=12, embed_dim=768)])
+@pytest.mark.parametrize("kw", [{}, O.TINY, dict(num_layers=12, num_heads=12, embed_dim=768),
+                                dict(O.TINY, use_cls_token=True)])
 def test_state_dict_matches_reference(hv, kw):
     m = hv.HybridViT(**kw)
     shapes = O.state_dict_shapes(O.HViTConfig(**kw))

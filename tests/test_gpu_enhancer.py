@@ -35,3 +35,47 @@ def test_enhance_clip_matches_oracle(hv):
     ref = E.AudioEnhancer(OracleModel(O.make_state(shapes, W), cfg), device="cpu").enhance(clip)
     assert out.shape == clip.shape
     assert np.abs(out - ref).max() < 2e-3 * np.abs(ref).max()
+
+
+def test_enhance_cli(hv, tmp_path):
+    """enhance.py (BASELINE config 1's CLI) end to end on the GPU: a YAML model
+    config, a Trainer-style checkpoint dict, --input/--output, --input-dir/
+    --output-dir and --synthetic; the files it writes equal the in-process
+    AudioEnhancer's output for the same weights."""
+    import yaml
+
+    import enhance
+    from hvit_amd import enhancer as E
+
+    cfg = {"model": {"encoder": {"channels": [8, 16, 32]},
+                     "transformer": {"embed_dim": 64, "num_heads": 4, "num_layers": 2},
+                     "decoder": {"channels": [32, 16, 8, 1]}}}
+    (tmp_path / "cfg.yaml").write_text(yaml.safe_dump(cfg))
+    ocfg = O.HViTConfig(**O.TINY)
+    W = CF.weights(O.state_dict_shapes(ocfg))
+    m = hv.create_hybrid_vit(cfg, precision="fp32")
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
+    ck = tmp_path / "best_model.pth"
+    torch.save({"epoch": 1, "model_state_dict": m.state_dict(), "best_val_loss": 0.1}, ck)  # trainer.py:350-380
+    d_in, d_out = tmp_path / "in", tmp_path / "out"
+    d_in.mkdir()
+    clips = [E.synthetic_clip(0.6, seed=20 + i) for i in range(2)]
+    for i, c in enumerate(clips):
+        E.write_wav(d_in / f"n{i}.wav", c, 16000)
+    ref = E.AudioEnhancer(m.cuda().eval(), device="cuda")
+    common = ["--checkpoint", str(ck), "--config", str(tmp_path / "cfg.yaml")]
+    enhance.main(common + ["--input", str(d_in / "n0.wav"), "--output", str(tmp_path / "e0.wav")])
+    got = E.read_wav(tmp_path / "e0.wav", 16000)
+    want = ref.enhance(E.read_wav(d_in / "n0.wav", 16000))
+    assert got.shape == clips[0].shape
+    assert np.abs(got - want).max() < 1e-4 * max(np.abs(want).max(), 1e-6) + 1e-4
+    enhance.main(common + ["--input-dir", str(d_in), "--output-dir", str(d_out)])
+    for i in range(2):
+        got = E.read_wav(d_out / f"n{i}.wav", 16000)
+        want = ref.enhance(E.read_wav(d_in / f"n{i}.wav", 16000))
+        assert np.abs(got - want).max() < 1e-4 * max(np.abs(want).max(), 1e-6) + 1e-4
+    enhance.main(["--config", str(tmp_path / "cfg.yaml"), "--synthetic", "0.5", "--output", str(tmp_path / "s.wav")])
+    s = E.read_wav(tmp_path / "s.wav", 16000)
+    assert s.shape == (8000,) and np.isfinite(s).all()
+    with pytest.raises(SystemExit):
+        enhance.main(["--config", str(tmp_path / "cfg.yaml")])

@@ -612,3 +612,34 @@ def test_mhsa_fwd_fp8_dropout_matches_bf16_mask(hv):
     emu = _attn_fp8_emulated(t[0], t[1], t[2], hd ** -0.5, keep)
     got = o8.float().view(B, N, H, hd).permute(0, 2, 1, 3)
     assert ((got - emu).norm() / emu.norm()).item() < 8e-3
+
+
+def test_pos_dropout_matches_fused_patch_embed(hv):
+    """PosDropFn (forward_transformer's entry and the CLS-token layout) applies
+    the same pos-embed add and counter-hash dropout mask (site 200) as the
+    patch-embedding GEMM's fused epilogue; masks bit-exact vs the numpy mirror,
+    values and gradients vs the fused path."""
+    import sys
+    HF = sys.modules["hvit_amd.functional"]
+    torch.manual_seed(9)
+    B, Hf, Wf, C, D, P, p, seed = 2, 12, 20, 32, 64, 4, 0.25, 987654321
+    feat = torch.randn(B, Hf, Wf, C, device=DEV)
+    w = (torch.randn(D, C, P, P, device=DEV) * 0.05).requires_grad_(True)
+    b = (torch.randn(D, device=DEV) * 0.1).requires_grad_(True)
+    pos = (torch.randn(1, 100, D, device=DEV) * 0.02).requires_grad_(True)
+    drop = HF.Drop(p, seed, 200)
+    fused = HF.PatchEmbedFn.apply(feat, w, b, pos, P, drop, True, hv._lib.F32)
+    plain = HF.PatchEmbedFn.apply(feat, w, b, None, P, HF.Drop(), False, hv._lib.F32)
+    split = HF.PosDropFn.apply(plain, pos, drop, True)
+    N = plain.shape[1]
+    keep = torch.as_tensor(keep_mask(seed, 200, B * N * D, p), device=DEV).view(B, N, D)
+    ds = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+    ref = (plain.detach() + pos.detach()[:, :N]) * keep.float() * ds
+    assert rel(split.detach(), ref) < 1e-6
+    assert rel(fused.detach(), split.detach()) < 1e-5
+    g = torch.randn_like(fused)
+    gf = torch.autograd.grad(fused, (w, b, pos), g)
+    gs = torch.autograd.grad(split, (w, b, pos), g)
+    for a, r in zip(gs, gf):
+        assert rel(a, r) < 1e-5
+    assert torch.count_nonzero(gs[2][:, N:]) == 0

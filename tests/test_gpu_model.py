@@ -48,7 +48,7 @@ def relnorm(a, b):
 
 
 CASES = [("tiny_64", O.TINY), ("tiny_odd", O.TINY), ("tiny_clip", O.TINY), ("default_256", {}),
-         ("default_clip", {}), ("large_256", LARGE)]
+         ("default_clip", {}), ("large_256", LARGE), ("tiny_cls", dict(O.TINY, use_cls_token=True))]
 
 
 def build(hv, kw, precision, train):

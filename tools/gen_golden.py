@@ -103,7 +103,7 @@ def record(name, cfgkw, shape, seed, full_grads=True, with_attn=True,
     d["train_out"] = y.detach().numpy()
     d["train_loss"] = np.float64(loss.item())
     d["train_pre_tanh"] = st["pre_tanh"].detach().numpy()
-    N = st["tokens"].shape[1]
+    N = st["tokens"].shape[1] + (1 if m.cls_token is not None else 0)   # positional rows used
     rows16 = rows16 or {}
     for k, p in m.named_parameters():
         g = p.grad.detach()
@@ -176,6 +176,8 @@ def main():
         # BASELINE config 5 architecture (D=768, 12 heads, 12 layers)
         "large_256": lambda: record("large_256", LARGE, (1, 1, 256, 256), 16, full_grads=False, with_attn=False,
                                     keep=("vit_out", "pre_tanh")),
+        # use_cls_token=True (hybrid_vit.py:118-123, 323-338; never set by create_hybrid_vit)
+        "tiny_cls": lambda: record("tiny_cls", dict(O.TINY, use_cls_token=True), (2, 1, 48, 80), 17),
         "loss_cases": record_losses,
     }
     for name, job in jobs.items():

@@ -25,7 +25,10 @@ for s in $STEPS; do
     roofprof) timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof -o run --output-format csv -- \
             python3 bench.py --roofline-only --roofline-op conv_wgrad > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $? ;;
     pmc) bash tools/pmc_pass.sh ${TAG}_rpmc bench.py --roofline-only --roofline-op conv_wgrad || exit $? ;;
-    pmcstep) bash tools/pmc_pass.sh ${TAG}_spmc bench.py --steps 2 --warmup 2 --no-cpu-baseline || exit $? ;;
+    large) timeout -k 10 300 python -u bench.py --variant large --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_large_bf16.log 2>&1 || exit $?
+           timeout -k 10 300 python -u bench.py --variant large --attn fp8 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_large_fp8.log 2>&1 || exit $?
+           timeout -k 10 300 python -u bench.py --mode infer --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_infer.log 2>&1 || exit $? ;;
+    pmcstep)bash tools/pmc_pass.sh ${TAG}_spmc bench.py --steps 2 --warmup 2 --no-cpu-baseline || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   echo "step $s ok"
