@@ -552,40 +552,44 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, 
   }
 }
 
-// k-major ("MN") bf16 tile: element (k, r) at k*PM + swizzled byte column.
-// The 128-byte XOR on k bit 3 (tiles with >= 128 rows) puts the two 16-lane
-// groups of a transposed read on disjoint bank halves.
+// k-major ("MN") bf16 tile, [64 k][R rows] with 2R-byte rows and no padding:
+// the 16-byte chunk c of row k sits at chunk c ^ swz(k), swz(k) = 2(k&3) ^
+// 8((k>>3)&1) (R = 128) or 2((k>>1)&1) ^ 4((k>>3)&1) (R = 64).  Conflict-free
+// for the 16x16x32 operand fragments read with two ds_read_b64_tr_b16 (checked
+// exhaustively) and for the ds_write_b128 of 8 lanes filling one row; the same
+// layout as the LDS-DMA MN image (DmaImg), which applies the swizzle on the
+// source side.
 template <int R>
-struct MnTile {
-  static constexpr int PM = R * 2 + 32;
-  __device__ __forceinline__ static int off(int k, int colbyte) {
-    return k * PM + (R >= 128 ? (colbyte ^ (((k >> 3) & 1) << 7)) : colbyte);
+struct MnSwz {
+  static_assert(R == 64 || R == 128, "MN tile: 64 or 128 rows");
+  static constexpr int ROWB = 2 * R;
+  __device__ __forceinline__ static int swz(int k) {
+    return R >= 128 ? ((2 * (k & 3)) ^ (8 * ((k >> 3) & 1))) : ((2 * ((k >> 1) & 1)) ^ (4 * ((k >> 3) & 1)));
+  }
+  __device__ __forceinline__ static int off(int k, int chunk) { return k * ROWB + ((chunk ^ swz(k)) << 4); }
+  // 16x16x32 operand fragment of rows rb..rb+15, k-step s: lane (g = l>>4,
+  // i = l&15) receives rows rb+i, k = 32s + 8g + 0..7
+  __device__ __forceinline__ static u32x4 frag(const char* img, int rb, int s, int lane) {
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int k0 = 32 * s + 8 * g + q;
+    const int ch = (rb >> 3) + (p >> 1), byte = (p & 1) * 8;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + off(k0, ch) + byte));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + off(k0 + 4, ch) + byte));
+    u32x4 r;
+    r[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+    r[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+    r[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+    r[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+    return r;
   }
 };
-
-// 16x16x32 bf16 operand fragment from a k-major tile via two transposed reads:
-// lane (g = l>>4, i = l&15) receives rows rb+i, k = 32s + 8g + 0..7.
-template <int R>
-__device__ __forceinline__ u32x4 frag_tr(const char* tile, int rb, int s, int lane) {
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int k0 = 32 * s + 8 * g + q;
-  const int cb = (rb + 4 * p) * 2;
-  v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + MnTile<R>::off(k0, cb)));
-  v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + MnTile<R>::off(k0 + 4, cb)));
-  u32x4 r;
-  r[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
-  r[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
-  r[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
-  r[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
-  return r;
-}
 
 template <typename T, int R, bool KC>
 struct TileCfg {
   static constexpr int E = Elem<T>::PER16;
   static constexpr int BK = KSTAGE / sizeof(T);
   static constexpr bool TR = !KC && sizeof(T) == 2;
-  static constexpr int BYTES = TR ? BK * MnTile<R>::PM : R * KSTAGE;  // per stage
+  static constexpr int BYTES = R * KSTAGE;  // per stage (MN bf16: 64 k x 2R bytes, unpadded)
   static constexpr int CH = R * KSTAGE / 16 / GEMM_THREADS;           // chunks per thread
   // chunk ch -> (row, k) offsets within the stage
   __device__ __forceinline__ static void map(int ch, int& row, int& k) {
@@ -603,7 +607,7 @@ struct TileCfg {
     if (KC) {
       *(u32x4*)(tile + kc_off(row, k / E)) = v;
     } else if (TR) {
-      *(u32x4*)(tile + MnTile<R>::off(k, row * 2)) = v;
+      *(u32x4*)(tile + MnSwz<R>::off(k, row / E)) = v;
     } else {  // f32 scatter-transpose into the KC layout
       const T* e = (const T*)&v;
 #pragma unroll
@@ -613,15 +617,18 @@ struct TileCfg {
   }
   __device__ __forceinline__ static u32x4 frag(const char* tile, int rb, int s, int lane) {
     if constexpr (TR) {
-      return frag_tr<R>(tile, rb, s, lane);
+      return MnSwz<R>::frag(tile, rb, s, lane);
     } else {
       return *(const u32x4*)(tile + kc_off(rb + (lane & 15), 4 * s + (lane >> 4)));
     }
   }
 };
 
-template <typename T, int BM, int BN, class LA, class LB>
+// NRS register stages: stage t + NRS - 1 is in flight (global loads) while
+// stage t runs on the MFMAs, so a load has NRS - 1 compute phases to land.
+template <typename T, int BM, int BN, class LA, class LB, int NRS = 2>
 struct GemmCore {
+  static_assert(NRS >= 2 && NRS <= 4, "register stages");
   using TA = TileCfg<T, BM, LA::KC>;
   using TB = TileCfg<T, BN, LB::KC>;
   static constexpr int BK = TA::BK;
@@ -669,7 +676,7 @@ struct GemmCore {
       kofb[c] = k;
       lb.init(sb, cb[c], n0 + row, kbeg + k);
     }
-    u32x4 ra0[CA], rb0[CB], ra1[CA], rb1[CB];
+    u32x4 ra[NRS][CA], rb[NRS][CB];
     // stage s is fetched with the cursors at kbeg + s*BK; stages beyond the end
     // re-read the last valid stage (keeps the load count static; never used)
     int fetched = 0;
@@ -735,7 +742,7 @@ struct GemmCore {
         const int rg = tid % RS_RG, kg = tid / RS_RG;
 #pragma unroll
         for (int i = 0; i < RS_KPG; ++i) {
-          const u32x4 v = *(const u32x4*)(at + MnTile<BM>::off(kg * RS_KPG + i, rg * 16));
+          const u32x4 v = *(const u32x4*)(at + MnSwz<BM>::off(kg * RS_KPG + i, rg));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             rsacc[2 * e] += __uint_as_float(v[e] << 16);
@@ -745,25 +752,25 @@ struct GemmCore {
       }
     };
 
-    // prologue: stage 0 -> regs0 -> LDS0; stage 1 -> regs1 (in flight)
-    fetch(ra0, rb0);
-    fetch(ra1, rb1);
-    stash(ra0, rb0, 0);
+    // prologue: stages 0 .. NRS-1 -> register slots; stage 0 -> LDS buffer 0
+#pragma unroll
+    for (int u = 0; u < NRS; ++u) fetch(ra[u], rb[u]);
+    stash(ra[0], rb[0], 0);
     __syncthreads();
-    for (int t = 0; t < nk; t += 2) {
-      // even stage t in LDS0; stage t+1 in regs1; prefetch stage t+2 -> regs0
-      fetch(ra0, rb0);
-      compute(0);
-      rowsum(0);
-      if (t + 1 < nk) stash(ra1, rb1, 1);
-      __syncthreads();
-      if (t + 1 >= nk) break;
-      // odd stage t+1 in LDS1; stage t+2 in regs0; prefetch stage t+3 -> regs1
-      fetch(ra1, rb1);
-      compute(1);
-      rowsum(1);
-      if (t + 2 < nk) stash(ra0, rb0, 0);
-      __syncthreads();
+    for (int t = 0; t < nk; t += NRS) {
+#pragma unroll
+      for (int u = 0; u < NRS; ++u) {
+        // stage t+u is in LDS buffer (t+u)&1 and its slot u is free: refill
+        // slot u with stage t+u+NRS, run stage t+u, then move stage t+u+1
+        // (slot (u+1) % NRS) into the other buffer
+        const int buf = (t + u) & 1;
+        fetch(ra[u], rb[u]);
+        compute(buf);
+        rowsum(buf);
+        if (t + u + 1 < nk) stash(ra[(u + 1) % NRS], rb[(u + 1) % NRS], buf ^ 1);
+        __syncthreads();
+        if (t + u + 1 >= nk) return;
+      }
     }
   }
 };
@@ -798,9 +805,7 @@ struct DmaImg {
   static constexpr int PIECES = BYTES / 1024;       // DMA wave-instructions per stage
   static constexpr int RPP = 1024 / ROWB;           // LDS rows per piece
   static_assert(KC || R == 64 || R == 128, "MN DMA image: 64 or 128 rows");
-  __device__ __forceinline__ static int swz(int k) {
-    return R >= 128 ? ((2 * (k & 3)) ^ (8 * ((k >> 3) & 1))) : ((2 * ((k >> 1) & 1)) ^ (4 * ((k >> 3) & 1)));
-  }
+  __device__ __forceinline__ static int swz(int k) { return MnSwz<KC ? 128 : R>::swz(k); }
   // byte offset (from the tile's origin element) that `lane` fetches for piece pc
   __device__ __forceinline__ static unsigned src_off(int pc, int lane, long ld) {
     const int row = pc * RPP + lane / NCH;  // KC: operand row; MN: k
@@ -813,19 +818,7 @@ struct DmaImg {
     if constexpr (KC) {
       return *(const u32x4*)(img + kc_off(rb + (lane & 15), 4 * s + (lane >> 4)));
     } else {
-      const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-      const int k0 = 32 * s + 8 * g + q;
-      const int ch = (rb >> 3) + (p >> 1), byte = (p & 1) * 8;
-      const char* a0 = img + k0 * ROWB + ((ch ^ swz(k0)) << 4) + byte;
-      const char* a1 = img + (k0 + 4) * ROWB + ((ch ^ swz(k0 + 4)) << 4) + byte;
-      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
-      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
-      u32x4 r;
-      r[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
-      r[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
-      r[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
-      r[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
-      return r;
+      return MnSwz<R>::frag(img, rb, s, lane);
     }
   }
 };
@@ -935,6 +928,13 @@ extern __device__ unsigned long long g_gemm_stamps[65536 * 4];
   } while (0)
 #endif
 
+template <typename X>
+struct IsConvWF : std::false_type {};
+template <typename T>
+struct IsConvWF<LdConvWF<T>> : std::true_type {};
+#ifndef HVIT_WF_STAGES
+#define HVIT_WF_STAGES 2
+#endif
 #ifndef HVIT_BIG_OCC
 #define HVIT_BIG_OCC 2
 #endif
@@ -967,7 +967,9 @@ __device__ __forceinline__ TileId tile_of(int remap) {
 template <typename T, int BM, int BN, class LA, class LB, int EK, bool RS = false, bool DMAK = false>
 __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
                                                                                             int K, int kps, Epi ep) {
-  using C = GemmCore<T, BM, BN, LA, LB>;
+  // the implicit-im2col weight gradient streams both operands from HBM once:
+  // deeper register prefetch (its 128x64 tiles have the registers for it)
+  using C = GemmCore<T, BM, BN, LA, LB, IsConvWF<LB>::value ? HVIT_WF_STAGES : 2>;
   constexpr int WM = C::WM, WN = C::WN, WTM = C::WTM, WTN = C::WTN, FM = C::FM, FN = C::FN;
   // LDS-DMA K loop (DMAK kernels): dense bf16 operands, no row sums
   constexpr bool DMA = sizeof(T) == 2 && IsDenseBf16<LA>::value && IsDenseBf16<LB>::value && !RS;

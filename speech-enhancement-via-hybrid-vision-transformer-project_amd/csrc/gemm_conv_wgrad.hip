@@ -1,6 +1,13 @@
 // C-ABI conv weight gradient (im2col operand, split-K slabs) on the MFMA GEMM.
 #include "gemm_host.h"
 
+// shifted-row-window path for the 3x3 convs (conv_wgrad_rows.hip)
+bool conv_wgrad_rows_geom_ok(const hvit_conv_geom_t* g);
+bool conv_wgrad_rows_ok(int dt, const hvit_conv_geom_t* g);
+long long conv_wgrad_rows_ws(const hvit_conv_geom_t* g);
+int conv_wgrad_rows(const hvit_conv_geom_t* g, const void* dy, float* dw_packed, float* ws, long long ws_elems,
+                    hipStream_t st);
+
 extern "C" long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g) {
   if (!g) return 0;
   if (thin_c1(g)) return hvit_thin_c1_wgrad_ws(g);
@@ -10,8 +17,10 @@ extern "C" long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g) {
   const long Wo = (Wi + 2 * g->pad - g->KS) / g->stride + 1;
   const long Kt = (long)g->KS * g->KS * (g->C1 + g->C2);
   const ConvWgTile t(g->Cout);
-  int s = wgrad_splits(g->Cout, Kt, g->N * Ho * Wo, t.bm, t.bn);
-  return s > 1 ? (long long)s * g->Cout * Kt : 0;
+  int s = conv_wgrad_splits(g->Cout, Kt, g->N * Ho * Wo, t.bm, t.bn);
+  const long long gen = s > 1 ? (long long)s * g->Cout * Kt : 0;
+  // the dtype is not known here: room for either path
+  return conv_wgrad_rows_geom_ok(g) ? std::max(gen, conv_wgrad_rows_ws(g)) : gen;
 }
 
 extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy, float* dw_packed, float* ws,
@@ -22,6 +31,7 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
   hipStream_t st = (hipStream_t)stream;
   if (thin_c1(g)) return hvit_thin_c1_wgrad(dt, g, dy, dw_packed, ws, ws_elems, st);
   if (thin_o1(g)) return hvit_thin_o1_wgrad(dt, g, dy, dw_packed, ws, ws_elems, st);
+  if (conv_wgrad_rows_ok(dt, g)) return conv_wgrad_rows(g, dy, dw_packed, ws, ws_elems, st);
   DT_DISPATCH(dt, {
     auto la = conv_a<T>(g, g->src1, g->C1, g->src2, g->C2, g->Hs, g->Ws, g->U, g->KS, g->stride, g->pad);
     LdConv<T, false> lb;
@@ -51,7 +61,7 @@ extern "C" int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy
     }
     const int M = g->Cout, N = la.Kt, K = la.P;
     const ConvWgTile t(M);
-    int splits = wgrad_splits(M, N, K, t.bm, t.bn);
+    int splits = conv_wgrad_splits(M, N, K, t.bm, t.bn);
     if ((long long)splits * M * N > ws_elems || !ws) splits = 1;
     splits = plan_splits<T>(K, splits);
     Epi ep;

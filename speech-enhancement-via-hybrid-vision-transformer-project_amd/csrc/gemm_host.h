@@ -59,12 +59,14 @@ int check_epi(const hvit_epilogue_t* e) {
 // choose split-K so that a wgrad launch has enough workgroups: about 256
 // workgroups of the given tile (one per CU, two for 64x64 tiles; each keeps
 // >= 4 K-stages)
-int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64) {
+// (conv: the implicit-im2col weight gradient, whose 128x64 tiles fit more
+// workgroups per CU; HVIT_WG_TARGET / HVIT_CONV_WG_TARGET override the targets
+// for A/B measurements only)
+int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64, bool conv = false) {
   long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
-  // small tiles: two per CU.  HVIT_WG_TARGET overrides the 128x128 target
-  // (A/B measurements only)
   static const long big = getenv("HVIT_WG_TARGET") ? atol(getenv("HVIT_WG_TARGET")) : 256;
-  const long target = bm * bn <= 64 * 64 ? 512 : big;
+  static const long cbig = getenv("HVIT_CONV_WG_TARGET") ? atol(getenv("HVIT_CONV_WG_TARGET")) : 256;
+  const long target = bm * bn <= 64 * 64 ? 512 : conv ? cbig : big;
   long want = (target + tiles - 1) / tiles;
   long maxs = K / (4 * bk);
   // a multiple of 8 slices: with the XCD-aware tile order (gemm.h tile_of)
@@ -75,6 +77,33 @@ int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64) {
   if (want > 256) want = 256;
   if (want < 1) want = 1;
   return (int)want;
+}
+// Split-K of the conv weight gradient (implicit-im2col tiles, up to 3
+// workgroups resident per CU).  tiles * splits workgroups are dealt evenly
+// over the 256 CUs, so the busiest CU runs ceil(nwg / 256) of them: pick the
+// split count that keeps the CUs evenly loaded (nwg / (256 ceil(nwg / 256))
+// near 1) with >= 1.5 workgroups per CU on average for latency hiding, and
+// prefer fewer splits (less slab traffic).  Measured on enc1 (9 tiles,
+// tools/wgrad_sweep.py, B=32): 288 WGs 226 us, 432 -> 169, 576 -> 203,
+// 792 -> 185.  HVIT_CONV_WG_TARGET selects the older fixed-target rule (A/B).
+int conv_wgrad_splits(int M, long N, long K, int bm, int bn, int bk = 64) {
+  if (getenv("HVIT_CONV_WG_TARGET")) return wgrad_splits(M, N, K, bm, bn, bk, true);
+  const long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
+  const long maxs = std::max(1L, std::min(256L, K / (4 * bk)));
+  int best = 1;
+  double bs = -1e30;
+  for (long s = 1; s <= maxs; ++s) {
+    const long nwg = tiles * s;
+    if (nwg > 768 && s > 1) break;
+    const long per = (nwg + 255) / 256;
+    double score = (double)nwg / (256.0 * per) - 0.02 * (double)nwg / 256.0;
+    if (nwg < 384) score -= 0.5 * (384.0 - (double)nwg) / 384.0;
+    if (score > bs + 1e-9) {
+      bs = score;
+      best = (int)s;
+    }
+  }
+  return best;
 }
 // wgrad tiles: dense x dense -> 128x128; dense x im2col -> 128x64 (fits the
 // register budget of the gathered operand's cursors)

@@ -62,9 +62,22 @@ template <typename T>
 __device__ __forceinline__ long stage_strip(const T* __restrict__ x, int P, int p0, int pend, int W, float* xs) {
   const long base = (long)p0 - W - 1;
   const int n = (pend - p0) + 2 * W + 2;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const long q = base + i;
-    xs[i] = (q >= 0 && q < P) ? Elem<T>::to_f(x[q]) : 0.f;
+  // batches of loads in flight per thread (a load -> store chain per element
+  // serialised the staging on memory latency)
+  constexpr int UB = 8;
+  for (int i0 = threadIdx.x; i0 < n; i0 += 256 * UB) {
+    float v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int i = i0 + u * 256;
+      const long q = base + i;
+      const bool ok = i < n && q >= 0 && q < P;
+      const float e = Elem<T>::to_f(x[ok ? q : 0]);  // unconditional load (clamped): no branch per element
+      v[u] = ok ? e : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+      if (i0 + u * 256 < n) xs[i0 + u * 256] = v[u];
   }
   __syncthreads();
   return base;
@@ -192,8 +205,14 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
 
 // partial[blk][co][tap] = sum over the block's pixels of dz[p][co] * x[p + tap]
 // (pixel chunks sized for >= 4 workgroups per CU at the model's shapes)
-constexpr int WG_PIX = 2048;   // Cin = 1 wgrad (2M pixels at B=32)
-constexpr int C1_WG_PF = 4;    // dz prefetch depth (pixels per thread)
+// Cin = 1 wgrad: pixels per workgroup sized so the grid is one round of
+// three resident workgroups per CU (2M pixels at B=32 -> 2752 per workgroup)
+constexpr int C1W_MIN_PIX = 512, C1W_GRID = 768;
+__host__ __device__ inline int c1w_pix(long P) {
+  const long per = (P + C1W_GRID - 1) / C1W_GRID;
+  return (int)std::max<long>(C1W_MIN_PIX, (per + 63) / 64 * 64);
+}
+constexpr int C1_WG_PF = 8;    // dz prefetch depth (pixels per thread)
 
 // 8 consecutive elements kept raw in registers until used
 template <typename T>
@@ -224,17 +243,22 @@ struct Raw8<float> {
   }
 };
 constexpr int WG_PIX_O1 = 256; // Cout = 1 wgrad (131k pixels at B=32)
-template <typename T>
+// CC = Cout / 8 is a template parameter so the lane reductions below unroll
+// (a runtime-bounded shuffle loop serialised 72 x 3 ds_bpermute round trips)
+template <typename T, int CC>
 __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
                                                        float* __restrict__ part, int N, int H, int W, int Cout) {
   // thread = (8-channel group cc, pixel lane); 72 accumulators in registers;
-  // wave-level shuffles then LDS across the 4 waves.
-  __shared__ float red[4][256 * 9];
-  extern __shared__ float xs[];  // the block's input strip (stage_strip)
-  const int CC = Cout / 8;  // power of two, <= 32
-  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC, lanes = 256 / CC;
+  // wave-level shuffles then LDS across the 4 waves.  Dynamic LDS: the input
+  // strip (stage_strip), then the [4 waves][Cout * 9] reduction buffer (sized
+  // by Cout so more workgroups fit per CU: more dz bytes in flight)
+  extern __shared__ float xs[];
+  constexpr int lanes = 256 / CC;
+  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int P = N * H * W;
-  const int pbeg = blockIdx.x * WG_PIX, pend = min(P, pbeg + WG_PIX);
+  const int wg_pix = c1w_pix(P);
+  const int pbeg = blockIdx.x * wg_pix, pend = min(P, pbeg + wg_pix);
+  float* red = xs + strip_floats(wg_pix, W);
   const long base = stage_strip(x, P, pbeg, pend, W, xs);
   float acc[9][8];
 #pragma unroll
@@ -275,11 +299,12 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, 
     for (int e = 0; e < 8; ++e) {
       float v = acc[t][e];
       for (int o = CC; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (ln < CC) red[wv][(cc * 8 + e) * 9 + t] = v;
+      if (ln < CC) red[wv * Cout * 9 + (cc * 8 + e) * 9 + t] = v;
     }
   __syncthreads();
-  for (int i = threadIdx.x; i < Cout * 9; i += 256)
-    part[(size_t)blockIdx.x * Cout * 9 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  const int R = Cout * 9;
+  for (int i = threadIdx.x; i < R; i += 256)
+    part[(size_t)blockIdx.x * R + i] = red[i] + red[R + i] + red[2 * R + i] + red[3 * R + i];
 }
 
 // --------------------------------------------------------------- Cout = 1 ---
@@ -341,6 +366,9 @@ __global__ __launch_bounds__(256) void o1_dgrad_kernel(const TD* __restrict__ dz
 }
 
 // part[blk][tap][ci] = sum_p dz[p] * in[p + tap][ci]
+__host__ __device__ inline size_t o1_strip_bytes(int pix, int W, int C, size_t esz) {
+  return ((size_t)(pix + 2 * W + 2) * C * esz + 1023) / 1024 * 1024;
+}
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void o1_wgrad_kernel(const T* __restrict__ x, const TD* __restrict__ dz,
                                                        float* __restrict__ part, int N, int Hs, int Ws, int U, int C) {
@@ -371,6 +399,80 @@ __global__ __launch_bounds__(256) void o1_wgrad_kernel(const T* __restrict__ x, 
     }
   }
   // lanes of a wave with the same cc differ by multiples of CC
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = acc[t][e];
+      for (int o = CC; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (ln < CC) red[wv * 9 * C + t * C + cc * 8 + e] = v;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 9 * C; i += 256)
+    part[(size_t)blockIdx.x * 9 * C + i] = red[i] + red[9 * C + i] + red[18 * C + i] + red[27 * C + i];
+}
+
+// The same for U == 1 with the input staged once: NHWC pixels are contiguous
+// in the flattened index p = (n, y, x), so every tap of the block's pixels lies
+// in [p0 - W - 1, pend + W + 1), staged into LDS (native dtype, 16-B vectors);
+// each input vector then leaves HBM once instead of once per tap, and the
+// per-pixel index math is the incremental PixCursor.
+template <typename T, typename TD, int CC>
+__global__ __launch_bounds__(256) void o1_wgrad_strip_kernel(const T* __restrict__ x, const TD* __restrict__ dz,
+                                                             float* __restrict__ part, int N, int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) char o1s[];
+  T* xs = (T*)o1s;
+  constexpr int C = CC * 8;
+  constexpr int G = 256 / CC;
+  const int cc = threadIdx.x % CC, lg = threadIdx.x / CC;
+  const int P = N * H * W;
+  const int p0 = blockIdx.x * WG_PIX_O1, pend = min(P, p0 + WG_PIX_O1);
+  const long base = (long)p0 - W - 1;
+  const int ns = (pend - p0) + 2 * W + 2;
+  const int upp = C * (int)sizeof(T) / 16;  // 16-B units per pixel
+  float* red = (float*)(o1s + o1_strip_bytes(WG_PIX_O1, W, C, sizeof(T)));
+  // LDS-DMA staging: 16-B units, lane-linear destinations (a wave-instruction
+  // fills 1 KiB; o1_strip_bytes rounds the strip up to whole KiB), units outside
+  // the tensor read as zeros through the buffer range check
+  {
+    const int nu = ns * upp;
+    const long u0 = base * upp, ulim = (long)P * upp;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(ulim * 16), 0x00020000);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i0 = wid * 64; i0 < nu; i0 += 256) {
+      const long q = u0 + i0 + lane;
+      const unsigned voff = (i0 + lane < nu && q >= 0 && q < ulim) ? (unsigned)(q * 16) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(o1s + (size_t)i0 * 16), 16,
+                                               voff, 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
+  float* dzs = red + 4 * 9 * C;  // the block's dz values (one per pixel)
+  if (p0 + (int)threadIdx.x < pend) dzs[threadIdx.x] = Elem<TD>::to_f(dz[p0 + threadIdx.x]);
+  __syncthreads();
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
+  PixCursor pc(p0 + lg, H, W);
+  for (int p = p0 + lg; p < pend; p += G, pc.advance(G, H, W)) {
+    const float d = dzs[p - p0];
+    const T* c = xs + (size_t)(p - base) * C + cc * 8;
+    const bool up = pc.y > 0, dn = pc.y + 1 < H, lf = pc.x > 0, rt = pc.x + 1 < W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool ok = (dy < 0 ? up : dy > 0 ? dn : true) && (dx < 0 ? lf : dx > 0 ? rt : true);
+      if (!ok) continue;
+      float v[8];
+      Vec8<T>::load(c + (dy * W + dx) * C, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t][e] += d * v[e];
+    }
+  }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -424,27 +526,35 @@ int hvit_thin_c1_bn_tile_rows() { return C1_BLOCK_PIX; }
 
 long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g) {
   const long P = (long)g->N * g->Hs * g->Ws;
-  return (long long)((P + WG_PIX - 1) / WG_PIX) * g->Cout * 9;
+  const int wp = c1w_pix(P);
+  return (long long)((P + wp - 1) / wp) * g->Cout * 9;
 }
 
 int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,
                        hipStream_t st) {
   HVIT_CHECK(g->Cout <= 256 && 256 % g->Cout == 0, "thin conv wgrad: Cout=%d must divide 256", g->Cout);
   const long P = (long)g->N * g->Hs * g->Ws;
-  const int nb = (int)((P + WG_PIX - 1) / WG_PIX);
+  const int wp = c1w_pix(P);
+  const int nb = (int)((P + wp - 1) / wp);
   HVIT_CHECK(ws && ws_elems >= (long long)nb * g->Cout * 9, "thin conv wgrad: workspace too small");
-  const size_t smem = sizeof(float) * strip_floats(WG_PIX, g->Ws);
-  HVIT_CHECK(smem + sizeof(float) * 4 * 256 * 9 <= 160 * 1024, "thin conv wgrad: W=%d too wide for the LDS strip",
-             g->Ws);
-  if (dt == HVIT_BF16) {
-    allow_lds(c1_wgrad_kernel<bf16_t>, smem);
-    hipLaunchKernelGGL((c1_wgrad_kernel<bf16_t>), dim3(nb), dim3(256), smem, st, (const bf16_t*)g->src1,
-                       (const bf16_t*)dz, ws, g->N, g->Hs, g->Ws, g->Cout);
-  } else {
-    allow_lds(c1_wgrad_kernel<float>, smem);
-    hipLaunchKernelGGL((c1_wgrad_kernel<float>), dim3(nb), dim3(256), smem, st, (const float*)g->src1,
-                       (const float*)dz, ws, g->N, g->Hs, g->Ws, g->Cout);
+  const size_t smem = sizeof(float) * (strip_floats(wp, g->Ws) + 4 * 9 * g->Cout);
+  HVIT_CHECK(smem <= 160 * 1024, "thin conv wgrad: W=%d too wide for the LDS strip", g->Ws);
+  auto go = [&](auto kern, auto xp) {
+    allow_lds(kern, smem);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(256), smem, st, xp, (decltype(xp))dz, ws, g->N, g->Hs, g->Ws, g->Cout);
+  };
+#define C1W_CASE(cc)                                                  \
+  case cc:                                                            \
+    if (dt == HVIT_BF16)                                              \
+      go(c1_wgrad_kernel<bf16_t, cc>, (const bf16_t*)g->src1);        \
+    else                                                              \
+      go(c1_wgrad_kernel<float, cc>, (const float*)g->src1);          \
+    break;
+  switch (g->Cout / 8) {
+    C1W_CASE(1) C1W_CASE(2) C1W_CASE(4) C1W_CASE(8) C1W_CASE(16) C1W_CASE(32)
+    default: HVIT_CHECK(false, "thin conv wgrad: Cout=%d unsupported", g->Cout);
   }
+#undef C1W_CASE
   HVIT_LAUNCH_CHECK();
   return hvit_sum_slabs(ws, nb, (long long)g->Cout * 9, dw, st);
 }
@@ -502,13 +612,34 @@ int hvit_thin_o1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float*
   const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
   const int nb = (int)((P + WG_PIX_O1 - 1) / WG_PIX_O1);
   HVIT_CHECK(ws && ws_elems >= (long long)nb * 9 * C, "thin conv wgrad: workspace too small");
-  const size_t smem = 4 * 9 * C * sizeof(float);
-  if (dt == HVIT_BF16)
-    hipLaunchKernelGGL((o1_wgrad_kernel<bf16_t, bf16_t>), dim3(nb), dim3(256), smem, st, (const bf16_t*)g->src1,
-                       (const bf16_t*)dz, ws, g->N, g->Hs, g->Ws, g->U, C);
-  else
-    hipLaunchKernelGGL((o1_wgrad_kernel<float, float>), dim3(nb), dim3(256), smem, st, (const float*)g->src1,
-                       (const float*)dz, ws, g->N, g->Hs, g->Ws, g->U, C);
+  const size_t esz = dt == HVIT_BF16 ? 2 : 4;
+  const size_t sstrip = o1_strip_bytes(WG_PIX_O1, g->Ws, C, esz) + (4 * 9 * C + WG_PIX_O1) * sizeof(float);
+  if (g->U == 1 && sstrip <= 150 * 1024 && P * C * (long)esz < (1L << 31)) {  // staged strip (every final conv of the model)
+    auto go = [&](auto kern, auto xp) {
+      allow_lds(kern, sstrip);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(256), sstrip, st, xp, (decltype(xp))dz, ws, g->N, g->Hs, g->Ws);
+    };
+#define O1W_CASE(cc)                                                              \
+  case cc:                                                                        \
+    if (dt == HVIT_BF16)                                                          \
+      go(o1_wgrad_strip_kernel<bf16_t, bf16_t, cc>, (const bf16_t*)g->src1);      \
+    else                                                                          \
+      go(o1_wgrad_strip_kernel<float, float, cc>, (const float*)g->src1);         \
+    break;
+    switch (C / 8) {
+      O1W_CASE(1) O1W_CASE(2) O1W_CASE(4) O1W_CASE(8) O1W_CASE(16) O1W_CASE(32) O1W_CASE(64)
+      default: HVIT_CHECK(false, "thin conv wgrad: Cin=%d unsupported", C);
+    }
+#undef O1W_CASE
+  } else {
+    const size_t smem = 4 * 9 * C * sizeof(float);
+    if (dt == HVIT_BF16)
+      hipLaunchKernelGGL((o1_wgrad_kernel<bf16_t, bf16_t>), dim3(nb), dim3(256), smem, st, (const bf16_t*)g->src1,
+                         (const bf16_t*)dz, ws, g->N, g->Hs, g->Ws, g->U, C);
+    else
+      hipLaunchKernelGGL((o1_wgrad_kernel<float, float>), dim3(nb), dim3(256), smem, st, (const float*)g->src1,
+                         (const float*)dz, ws, g->N, g->Hs, g->Ws, g->U, C);
+  }
   HVIT_LAUNCH_CHECK();
   return hvit_sum_slabs(ws, nb, 9LL * C, dw, st);
 }

@@ -194,6 +194,12 @@ CONV_CASES = [
     (2, 33, 47, 1, 0, 1, 8, 3),
     (3, 20, 256, 1, 0, 1, 64, 3),  # Cin = 1 strips spanning images (enc0 shape class)
     (2, 12, 10, 64, 0, 1, 1, 3),
+    (1, 128, 128, 64, 0, 1, 128, 3),  # enc1 shape class (shifted-row wgrad, rows of 128)
+    (2, 64, 64, 128, 0, 1, 256, 3),   # enc2 shape class (rows of 64, two channel blocks)
+    (1, 16, 16, 128, 64, 2, 64, 3),   # dec2 shape class (x2 upsample, concat, 64-channel tiles)
+    (2, 64, 64, 64, 0, 1, 1, 3),   # the final conv's shape class (staged-strip wgrad)
+    (3, 5, 7, 32, 0, 1, 1, 3),     # Cout = 1, strips spanning several images
+    (1, 8, 6, 16, 0, 2, 1, 3),     # Cout = 1 with upsampling (per-tap wgrad kernel)
 ]
 
 
