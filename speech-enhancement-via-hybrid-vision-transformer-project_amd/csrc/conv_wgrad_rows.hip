@@ -45,22 +45,6 @@ constexpr int ROWS_BN = 192;     // 3 kx x 64 ci
 constexpr int ROWS_BROWS = 72;   // staged input rows per stage (>= 64 + 2 * (64 / Wo))
 constexpr int ROWS_NBUF = 3;
 
-// 16x16x32 fragment of a k-major image with its two k-row groups at physical
-// rows rlo / rhi (the shifted windows of the input strip)
-template <int R>
-__device__ __forceinline__ u32x4 frag_rows(const char* img, int rb, int rlo, int rhi, int lane) {
-  const int li = lane & 15, p = li & 3;
-  const int ch = (rb >> 3) + (p >> 1), byte = (p & 1) * 8;
-  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + MnSwz<R>::off(rlo, ch) + byte));
-  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + MnSwz<R>::off(rhi, ch) + byte));
-  u32x4 r;
-  r[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
-  r[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
-  r[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
-  r[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
-  return r;
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 16, "vmcnt immediate");
@@ -76,9 +60,8 @@ __device__ __forceinline__ void rows_body(const RowsArgs& a, char* smem) {
   constexpr int B_BYTES = ROWS_BROWS * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int PA = IA::PIECES / 4;                   // A pieces per wave per stage
-  constexpr int PBMAX = (ROWS_BROWS / 8 + 3) / 4;      // B pieces per wave (wave 0 one more)
-  constexpr int INF0 = PA + ROWS_BROWS / 8 - 3 * (ROWS_BROWS / 8 / 4);  // wave 0's DMA count
-  constexpr int INF1 = PA + ROWS_BROWS / 8 / 4;                           // waves 1..3
+  constexpr int PB = 3;                                // B pieces per wave (piece 8 on every wave)
+  constexpr int INF = PA + PB;                         // DMA instructions per wave per stage
   static_assert(ROWS_BROWS % 8 == 0 && ROWS_BROWS / 8 == 9, "9 input pieces per stage");
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -119,18 +102,22 @@ __device__ __forceinline__ void rows_body(const RowsArgs& a, char* smem) {
         (void*)(first ? a.src1 : a.src2), (short)0, (int)(first ? a.bytes1 : a.bytes2), 0x00020000);
     const bool wide = a.Wo >= 64;
     const int SW = a.Wo + 2, nseg = wide ? 1 : 64 / a.Wo;
-    // this lane's rows of its B pieces: segment, column, and the swizzled channel chunk
-    int bseg[PBMAX], bcol[PBMAX], bch[PBMAX];
-    bool bon[PBMAX];
+    // this lane's rows of its B pieces: segment, column, and the swizzled
+    // channel chunk.  Nine pieces per stage: waves 1..3 also issue piece 8
+    // (same source, same destination, same bytes), so every wave has the same
+    // DMA count per stage and the waits below are uniform immediates (a
+    // per-wave count made the compiler drain vmcnt(0) before the LDS reads)
+    int bseg[PB], bcol[PB], bch[PB];
+    bool bon[PB];
 #pragma unroll
-    for (int i = 0; i < PBMAX; ++i) {
-      const int piece = wid + 4 * i;
+    for (int i = 0; i < PB; ++i) {
+      const int piece = i < PB - 1 ? wid + 4 * i : 8;
       const int r = piece * 8 + (lane >> 3);
       const int seg = wide ? 0 : r / SW;
       bseg[i] = seg;
       bcol[i] = wide ? r : r - seg * SW;
       bch[i] = coff + 8 * ((lane & 7) ^ MnSwz<64>::swz(r));
-      bon[i] = piece < ROWS_BROWS / 8 && seg < nseg && bcol[i] < (wide ? 66 : SW);
+      bon[i] = seg < nseg && bcol[i] < (wide ? 66 : SW);
     }
     auto issue = [&](int t) {
       char* abuf = smem + (t % ROWS_NBUF) * STAGE;
@@ -146,52 +133,88 @@ __device__ __forceinline__ void rows_body(const RowsArgs& a, char* smem) {
       const int row0 = p0 / a.Wo, ox0 = p0 - row0 * a.Wo;
       const int n = row0 / a.Ho, oy0 = row0 - n * a.Ho;
 #pragma unroll
-      for (int i = 0; i < PBMAX; ++i) {
-        const int piece = wid + 4 * i;
-        if (piece < ROWS_BROWS / 8) {  // uniform
-          const int iy = oy0 + bseg[i] + ky - 1, ix = ox0 + bcol[i] - 1;
-          const bool ok = bon[i] && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-          const unsigned off =
-              (unsigned)((((n * a.Hs + (iy >> a.ushift)) * a.Ws + (ix >> a.ushift)) * Cx + bch[i]) * 2);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbs, (__attribute__((address_space(3))) void*)(bbuf + piece * 1024),
-                                                   16, ok ? off : 0x80000000u, 0, 0, 0);
-        }
+      for (int i = 0; i < PB; ++i) {
+        const int piece = i < PB - 1 ? wid + 4 * i : 8;
+        const int iy = oy0 + bseg[i] + ky - 1, ix = ox0 + bcol[i] - 1;
+        const bool ok = bon[i] && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+        const unsigned off =
+            (unsigned)((((n * a.Hs + (iy >> a.ushift)) * a.Ws + (ix >> a.ushift)) * Cx + bch[i]) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rbs, (__attribute__((address_space(3))) void*)(bbuf + piece * 1024),
+                                                 16, ok ? off : 0x80000000u, 0, 0, 0);
       }
     };
-    // physical strip row of logical pixel k for tap kx (short rows: +2 per row of halo)
-    const int lg = lane >> 4, lq = (lane & 15) >> 2;
-    auto prow = [&](int k, int kx) { return k + kx + (wide ? 0 : 2 * (k / a.Wo)); };
-    auto compute = [&](int t) {
-      const char* at = smem + (t % ROWS_NBUF) * STAGE;
-      const char* bt = at + A_BYTES;
+    // Per-lane byte offsets of the transposed fragment reads, hoisted out of
+    // the loop.  A lane reads rows k = 32s + 8g + q (+4) of a k-major image;
+    // the chunk of a 16-row block rb is (rb / 8 + p / 2) ^ swz(row), and rb / 8
+    // has no bits in common with p / 2, so the block is applied as an XOR of
+    // (rb / 8) << 4 on a per-lane base (swz depends on the row bits 0..3 only).
+    // The input strip's rows are k + kx (+ 2 per short row of halo).
+    const int lg = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+    const int ch0 = lp >> 1, byte = (lp & 1) * 8;
+    unsigned aoff[2], boff[2][3][2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        u32x4 fa[FM], fb[FN];
+    for (int hi = 0; hi < 2; ++hi) {
+      const int row = 8 * lg + lq + 4 * hi;
+      aoff[hi] = (unsigned)(row * IA::ROWB + ((ch0 ^ MnSwz<BM>::swz(row)) << 4) + byte);
+    }
 #pragma unroll
-        for (int i = 0; i < FM; ++i) fa[i] = MnSwz<BM>::frag(at, wm * WTM + i * 16, s, lane);
-        const int k0 = 32 * s + 8 * lg + lq;
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int col = wn * WTN + j * 16;  // compile-time kx / channel block per j and wave half
-          const int kx = col >> 6, rb = col & 63;
-          fb[j] = frag_rows<64>(bt, rb, prow(k0, kx), prow(k0 + 4, kx), lane);
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi) {
+          const int k = 32 * s2 + 8 * lg + lq + 4 * hi;
+          const int row = k + kx + (wide ? 0 : 2 * (k / a.Wo));
+          boff[s2][kx][hi] = (unsigned)(row * 128 + ((ch0 ^ MnSwz<64>::swz(row)) << 4) + byte);
         }
+    auto load = [&](unsigned at, unsigned bt, int s2, u32x4 (&fa)[FM], u32x4 (&fb)[FN]) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
-                                                                __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FM; ++i) {
+        const unsigned x = (unsigned)(((wm * WTM + i * 16) >> 3) << 4);
+        const unsigned ab = at + s2 * 32 * IA::ROWB;
+        fa[i] = tr2_asm(ab + (aoff[0] ^ x), ab + (aoff[1] ^ x));
       }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WTN + j * 16;  // kx / channel block per j and wave half
+        const int kx = col >> 6;
+        const unsigned x = (unsigned)(((col & 63) >> 3) << 4);
+        fb[j] = tr2_asm(bt + (boff[s2][kx][0] ^ x), bt + (boff[s2][kx][1] ^ x));
+      }
+    };
+    auto mma = [&](const u32x4 (&fa)[FM], const u32x4 (&fb)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
+                                                              __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+    };
+    const unsigned smem_a = lds_addr(smem);
+    // k-step 0's fragments, then k-step 1's reads in flight under k-step 0's MFMAs
+    auto compute = [&](int t) {
+      const unsigned at = smem_a + (unsigned)((t % ROWS_NBUF) * STAGE);
+      const unsigned bt = at + A_BYTES;
+      u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+      load(at, bt, 0, fa0, fb0);
+      lgkm_wait0();
+      lds_pin(fa0);
+      lds_pin(fb0);
+      load(at, bt, 1, fa1, fb1);
+      mma(fa0, fb0);
+      lgkm_wait0();
+      lds_pin(fa1);
+      lds_pin(fb1);
+      mma(fa1, fb1);
     };
     issue(0);
     if (nk > 1) issue(1);
     for (int t = 0; t < nk; ++t) {
       if (t + 2 < nk) {
         issue(t + 2);
-        if (wid == 0) wait_vm<2 * INF0>(); else wait_vm<2 * INF1>();  // stage t landed (this wave)
+        wait_vm<2 * INF>();  // stage t landed (this wave's pieces)
       } else if (t + 1 < nk) {
-        if (wid == 0) wait_vm<INF0>(); else wait_vm<INF1>();
+        wait_vm<INF>();
       } else {
         wait_vm<0>();
       }
@@ -199,8 +222,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs& a, char* smem) {
       __builtin_amdgcn_s_barrier();  // every wave's stage-t pieces have landed
       asm volatile("" ::: "memory");
       compute(t);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // buffer t % 3 is free for stage t + 3
+      __builtin_amdgcn_s_barrier();  // buffer t % 3 is free for stage t + 3 (reads drained in compute)
       asm volatile("" ::: "memory");
     }
   }

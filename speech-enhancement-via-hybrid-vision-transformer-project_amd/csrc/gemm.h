@@ -584,6 +584,31 @@ struct MnSwz {
   }
 };
 
+// ds_read_b64_tr_b16 through inline asm, for images filled by LDS-DMA: the
+// intrinsic carries no memory operand, so the compiler's wait-count pass
+// assumes it may alias every in-flight LDS-DMA and drains vmcnt(0) before the
+// first transposed read of a stage (which defeats the DMA prefetch).  Reads
+// issued this way are invisible to that pass: lgkm_wait0() waits for them
+// (lgkmcnt(0)) and lds_pin() pins the fragment registers after the wait.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ uint2 ds_tr16_asm(unsigned addr) {
+  uint2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+__device__ __forceinline__ u32x4 tr2_asm(unsigned lo, unsigned hi) {
+  const uint2 l = ds_tr16_asm(lo), h = ds_tr16_asm(hi);
+  return (u32x4){l.x, l.y, h.x, h.y};
+}
+template <int NF>
+__device__ __forceinline__ void lds_pin(u32x4 (&f)[NF]) {
+#pragma unroll
+  for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(f[i]));
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 template <typename T, int R, bool KC>
 struct TileCfg {
   static constexpr int E = Elem<T>::PER16;
@@ -813,12 +838,17 @@ struct DmaImg {
     const int c = KC ? (pcn ^ (row & 7)) : (pcn ^ swz(row));
     return (unsigned)(((long)row * ld + c * 8) * 2);
   }
-  // 16x16x32 operand fragment of rows rb..rb+15, k-step s
+  // 16x16x32 operand fragment of rows rb..rb+15, k-step s (MN: asm transposed
+  // reads, see lds_fence; callers wait with lgkm_wait0 + lds_pin)
   __device__ __forceinline__ static u32x4 frag(const char* img, int rb, int s, int lane) {
     if constexpr (KC) {
       return *(const u32x4*)(img + kc_off(rb + (lane & 15), 4 * s + (lane >> 4)));
     } else {
-      return MnSwz<R>::frag(img, rb, s, lane);
+      const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+      const int k0 = 32 * s + 8 * g + q;
+      const int ch = (rb >> 3) + (p >> 1), byte = (p & 1) * 8;
+      const unsigned base = lds_addr(img) + byte;
+      return tr2_asm(base + MnSwz<R>::off(k0, ch), base + MnSwz<R>::off(k0 + 4, ch));
     }
   }
 };
@@ -874,23 +904,37 @@ struct GemmCoreDma {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(bbuf + (wid + 4 * i) * 1024),
                                                  16, vb[i], sb, 0, 0);
     };
+    auto load = [&](const char* at, const char* bt, int s, u32x4 (&fa)[FM], u32x4 (&fb)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = IA::frag(at, wm * WTM + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, s, lane);
+    };
+    auto mma = [&](const u32x4 (&fa)[FM], const u32x4 (&fb)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
+                                                              __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+    };
+    // k-step 0's fragments, then k-step 1's reads in flight under k-step 0's
+    // MFMAs (explicit lgkmcnt waits: the MN reads are asm, DmaImg::frag)
     auto compute = [&](int t) {
       const char* at = smem + (t & 1) * (IA::BYTES + IB::BYTES);
       const char* bt = at + IA::BYTES;
-#pragma unroll
-      for (int s = 0; s < BK / 32; ++s) {
-        u32x4 fa[FM], fb[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) fa[i] = IA::frag(at, wm * WTM + i * 16, s, lane);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, s, lane);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
-                                                                __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
-      }
+      static_assert(BK == 64, "two k-steps per stage");
+      u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+      load(at, bt, 0, fa0, fb0);
+      lgkm_wait0();
+      lds_pin(fa0);
+      lds_pin(fb0);
+      load(at, bt, 1, fa1, fb1);
+      mma(fa0, fb0);
+      lgkm_wait0();
+      lds_pin(fa1);
+      lds_pin(fb1);
+      mma(fa1, fb1);
     };
     constexpr int INFLIGHT = PA + PB;  // this wave's DMA instructions of one stage
     issue(0);
