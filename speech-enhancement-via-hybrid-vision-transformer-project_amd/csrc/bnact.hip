@@ -46,6 +46,19 @@ struct BnArgs {
   uint32_t site;
 };
 
+// CV per-channel constants p[c .. c+CV-1] as 16-byte vector loads (c is a
+// multiple of CV): scalar loads of them came out serialised one round trip
+// each (48 of them in the apply pass), a ~20 us floor on every launch
+template <int CV>
+__device__ __forceinline__ void load_cv(const float* __restrict__ p, int c, float* out) {
+#pragma unroll
+  for (int v = 0; v < CV / 4; ++v) {
+    const f32x4 x = *(const f32x4*)(p + c + 4 * v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[4 * v + e] = x[e];
+  }
+}
+
 // Dropout2d multipliers of channels c .. c+CV-1 of sample n (element index
 // n*C + c, a multiple of 4: one 64-bit hash yields four 16-bit uniforms)
 template <int CV>
@@ -73,11 +86,15 @@ __global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z,
   const int total = a.N * Ho * Wo * G;
   // a thread's channel group never changes (256 % G == 0, grid stride % G == 0)
   const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
-  float sc[CV], sh[CV];
+  float sc[CV], sh[CV], mu_[CV], is_[CV], ga_[CV], be_[CV];
+  load_cv<CV>(a.mean, c, mu_);
+  load_cv<CV>(a.invstd, c, is_);
+  load_cv<CV>(a.gamma, c, ga_);
+  load_cv<CV>(a.beta, c, be_);
 #pragma unroll
   for (int e = 0; e < CV; ++e) {
-    sc[e] = a.invstd[c + e] * a.gamma[c + e];
-    sh[e] = a.beta[c + e] - a.mean[c + e] * sc[e];
+    sc[e] = is_[e] * ga_[e];
+    sh[e] = be_[e] - mu_[e] * sc[e];
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     int t = i / G;
@@ -132,18 +149,22 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
   const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
   // sc, sh: relu(bn(z)) = max(z*sc + sh, 0).  Reduce pass: xhat = (z - mu)*is.
   // Apply pass (training): dz = sc*(g - s1 - xhat*s2) = sc*g + ca + cb*z.
-  float sc[CV], sh[CV], mu[CV], is[CV], ca[CV], cb[CV];
+  float sc[CV], sh[CV], mu[CV], is[CV], ca[CV], cb[CV], ga_[CV], be_[CV], s1v[CV], s2v[CV];
+  load_cv<CV>(a.mean, c, mu);
+  load_cv<CV>(a.invstd, c, is);
+  load_cv<CV>(a.gamma, c, ga_);
+  load_cv<CV>(a.beta, c, be_);
+  load_cv<CV>(sums, c, s1v);        // (reduce pass: zeroed accumulators, unused)
+  load_cv<CV>(sums + a.C, c, s2v);
+  const bool use_s = APPLY && training;
 #pragma unroll
   for (int e = 0; e < CV; ++e) {
-    const float m_ = a.mean[c + e], i_ = a.invstd[c + e];
-    sc[e] = i_ * a.gamma[c + e];
-    sh[e] = a.beta[c + e] - m_ * sc[e];
-    mu[e] = m_;
-    is[e] = i_;
-    const float s1 = (APPLY && training) ? sums[c + e] * invM : 0.f;
-    const float s2 = (APPLY && training) ? sums[a.C + c + e] * invM : 0.f;
-    cb[e] = -sc[e] * s2 * i_;
-    ca[e] = -sc[e] * s1 - cb[e] * m_;
+    sc[e] = is[e] * ga_[e];
+    sh[e] = be_[e] - mu[e] * sc[e];
+    const float s1 = use_s ? s1v[e] * invM : 0.f;
+    const float s2 = use_s ? s2v[e] * invM : 0.f;
+    cb[e] = -sc[e] * s2 * is[e];
+    ca[e] = -sc[e] * s1 - cb[e] * mu[e];
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     int t = i / G;
@@ -273,13 +294,15 @@ __global__ __launch_bounds__(256) void bnact_sums_kernel(const T* __restrict__ z
   const int Ho = a.H / P, Wo = a.W / P;
   const int total = a.N * Ho * Wo * G;  // full windows only
   const int c = ((blockIdx.x * blockDim.x + threadIdx.x) % G) * CV;
-  float sc[CV], sh[CV], mu[CV], is[CV], acc1[CV], acc2[CV];
+  float sc[CV], sh[CV], mu[CV], is[CV], acc1[CV], acc2[CV], ga_[CV], be_[CV];
+  load_cv<CV>(a.mean, c, mu);
+  load_cv<CV>(a.invstd, c, is);
+  load_cv<CV>(a.gamma, c, ga_);
+  load_cv<CV>(a.beta, c, be_);
 #pragma unroll
   for (int e = 0; e < CV; ++e) {
-    mu[e] = a.mean[c + e];
-    is[e] = a.invstd[c + e];
-    sc[e] = is[e] * a.gamma[c + e];
-    sh[e] = a.beta[c + e] - mu[e] * sc[e];
+    sc[e] = is[e] * ga_[e];
+    sh[e] = be_[e] - mu[e] * sc[e];
     acc1[e] = acc2[e] = 0.f;
   }
   struct Item {
@@ -386,6 +409,8 @@ constexpr long BN_GRID_FWD = 2048, BN_GRID_SUMS = 2048, BN_GRID_APPLY = 1024;
 static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const float* mean, const float* invstd,
                      const float* gamma, const float* beta, const hvit_dropout_t* dr, int cv) {
   HVIT_CHECK(mean && invstd && gamma && beta, "bn_act: null statistics / affine pointer");
+  HVIT_CHECK(aligned16(mean) && aligned16(invstd) && aligned16(gamma) && aligned16(beta),
+             "bn_act: statistics / affine vectors must be 16-byte aligned");
   HVIT_CHECK(pool == 1 || pool == 2, "bn_act: pool must be 1 or 2");
   HVIT_CHECK(C > 0 && C % cv == 0 && (C / cv) <= 256 && (256 % (C / cv)) == 0,
              "bn_act: C=%d must be a multiple of %d with C/%d dividing 256", C, cv, cv);
