@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z,
         float v[CV];
         V16<T>::load(z + ((size_t)(n * a.H + oy * a.pool + dy) * a.W + ox * a.pool + dx) * a.C + c, v);
 #pragma unroll
-        for (int e = 0; e < CV; ++e) best[e] = fmaxf(best[e], v[e] * sc[e] + sh[e]);
+        for (int e = 0; e < CV; ++e) best[e] = fmaxf(best[e], __builtin_fmaf(v[e], sc[e], sh[e]));
       }
     float m[CV];
     drop_mask<CV>(a, n, c, m);
@@ -127,7 +127,11 @@ __global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z,
   }
 }
 
-// backward: APPLY = false -> per-channel sums; APPLY = true -> dz
+// backward: APPLY = false -> per-channel sums; APPLY = true -> dz.  The
+// window values are formed with one explicit fma each (forward, reduce and
+// apply alike): equal inputs must give equal values so that a tie routes to
+// the first maximum, as torch's max-pool does (compiler-chosen contraction
+// made tied bf16 inputs differ by an ulp and move the gradient)
 template <typename T, typename TD, bool APPLY>
 __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z, const TD* __restrict__ dy,
                                                        BnArgs a, float* __restrict__ sums, int training,
@@ -202,11 +206,11 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
       drop_mask<CV>(a, n, c, m);
 #pragma unroll
       for (int e = 0; e < CV; ++e) {
-        float best = fmaxf(zv[0][e] * sc[e] + sh[e], 0.f);
+        float best = fmaxf(__builtin_fmaf(zv[0][e], sc[e], sh[e]), 0.f);
 #pragma unroll
         for (int q = 1; q < MAXW; ++q) {
           if (!inb[q]) continue;
-          const float v = fmaxf(zv[q][e] * sc[e] + sh[e], 0.f);
+          const float v = fmaxf(__builtin_fmaf(zv[q][e], sc[e], sh[e]), 0.f);
           if (v > best) {
             best = v;
             arg[e] = q;
@@ -335,12 +339,12 @@ __global__ __launch_bounds__(256) void bnact_sums_kernel(const T* __restrict__ z
 #pragma unroll
     for (int e = 0; e < CV; ++e) {
       float zs = raw_elem<T>(it.zr[0], e);
-      float best = fmaxf(zs * sc[e] + sh[e], 0.f);
+      float best = fmaxf(__builtin_fmaf(zs, sc[e], sh[e]), 0.f);
 #pragma unroll
       for (int q = 1; q < MAXW; ++q) {
         if (q >= P * P) break;
         const float zq = raw_elem<T>(it.zr[q], e);
-        const float v = fmaxf(zq * sc[e] + sh[e], 0.f);
+        const float v = fmaxf(__builtin_fmaf(zq, sc[e], sh[e]), 0.f);
         if (v > best) {  // first maximum wins ties (torch's max-pool routing)
           best = v;
           zs = zq;
