@@ -156,11 +156,11 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_fwd_kernel(const T* __restric
 #pragma unroll
       for (int o2 = 8; o2 > 0; o2 >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
       float mn = fmaxf(mrow[r], mx);
-      alpha[r] = exp2f(mrow[r] - mn);
+      alpha[r] = __builtin_amdgcn_exp2f(mrow[r] - mn);
       float sum = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float p = exp2f(s[j][r] - mn);
+        float p = __builtin_amdgcn_exp2f(s[j][r] - mn);
         sum += p;
         s[j][r] = p;
       }
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dq_kernel(const T* __restrict
       for (int r = 0; r < 4; ++r) {
         int qi = q0 + 4 * fq + r, kj = k0 + 16 * j + frow;
         bool valid = qi < N && kj < N;
-        float p = valid ? exp2f(s[j][r] * c2 - lse2[r]) : 0.f;
+        float p = valid ? __builtin_amdgcn_exp2f(s[j][r] * c2 - lse2[r]) : 0.f;
         bool keep = true;
         if (thr && valid) keep = rng_keep(seed, site, (bh * N + qi) * (uint64_t)N + kj, thr);
         if (PROBS) {
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_kernel(const T* __restric
       for (int r = 0; r < 4; ++r) {
         int kj = key0 + 4 * fq + r;
         bool valid = qi < N && kj < N;
-        float p = valid ? exp2f(s[j][r] * c2 - l2) : 0.f;
+        float p = valid ? __builtin_amdgcn_exp2f(s[j][r] * c2 - l2) : 0.f;
         bool keep = true;
         if (thr && valid) keep = rng_keep(seed, site, (bh * N + qi) * (uint64_t)N + kj, thr);
         float pd = thr ? (keep ? p * dscale : 0.f) : p;
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
     if (j < nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(st[j][r] - mx);
+        const float p = __builtin_amdgcn_exp2f(st[j][r] - mx);
         st[j][r] = p;
         sum += p;
       }
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool valid = qv && (16 * j + 4 * fq + r < N);
-        const float p = valid ? exp2f(s[r] * c2 - lse2) : 0.f;
+        const float p = valid ? __builtin_amdgcn_exp2f(s[r] * c2 - lse2) : 0.f;
         ds2[u][r] = p * (dp[r] * keep[r] - dl);
       }
     }
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
       for (int r = 0; r < 4; ++r) {
         const int qi = 16 * j + 4 * fq + r;
         const bool valid = kv && qi < N;
-        const float p = valid ? exp2f(s[r] * c2 - Ls[qi]) : 0.f;
+        const float p = valid ? __builtin_amdgcn_exp2f(s[r] * c2 - Ls[qi]) : 0.f;
         float kp = 1.f;
         if (thr) {
           const int src = (lane & ~3) | r;

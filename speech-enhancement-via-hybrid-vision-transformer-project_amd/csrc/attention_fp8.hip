@@ -178,7 +178,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
     if (j < nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(st[j][r] - mx);
+        const float p = __builtin_amdgcn_exp2f(st[j][r] - mx);
         st[j][r] = p;
         sum += p;
       }
