@@ -573,11 +573,7 @@ __device__ __forceinline__ v4s_t v2_pack(f32x4 v) {
 __device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uint32_t thr, float dscale,
                                          unsigned long long seed, uint32_t site) {
   const uint64_t idx = (bh * N + qi) * (uint64_t)N + kj;
-  const uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
-  f32x4 k;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) k[e] = ((uint32_t)(h >> (16 * e)) & 0xffffu) >= thr ? dscale : 0.f;
-  return k;
+  return keep4_at(rng_key(seed, site), idx, thr, dscale);
 }
 
 // forward: workgroup = (b, h, 16*WAVES queries); wave = 16 queries x all keys.
@@ -827,14 +823,15 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
       dp = v2_mma32(v2_fragj(Ds, LN, j, 0), vf[0], dp);
       dp = v2_mma32(v2_fragj(Ds, LN, j, 1), vf[1], dp);
       // dropout: lane (quad position c = key & 3) hashes query row 16j+4fq+c of
-      // its key group; the quad exchanges the 16-bit slices (4 queries x 4 keys)
+      // its key group (two pair hashes); the quad exchanges the 16-bit slices
+      // (4 queries x 4 keys)
       uint32_t hlo = 0u, hhi = 0u;
       if (thr) {
         const int qc = 16 * j + 4 * fq + (frow & 3);
         const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
-        const uint64_t hv = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
-        hlo = (uint32_t)hv;
-        hhi = (uint32_t)(hv >> 32);
+        const uint32_t rk = rng_key(seed, site);
+        hlo = rng_pair(rk, idx);      // keys (key & ~3) + 0, 1
+        hhi = rng_pair(rk, idx + 2);  // keys (key & ~3) + 2, 3
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

@@ -66,11 +66,7 @@ __device__ __forceinline__ uint2 to_f8(const u32x4& u, float s) {
 __device__ __forceinline__ f32x4 keep4q(uint64_t bh, int N, int qi, int kj, uint32_t thr, float dscale,
                                        unsigned long long seed, uint32_t site) {
   const uint64_t idx = (bh * N + qi) * (uint64_t)N + kj;
-  const uint64_t hv = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
-  f32x4 k;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) k[e] = ((uint32_t)(hv >> (16 * e)) & 0xffffu) >= thr ? dscale : 0.f;
-  return k;
+  return keep4_at(rng_key(seed, site), idx, thr, dscale);
 }
 
 template <int WAVES>

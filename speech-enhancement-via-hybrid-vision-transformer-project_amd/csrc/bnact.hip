@@ -42,8 +42,7 @@ struct BnArgs {
   const float* beta;
   uint32_t thr;
   float dscale;
-  unsigned long long seed;
-  uint32_t site;
+  uint32_t key;  // rng_key(seed, site)
 };
 
 // CV per-channel constants p[c .. c+CV-1] as 16-byte vector loads (c is a
@@ -60,7 +59,7 @@ __device__ __forceinline__ void load_cv(const float* __restrict__ p, int c, floa
 }
 
 // Dropout2d multipliers of channels c .. c+CV-1 of sample n (element index
-// n*C + c, a multiple of 4: one 64-bit hash yields four 16-bit uniforms)
+// n*C + c, a multiple of 4: two pair hashes per four channels)
 template <int CV>
 __device__ __forceinline__ void drop_mask(const BnArgs& a, int n, int c, float* m) {
   if (!a.thr) {
@@ -71,9 +70,9 @@ __device__ __forceinline__ void drop_mask(const BnArgs& a, int n, int c, float* 
   const uint64_t i0 = (uint64_t)n * a.C + c;
 #pragma unroll
   for (int e4 = 0; e4 < CV; e4 += 4) {
-    const uint64_t h = mix64(a.seed ^ ((uint64_t)a.site << 48) ^ (((i0 + e4) >> 2) * 0xD6E8FEB86659FD93ull));
+    const f32x4 k = keep4_at(a.key, i0 + e4, a.thr, a.dscale);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) m[e4 + e] = ((uint32_t)(h >> (16 * e)) & 0xffffu) >= a.thr ? a.dscale : 0.f;
+    for (int e = 0; e < 4; ++e) m[e4 + e] = k[e];
   }
 }
 
@@ -423,8 +422,7 @@ static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const floa
   a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.beta = beta;
   a.thr = dr ? drop_threshold(dr->p) : 0;
   a.dscale = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-  a.seed = dr ? dr->seed : 0;
-  a.site = dr ? dr->site : 0;
+  a.key = dr ? rng_key(dr->seed, dr->site) : 0u;
   return HVIT_OK;
 }
 

@@ -78,21 +78,49 @@ __device__ __forceinline__ void st_dt(void* p, long i, float v, int dt) {
 }
 
 // ---------------------------------------------------------------- dropout RNG --
-// Counter-based: one 64-bit mix per group of four elements, 16 bits per element.
-// keep(i) == (u16(i) >= thr) with thr = round(p * 65536).  Forward and backward
-// regenerate identical masks from (seed, site, index).
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+// Counter-based, 32-bit per element pair:
+//   key       = fold32(splitmix64(seed ^ site << 48))     (once per launch: scalar unit)
+//   h(pair)   = lowbias32(key ^ (uint32)(idx >> 1))       (2 multiplies per 2 elements)
+//   u16(idx)  = (h >> 16 * (idx & 1)) & 0xffff
+//   keep(idx) = u16(idx) >= thr,  thr = round(p * 65536)
+// Forward and backward regenerate identical masks from (seed, site, index).  The
+// pair counter is 32 bits, so a site's mask is unique over its first 2^33
+// elements.  (Round 1 hashed a 64-bit splitmix per 4 elements: ~9 quarter-rate
+// 32-bit multiplies per group, which made dropout the largest VALU cost of the
+// attention and GEMM epilogues.)  Mirror: tests/conftest.py keep_mask.
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint32_t rng_u16(uint64_t seed, uint32_t site, uint64_t idx) {
-  uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ ((idx >> 2) * 0xD6E8FEB86659FD93ull));
-  return (uint32_t)(h >> (16 * (idx & 3))) & 0xffffu;
+__host__ __device__ inline uint32_t rng_key(uint64_t seed, uint32_t site) {
+  const uint64_t m = mix64(seed ^ ((uint64_t)site << 48));
+  return (uint32_t)(m ^ (m >> 32));
+}
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {  // lowbias32 (Wellons)
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  return x ^ (x >> 16);
+}
+// hash of the pair holding element idx (both 16-bit halves)
+__device__ __forceinline__ uint32_t rng_pair(uint32_t key, uint64_t idx) {
+  return hash32(key ^ (uint32_t)(idx >> 1));
+}
+__device__ __forceinline__ float keep_lo(uint32_t h, uint32_t thr, float ds) { return (h & 0xffffu) >= thr ? ds : 0.f; }
+__device__ __forceinline__ float keep_hi(uint32_t h, uint32_t thr, float ds) { return (h >> 16) >= thr ? ds : 0.f; }
+__device__ __forceinline__ uint32_t rng_u16k(uint32_t key, uint64_t idx) {
+  return (rng_pair(key, idx) >> (16 * (uint32_t)(idx & 1))) & 0xffffu;
 }
 __device__ __forceinline__ bool rng_keep(uint64_t seed, uint32_t site, uint64_t idx, uint32_t thr) {
-  return rng_u16(seed, site, idx) >= thr;
+  return rng_u16k(rng_key(seed, site), idx) >= thr;
+}
+// multipliers of 4 adjacent elements i0..i0+3 (i0 even): two pair hashes
+__device__ __forceinline__ f32x4 keep4_at(uint32_t key, uint64_t i0, uint32_t thr, float ds) {
+  const uint32_t h0 = rng_pair(key, i0), h1 = rng_pair(key, i0 + 2);
+  return (f32x4){keep_lo(h0, thr, ds), keep_hi(h0, thr, ds), keep_lo(h1, thr, ds), keep_hi(h1, thr, ds)};
 }
 static inline uint32_t drop_threshold(float p) {
   if (p <= 0.f) return 0;

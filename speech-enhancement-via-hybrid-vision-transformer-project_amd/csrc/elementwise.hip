@@ -84,9 +84,7 @@ __global__ void dropout_scale4_kernel(const void* g, int gdt, void* out, int odt
                   __uint_as_float(u.y & 0xffff0000u)};
     }
     if (thr) {
-      const uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ (((uint64_t)i >> 2) * 0xD6E8FEB86659FD93ull));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= thr) ? v[e] * ds : 0.f;
+      v *= keep4_at(rng_key(seed, site), (uint64_t)i, thr, ds);
     }
     if (rowscale) v *= rowscale[(i / N) / rps];
     if (odt == HVIT_F32) {
@@ -141,9 +139,7 @@ __global__ __launch_bounds__(DSC_THREADS) void dropout_scale4_colsum_kernel(cons
       if (base + k * stride >= total4) break;
       const int i = (base + k * stride) * 4;
       if (thr) {
-        const uint64_t h = mix64(seed ^ ((uint64_t)site << 48) ^ (((uint64_t)i >> 2) * 0xD6E8FEB86659FD93ull));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[k][e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= thr) ? v[k][e] * ds : 0.f;
+        v[k] *= keep4_at(rng_key(seed, site), (uint64_t)i, thr, ds);
       }
       if (rowscale) v[k] *= rowscale[(i / N) / rps];
       cs += v[k];

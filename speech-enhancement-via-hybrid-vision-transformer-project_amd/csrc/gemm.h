@@ -358,8 +358,7 @@ struct Epi {
   long ldaux = 0;
   uint32_t drop_thr = 0;  // dropout keep test (0 = off)
   float drop_scale = 1.f;
-  unsigned long long seed = 0;
-  uint32_t site = 0;
+  uint32_t drop_key = 0;  // rng_key(seed, site)
   const float* resid = nullptr;  // v = resid[m][n] + rowscale[m / rps] * v
   long ldr = 0;
   const float* rowscale = nullptr;
@@ -459,15 +458,11 @@ __device__ __forceinline__ f32x4 load4v(const void* p, long off, int nv, int dt)
   }
 }
 
-// dropout multipliers of 4 adjacent elements (index i0 = m*N + n, i0 % 4 == 0):
-// one 64-bit hash gives the four 16-bit uniforms
+// dropout multipliers of 4 adjacent elements (index i0 = m*N + n, i0 even):
+// two pair hashes give the four 16-bit uniforms
 __device__ __forceinline__ f32x4 keep4(const Epi& ep, int m, int n, int N) {
   const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-  const uint64_t h = mix64(ep.seed ^ ((uint64_t)ep.site << 48) ^ ((i0 >> 2) * 0xD6E8FEB86659FD93ull));
-  f32x4 k;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) k[e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= ep.drop_thr) ? ep.drop_scale : 0.f;
-  return k;
+  return keep4_at(ep.drop_key, i0, ep.drop_thr, ep.drop_scale);
 }
 
 // Inputs the epilogue reads besides the accumulator, loaded for all of a
@@ -497,13 +492,13 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, 
   float keep[4] = {1.f, 1.f, 1.f, 1.f};
   if (ep.drop_thr) {
     const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-    if (FAST || (i0 & 3) == 0) {
-      uint64_t h = mix64(ep.seed ^ ((uint64_t)ep.site << 48) ^ ((i0 >> 2) * 0xD6E8FEB86659FD93ull));
+    if (FAST || (i0 & 1) == 0) {
+      const f32x4 k = keep4_at(ep.drop_key, i0, ep.drop_thr, ep.drop_scale);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) keep[e] = (((uint32_t)(h >> (16 * e)) & 0xffffu) >= ep.drop_thr) ? ep.drop_scale : 0.f;
+      for (int e = 0; e < 4; ++e) keep[e] = k[e];
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) keep[e] = rng_keep(ep.seed, ep.site, i0 + e, ep.drop_thr) ? ep.drop_scale : 0.f;
+      for (int e = 0; e < 4; ++e) keep[e] = rng_u16k(ep.drop_key, i0 + e) >= ep.drop_thr ? ep.drop_scale : 0.f;
     }
   } else if (ep.drop_scale != 1.f) {
 #pragma unroll

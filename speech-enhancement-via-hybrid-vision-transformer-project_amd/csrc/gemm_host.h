@@ -33,8 +33,7 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
   if (e->dropout.p > 0.f) {
     ep.drop_thr = drop_threshold(e->dropout.p);
     ep.drop_scale = 1.f / (1.f - e->dropout.p);
-    ep.seed = e->dropout.seed;
-    ep.site = e->dropout.site;
+    ep.drop_key = rng_key(e->dropout.seed, e->dropout.site);
   }
   ep.resid = e->resid;
   ep.ldr = ldo;

@@ -38,12 +38,29 @@ def _mix64(z):
         return z ^ (z >> np.uint64(31))
 
 
-def keep_mask(seed, site, n, p):
-    """Boolean keep mask for element indices 0..n-1 (same as rng_keep)."""
-    idx = np.arange(n, dtype=np.uint64)
+def _hash32(x):
+    """lowbias32 on uint32 arrays (csrc/common.h hash32)."""
+    x = x.astype(np.uint32)
     with np.errstate(over="ignore"):
-        h = _mix64(np.uint64(seed) ^ (np.uint64(site) << np.uint64(48)) ^
-                   ((idx >> np.uint64(2)) * np.uint64(0xD6E8FEB86659FD93)))
-    u16 = (h >> (np.uint64(16) * (idx & np.uint64(3)))) & np.uint64(0xFFFF)
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x7FEB352D)
+        x ^= x >> np.uint32(15)
+        x *= np.uint32(0x846CA68B)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def rng_key(seed, site):
+    m = int(_mix64(np.uint64(seed) ^ (np.uint64(site) << np.uint64(48))))
+    return np.uint32((m ^ (m >> 32)) & 0xFFFFFFFF)
+
+
+def keep_mask(seed, site, n, p):
+    """Boolean keep mask for element indices 0..n-1 (same as rng_keep):
+    one lowbias32 hash per element pair, 16 bits per element."""
+    idx = np.arange(n, dtype=np.uint64)
+    pair = (idx >> np.uint64(1)).astype(np.uint32)  # 32-bit pair counter (wraps past 2^33)
+    h = _hash32(rng_key(seed, site) ^ pair)
+    u16 = (h >> (np.uint32(16) * (idx & np.uint64(1)).astype(np.uint32))) & np.uint32(0xFFFF)
     thr = 0 if p <= 0 else min(65536, int(p * 65536.0 + 0.5))
-    return u16 >= np.uint64(thr)
+    return u16 >= np.uint32(thr)
