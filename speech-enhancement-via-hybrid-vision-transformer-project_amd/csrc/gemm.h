@@ -603,6 +603,15 @@ __device__ __forceinline__ void lds_pin(u32x4 (&f)[NF]) {
   for (int i = 0; i < NF; ++i) asm volatile("" : "+v"(f[i]));
 }
 __device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Epilogue barrier over LDS only: the tile image and reduction scratch are the
+// only data shared between waves there.  __syncthreads() is a workgroup
+// release/acquire fence as well, which makes every wave wait (vmcnt(0)) for
+// all of its output stores to land before the next half can be staged.
+__device__ __forceinline__ void epi_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 template <typename T, int R, bool KC>
 struct TileCfg {
@@ -1144,7 +1153,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
     };
 #pragma unroll
     for (int hh = 0; hh < HALVES; ++hh) {
-      if (hh > 0) __syncthreads();
+      if (hh > 0) epi_barrier();
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1154,7 +1163,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
             const int row = wm * WTM + i * 16 + fq * 4 + r - hh * 64;
             if (row >= 0 && row < 64) Cs[row * CP + wn * WTN + j * 16 + frow] = acc[i][j][r];
           }
-      __syncthreads();
+      epi_barrier();
       const int mbase = m0 + hh * 64;
       f32x4 ra[NR8], rb[NR8];
       float rsc[NR8];
@@ -1230,10 +1239,10 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
     }
     if (ep.colsum) {
       float* red = Cs + 64 * CP;  // [RS8][BN]
-      __syncthreads();
+      epi_barrier();
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[q0 * BN + c8 * 8 + e] = cs8[e];
-      __syncthreads();
+      epi_barrier();
       if (q0 == 0)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -1253,12 +1262,13 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
   // and coalesced, and every acc[][] index stays static (no scratch).  Halves
   // whose rows and columns are all in range take a branch-free row loop.
   static_assert((64 * CP + RSTEP * BN) * 4 <= (int)sizeof(smem), "epilogue tile exceeds LDS");
+  static_assert(2 * RSTEP * BN <= 64 * CP, "BN statistics scratch exceeds the tile image");
   float* Cs = (float*)smem;
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int hh = 0; hh < HALVES; ++hh) {
-    if (hh > 0) __syncthreads();
+    if (hh > 0) epi_barrier();
     // write this half's accumulators: wave rows wm*WTM + i*16 + fq*4 + r
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -1269,11 +1279,12 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
           const int row = wm * WTM + i * 16 + fq * 4 + r - hh * 64;
           if (row >= 0 && row < 64) Cs[row * CP + wn * WTN + j * 16 + frow] = acc[i][j][r];
         }
-    __syncthreads();
+    epi_barrier();
     const int mbase = m0 + hh * 64;
     const int rows_here = min(64, M - mbase);
     const bool all_in = mbase + 64 <= M && n0 + BN <= N && ep.vec_ok;  // uniform
     float st_sum[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 sv[NR];  // BN statistics: this thread's output values (registers, no Cs re-read)
 
     auto rows = [&](auto pred) {
       constexpr bool PRED = decltype(pred)::value;
@@ -1309,7 +1320,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
             csum[e] += v[e];
             st_sum[e] += v[e];
           }
-          if (ep.stats) *(f32x4*)(Cs + row * CP + c4 * 4) = v;
+          sv[i] = v;
         }
       } else if constexpr (EK == EK_GELU_DUAL) {
         // h = v + b (saved for backward), a = dropout(gelu(h))
@@ -1409,7 +1420,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
               st_sum[e] += v[e];
             }
           }
-          *(f32x4*)(Cs + row * CP + c4 * 4) = v;
+          sv[i] = v;
         }
       }
     };
@@ -1420,42 +1431,73 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
       else rows(std::true_type());
     }
     if (ep.stats && rows_here > 0) {
-      // per-column (mean, M2) of this 64-row sub-tile: sums -> mean -> M2
-      float* red = Cs + 64 * CP;  // [RSTEP][BN] scratch after the tile
-      __syncthreads();
-      for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = st_sum[e];
-      __syncthreads();
+      // per-column (mean, M2) of this 64-row sub-tile.  Each thread holds its
+      // rows r0 + i*RSTEP (i < cnt) of 4 columns in registers: local mean and
+      // M2 there; the RSTEP partials of a column are then merged by one thread
+      // per column (r0 < 4 picks column n + r0), 128 columns in parallel.  Full
+      // halves (every partial over NR rows) merge without divisions:
+      //   mean = sum(m_k) / RSTEP,  M2 = sum(M2_k) + NR sum((m_k - mean)^2);
+      // ragged ones by Chan's pairwise rule.  (A single-wave sequential merge
+      // with IEEE divisions cost ~1.5 us per tile, 34 us of the enc1 conv.)
+      const bool fullh = rows_here == 64;  // uniform
+      const int cnt = fullh ? NR : (rows_here > r0 ? min(NR, (rows_here - r0 + RSTEP - 1) / RSTEP) : 0);
+      const float inv = fullh ? 1.f / (float)NR : (cnt ? 1.f / (float)cnt : 0.f);
       float mean[4], q[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int e = 0; e < 4; ++e) {
-        float s = 0.f;
-        for (int k = 0; k < RSTEP; ++k) s += red[k * BN + c4 * 4 + e];
-        mean[e] = s / (float)rows_here;
-      }
-      for (int row = r0; row < rows_here; row += RSTEP)
-        for (int e = 0; e < 4; ++e) {
-          float d = Cs[row * CP + c4 * 4 + e] - mean[e];
-          q[e] += d * d;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mean[e] = st_sum[e] * inv;
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+        if (fullh || i < cnt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = sv[i][e] - mean[e];
+            q[e] += d * d;
+          }
+      float* red = Cs;  // [2][RSTEP][BN]; the tile's LDS image is no longer read
+      epi_barrier();
+      *(f32x4*)(red + r0 * BN + c4 * 4) = (f32x4){mean[0], mean[1], mean[2], mean[3]};
+      *(f32x4*)(red + (RSTEP + r0) * BN + c4 * 4) = (f32x4){q[0], q[1], q[2], q[3]};
+      epi_barrier();
+      if (r0 < 4 && n + r0 < N) {
+        const int col = c4 * 4 + r0;
+        float mk[RSTEP], qs = 0.f, mu = 0.f, m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < RSTEP; ++k) {
+          mk[k] = red[k * BN + col];
+          qs += red[(RSTEP + k) * BN + col];
         }
-      __syncthreads();
-      for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = q[e];
-      __syncthreads();
-      if (r0 == 0) {
+        if (fullh) {
+#pragma unroll
+          for (int k = 0; k < RSTEP; ++k) mu += mk[k];
+          mu *= 1.f / (float)RSTEP;
+          float dd = 0.f;
+#pragma unroll
+          for (int k = 0; k < RSTEP; ++k) dd += (mk[k] - mu) * (mk[k] - mu);
+          m2 = qs + (float)NR * dd;
+        } else {
+          float na = 0.f;
+          m2 = qs;
+#pragma unroll
+          for (int k = 0; k < RSTEP; ++k) {
+            const int ck = rows_here > k ? min(NR, (rows_here - k + RSTEP - 1) / RSTEP) : 0;
+            if (ck == 0) continue;
+            const float nn = na + (float)ck, wb = (float)ck / nn;
+            const float d = mk[k] - mu;
+            mu += d * wb;
+            m2 += d * d * (na * wb);
+            na = nn;
+          }
+        }
         const long tile = (m0 / 64) + hh;
-        for (int e = 0; e < 4; ++e) {
-          if (n + e >= N) break;
-          float s = 0.f;
-          for (int k = 0; k < RSTEP; ++k) s += red[k * BN + c4 * 4 + e];
-          ep.stats[(tile * N + n + e) * 2] = mean[e];
-          ep.stats[(tile * N + n + e) * 2 + 1] = s;
-        }
+        *(float2*)(ep.stats + (tile * N + n + r0) * 2) = make_float2(mu, m2);
       }
     }
   }
   if (ep.colsum) {
     float* red = Cs + 64 * CP;
-    __syncthreads();
+    epi_barrier();
     for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = csum[e];
-    __syncthreads();
+    epi_barrier();
     if (r0 == 0)
       for (int e = 0; e < 4; ++e) {
         if (n + e >= N) break;

@@ -31,9 +31,11 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
     HVIT_CHECK(la.Ho > 0 && la.Wo > 0, "hvit_conv_fwd: empty output");
     int Kt = la.Kt;
     if constexpr (sizeof(T) == 2) {
+      // HVIT_CONV_FWD_TILE = 128 / 12864 / 64 forces the tile (A/B measurements only)
+      static const int ft = getenv("HVIT_CONV_FWD_TILE") ? atoi(getenv("HVIT_CONV_FWD_TILE")) : 0;
       if (conv_fast_ok(la, g->N))
         return launch_gemm<T>(conv_fast(la, g->N), dense<T, true>(w_packed, Kt, g->Cout, Kt), la.P, g->Cout, Kt, 1,
-                              ep, (hipStream_t)stream);
+                              ep, (hipStream_t)stream, ft);
     }
     // odd reduction length (Cin=1 first conv): weights take the scalar load path
     return launch_gemm<T>(la, dense<T, true>(w_packed, Kt, g->Cout, Kt), la.P, g->Cout, Kt, 1, ep,

@@ -523,12 +523,15 @@ def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):
     return dx, dgw, dgb
 
 
-def droppath_scale(B, p, seed, site, dev):
+def droppath_scales(B, p, seed, dev):
+    """DropPath (components.py:407-427) multipliers of a block's two residual
+    branches from one launch: keep(seed, site 1, b) for the attention branch,
+    keep(seed, site 1, B + b) for the MLP branch."""
     if p <= 0:
-        return None
-    out = torch.empty(B, dtype=torch.float32, device=dev)
-    call("hvit_droppath_scale", B, L.dropout(p, seed, site), out.data_ptr(), stream_ptr())
-    return out
+        return None, None
+    out = torch.empty(2 * B, dtype=torch.float32, device=dev)
+    call("hvit_droppath_scale", 2 * B, L.dropout(p, seed, 1), out.data_ptr(), stream_ptr())
+    return out[:B], out[B:]
 
 
 class ViTBlockFn(torch.autograd.Function):
@@ -549,8 +552,7 @@ class ViTBlockFn(torch.autograd.Function):
         scale = hd ** -0.5
         x2d = x.contiguous().view(M, D)
         d_attn, d_proj, d_fc1, d_fc2, dp_seed = drops if training else (Drop(),) * 4 + (0,)
-        rs1 = droppath_scale(B, dpr if training else 0.0, dp_seed, 1, dev)
-        rs2 = droppath_scale(B, dpr if training else 0.0, dp_seed, 2, dev)
+        rs1, rs2 = droppath_scales(B, dpr if training else 0.0, dp_seed, dev)
         xn1, m1, r1 = _ln(x2d, n1w, n1b, dt)
         Wqkv = cast(qkvw, dt)
         qkv = _empty((M, 3 * D), dt, dev)

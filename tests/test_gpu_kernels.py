@@ -525,8 +525,8 @@ def test_vit_block_droppath_matches_torch(hv):
                                m[3].bias, H, drops, 0.5, True, hv._lib.F32, False)
     g = torch.randn_like(y)
     (y * g).sum().backward()
-    k1 = torch.as_tensor(keep_mask(seed, 1, B, 0.5), device=DEV).float() / 0.5
-    k2 = torch.as_tensor(keep_mask(seed, 2, B, 0.5), device=DEV).float() / 0.5
+    kk = torch.as_tensor(keep_mask(seed, 1, 2 * B, 0.5), device=DEV).float() / 0.5  # both branches, one launch
+    k1, k2 = kk[:B], kk[B:]
     assert 0 < k1.count_nonzero() < B and 0 < k2.count_nonzero() < B  # both outcomes occur
 
     xr = x.detach().clone().requires_grad_(True)
