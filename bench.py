@@ -16,7 +16,8 @@ of the same steps records HIP events around every launch of each op class
 (functional.timed) on the stream it runs on; ``op_table`` lists each class's
 GPU time per step and algorithmic FLOP/s (or bytes/s) against its roofline,
 and ``roofline`` is the class with the most GPU time (the ViT linear
-weight-gradient GEMMs at the default config).  ``cpu_baseline`` times the CPU
+weight-gradient GEMMs at the default config; ``traffic`` from the committed
+PMC pass, profiles/roofline_pmc.json).  ``cpu_baseline`` times the CPU
 oracle (oracle/, fp32 PyTorch restatement of the reference) on a bounded
 sample of the same step, on this host's cores.
 """
@@ -55,7 +56,7 @@ def parse():
                     help="fp8: e4m3 MFMA attention forward (BASELINE config 5), bf16 attention backward")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant op class, re-run in isolation (rocprofv3 --pmc passes)")
-    ap.add_argument("--roofline-op", default="conv_wgrad",
+    ap.add_argument("--roofline-op", default="vit_linear_wgrad",
                     help="op class for --roofline-only (functional.timed tag with a recorded replay)")
     a = ap.parse_args()
     if a.batch is None:

@@ -309,7 +309,8 @@ def attn_ref(qkv, B, N, H, hd, p=0.0, mask=None):
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("B,N,H,hd,p", [(2, 256, 8, 64, 0.0), (1, 240, 8, 64, 0.1), (2, 16, 4, 16, 0.0),
-                                        (1, 4, 4, 16, 0.2), (3, 100, 2, 32, 0.0), (2, 300, 2, 64, 0.1)])
+                                        (1, 4, 4, 16, 0.2), (3, 100, 2, 32, 0.0), (2, 300, 2, 64, 0.1),
+                                        (2, 228, 4, 64, 0.1)])  # 228: pipelined staging, odd tile count
 def test_mhsa_fwd_bwd(hv, dt, B, N, H, hd, p):
     l = L(hv)
     D = H * hd

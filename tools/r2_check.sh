@@ -23,8 +23,8 @@ for s in $STEPS; do
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
     roofprof) timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof -o run --output-format csv -- \
-            python3 bench.py --roofline-only --roofline-op conv_wgrad > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $? ;;
-    pmc) bash tools/pmc_pass.sh ${TAG}_rpmc bench.py --roofline-only --roofline-op conv_wgrad || exit $? ;;
+            python3 bench.py --roofline-only --roofline-op ${ROOFOP:-vit_linear_wgrad} > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $? ;;
+    pmc) bash tools/pmc_pass.sh ${TAG}_rpmc bench.py --roofline-only --roofline-op ${ROOFOP:-vit_linear_wgrad} || exit $? ;;
     large) timeout -k 10 300 python -u bench.py --variant large --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_large_bf16.log 2>&1 || exit $?
            timeout -k 10 300 python -u bench.py --variant large --attn fp8 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_large_fp8.log 2>&1 || exit $?
            timeout -k 10 300 python -u bench.py --mode infer --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_infer.log 2>&1 || exit $? ;;
