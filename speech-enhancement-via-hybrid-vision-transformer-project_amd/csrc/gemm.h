@@ -857,7 +857,7 @@ struct DmaImg {
   }
 };
 
-template <int BM, int BN, bool KCA, bool KCB>
+template <int BM, int BN, bool KCA, bool KCB, int NB = 2>
 struct GemmCoreDma {
   using IA = DmaImg<BM, KCA>;
   using IB = DmaImg<BN, KCB>;
@@ -866,7 +866,8 @@ struct GemmCoreDma {
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
   static constexpr int PA = IA::PIECES / 4, PB = IB::PIECES / 4;  // pieces per wave per stage
-  static constexpr int SM_LOOP = 2 * (IA::BYTES + IB::BYTES);
+  static constexpr int SM_LOOP = NB * (IA::BYTES + IB::BYTES);
+  static_assert(NB == 1 || NB == 2, "one or two LDS stage buffers");
   static_assert(IA::PIECES % 4 == 0 && IB::PIECES % 4 == 0, "pieces per stage must split over 4 waves");
 
   template <class L>
@@ -896,7 +897,7 @@ struct GemmCoreDma {
 #pragma unroll
     for (int i = 0; i < PB; ++i) vb[i] = IB::src_off(wid + 4 * i, lane, lb.ld);
     auto issue = [&](int t) {
-      char* abuf = smem + (t & 1) * (IA::BYTES + IB::BYTES);
+      char* abuf = smem + (NB == 2 ? (t & 1) : 0) * (IA::BYTES + IB::BYTES);
       char* bbuf = abuf + IA::BYTES;
       const unsigned sa = oa + (unsigned)t * da, sb = ob + (unsigned)t * db;
 #pragma unroll
@@ -925,7 +926,7 @@ struct GemmCoreDma {
     // k-step 0's fragments, then k-step 1's reads in flight under k-step 0's
     // MFMAs (explicit lgkmcnt waits: the MN reads are asm, DmaImg::frag)
     auto compute = [&](int t) {
-      const char* at = smem + (t & 1) * (IA::BYTES + IB::BYTES);
+      const char* at = smem + (NB == 2 ? (t & 1) : 0) * (IA::BYTES + IB::BYTES);
       const char* bt = at + IA::BYTES;
       static_assert(BK == 64, "two k-steps per stage");
       u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
@@ -941,6 +942,23 @@ struct GemmCoreDma {
       mma(fa1, fb1);
     };
     constexpr int INFLIGHT = PA + PB;  // this wave's DMA instructions of one stage
+    if constexpr (NB == 1) {
+      // one stage buffer (the 3-workgroups-per-CU variant): no prefetch inside
+      // the workgroup; the co-resident workgroups, out of phase, keep the CU's
+      // DMA and matrix cores busy
+      for (int t = 0; t < nk; ++t) {
+        issue(t);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        compute(t);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      return;
+    }
     issue(0);
     for (int t = 0; t < nk; ++t) {
       if (t + 1 < nk) {
@@ -1012,8 +1030,10 @@ __device__ __forceinline__ TileId tile_of(int remap) {
   return {mt, rem - mt * gy, z};
 }
 
-template <typename T, int BM, int BN, class LA, class LB, int EK, bool RS = false, bool DMAK = false>
-__global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
+// DMAK: 0 = register-staged K loop, 2 = LDS-DMA with two stage buffers (two
+// workgroups per CU), 1 = LDS-DMA with one stage buffer (three per CU)
+template <typename T, int BM, int BN, class LA, class LB, int EK, bool RS = false, int DMAK = 0>
+__global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
                                                                                             int K, int kps, Epi ep) {
   // the implicit-im2col weight gradient streams both operands from HBM once:
   // deeper register prefetch (its 128x64 tiles have the registers for it)
@@ -1021,9 +1041,12 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
   constexpr int WM = C::WM, WN = C::WN, WTM = C::WTM, WTN = C::WTN, FM = C::FM, FN = C::FN;
   // LDS-DMA K loop (DMAK kernels): dense bf16 operands, no row sums
   constexpr bool DMA = sizeof(T) == 2 && IsDenseBf16<LA>::value && IsDenseBf16<LB>::value && !RS;
-  constexpr int SM_LOOP = C::SM_LOOP;
+  constexpr int SM_LOOP = DMAK == 1 ? GemmCoreDma<BM, BN, LA::KC, LB::KC, 1>::SM_LOOP : C::SM_LOOP;
   constexpr int SM_EPI = (64 * (BN + 4) + (GEMM_THREADS / (BN / 4)) * BN) * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI];
+  // the wide (8-column) epilogue's column-sum scratch follows the 64-row tile image
+  constexpr int SM_W8 = DMAK ? (64 * (BN + 4) + (GEMM_THREADS / (BN / 8)) * BN) * 4 : 0;
+  constexpr int SM_E = SM_EPI > SM_W8 ? SM_EPI : SM_W8;
+  __shared__ __attribute__((aligned(16))) char smem[SM_LOOP > SM_E ? SM_LOOP : SM_E];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1112,7 +1135,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (BM >= 128 ? HVIT_BIG_OCC : 2)) void 
     // is compiled into the kernel, so it keeps its own register budget)
     static_assert(DMA, "DMA-only kernel needs dense bf16 operands");
     (void)interior;
-    GemmCoreDma<BM, BN, LA::KC, LB::KC>::run(la, lb, smem, m0, n0, kbeg, kend, acc);
+    GemmCoreDma<BM, BN, LA::KC, LB::KC, DMAK == 1 ? 1 : 2>::run(la, lb, smem, m0, n0, kbeg, kend, acc);
   } else {
     if (interior) C::template run<false, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
     else C::template run<true, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
@@ -1616,7 +1639,20 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
         dim3 g(cdiv(M, BMc), cdiv(N, BNc), splits);
         if constexpr (DMA_OK && !RSc) {
           if (all_in) {
-            hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, true>), g, dim3(GEMM_THREADS), 0, st,
+            // one-buffer LDS-DMA kernels (3 workgroups per CU, out of phase, so one's
+            // epilogue overlaps another's K loop) for the 128x128 forward kinds:
+            // vit_linear_fwd 0.732 -> 0.721 ms/step.  Not for GELU_BWD (its h
+            // prefetch spills at 168 VGPRs: dgrad 0.737 -> 0.780).  HVIT_DMA1=0
+            // disables (A/B only)
+            static const bool nb1 = !getenv("HVIT_DMA1") || atoi(getenv("HVIT_DMA1"));
+            if constexpr (BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
+              if (nb1) {
+                hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 1>), g, dim3(GEMM_THREADS), 0, st,
+                                   la, lb, M, N, K, kps, ep);
+                return;
+              }
+            }
+            hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 2>), g, dim3(GEMM_THREADS), 0, st,
                                la, lb, M, N, K, kps, ep);
             return;
           }
