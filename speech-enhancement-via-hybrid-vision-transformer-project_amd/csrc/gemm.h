@@ -826,6 +826,11 @@ struct IsDenseBf16 : std::false_type {};
 template <bool KC>
 struct IsDenseBf16<LdDense<bf16_t, KC>> : std::true_type {};
 
+template <typename X>
+struct IsConvFBf16 : std::false_type {};
+template <>
+struct IsConvFBf16<LdConvF<bf16_t>> : std::true_type {};
+
 template <int R, bool KC>
 struct DmaImg {
   static constexpr int ROWB = KC ? KSTAGE : 2 * R;  // bytes per LDS row
@@ -878,32 +883,103 @@ struct GemmCoreDma {
                                              0x00020000);
   }
 
+  // A is a dense bf16 matrix or the implicit-im2col conv loader (LdConvF: A
+  // rows are output pixels, one 64-channel stage lies in one tap and one
+  // source).  For the conv, a lane's row in each of its A pieces is a fixed
+  // pixel (source row base, iy0, ix0 kept per piece), its 16-byte chunk a fixed
+  // 8-channel offset (the KC source swizzle depends on the lane only), and the
+  // stage's tap / channel base is wave-uniform: each stage's per-lane byte
+  // offset is a few integer ops, and taps in the zero padding (or past the
+  // tensor) get an offset past num_records, which the DMA reads as zeros.
   __device__ __forceinline__ static void run(const LdDense<bf16_t, KCA>& la, const LdDense<bf16_t, KCB>& lb,
                                              char* smem, int m0, int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN]) {
+    run_t(la, lb, smem, m0, n0, kbeg, kend, acc);
+  }
+  __device__ __forceinline__ static void run(const LdConvF<bf16_t>& la, const LdDense<bf16_t, KCB>& lb, char* smem,
+                                             int m0, int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN]) {
+    run_t(la, lb, smem, m0, n0, kbeg, kend, acc);
+  }
+  template <class LA>
+  __device__ __forceinline__ static void run_t(const LA& la, const LdDense<bf16_t, KCB>& lb, char* smem, int m0,
+                                               int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN]) {
+    constexpr bool CONV = IsConvFBf16<LA>::value;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
     const int nk = (kend - kbeg) / BK;
     if (nk <= 0) return;
-    const __amdgpu_buffer_rsrc_t ra = rsrc(la), rb = rsrc(lb);
-    // tile origin and per-stage advance (bytes, wave-uniform -> soffset)
-    const unsigned oa = (unsigned)(KCA ? ((long)m0 * la.ld + kbeg) * 2 : ((long)kbeg * la.ld + m0) * 2);
+    const __amdgpu_buffer_rsrc_t rb = rsrc(lb);
     const unsigned ob = (unsigned)(KCB ? ((long)n0 * lb.ld + kbeg) * 2 : ((long)kbeg * lb.ld + n0) * 2);
-    const unsigned da = (unsigned)(KCA ? BK * 2 : (long)BK * la.ld * 2);
     const unsigned db = (unsigned)(KCB ? BK * 2 : (long)BK * lb.ld * 2);
-    unsigned va[PA], vb[PB];
-#pragma unroll
-    for (int i = 0; i < PA; ++i) va[i] = IA::src_off(wid + 4 * i, lane, la.ld);
+    unsigned vb[PB];
 #pragma unroll
     for (int i = 0; i < PB; ++i) vb[i] = IB::src_off(wid + 4 * i, lane, lb.ld);
+    // dense A: per-lane source offsets and a uniform per-stage advance
+    __amdgpu_buffer_rsrc_t ra;
+    unsigned va[PA], oa = 0, da = 0;
+    // conv A: per-piece pixel state, the lane's chunk offset, the stage tap cursor
+    int crb[PA], ciy[PA], cix[PA], cl8 = 0, c0 = 0, kx = 0, ky = 0;
+    __amdgpu_buffer_rsrc_t ra2;
+    if constexpr (CONV) {
+      static_assert(KCA, "conv A operand is k-contiguous");
+      ra = __builtin_amdgcn_make_buffer_rsrc((void*)la.src1, (short)0, (int)la.bytes1, 0x00020000);
+      ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)la.src2, (short)0, (int)la.bytes2, 0x00020000);
+      cl8 = ((lane & 7) ^ ((lane >> 3) & 7)) << 3;
+      const int hw = la.Ho * la.Wo;
+#pragma unroll
+      for (int i = 0; i < PA; ++i) {
+        const int p = m0 + (wid + 4 * i) * IA::RPP + (lane >> 3);
+        const int n = p / hw, rem = p - n * hw;
+        const int oy = rem / la.Wo, ox = rem - oy * la.Wo;
+        crb[i] = n * la.Hs;
+        ciy[i] = oy * la.S - la.Pd;
+        cix[i] = ox * la.S - la.Pd;
+      }
+      const int kb = __builtin_amdgcn_readfirstlane(kbeg);
+      const int tap = kb / la.Ctot;
+      c0 = kb - tap * la.Ctot;
+      ky = tap / la.KS;
+      kx = tap - ky * la.KS;
+    } else {
+      ra = rsrc(la);
+      oa = (unsigned)(KCA ? ((long)m0 * la.ld + kbeg) * 2 : ((long)kbeg * la.ld + m0) * 2);
+      da = (unsigned)(KCA ? BK * 2 : (long)BK * la.ld * 2);
+#pragma unroll
+      for (int i = 0; i < PA; ++i) va[i] = IA::src_off(wid + 4 * i, lane, la.ld);
+    }
     auto issue = [&](int t) {
       char* abuf = smem + (NB == 2 ? (t & 1) : 0) * (IA::BYTES + IB::BYTES);
       char* bbuf = abuf + IA::BYTES;
-      const unsigned sa = oa + (unsigned)t * da, sb = ob + (unsigned)t * db;
+      const unsigned sb = ob + (unsigned)t * db;
+      if constexpr (CONV) {
+        const bool first = c0 < la.C1;  // uniform
+        const int Cx = first ? la.C1 : la.C2;
+        const int coff = (first ? c0 : c0 - la.C1) + cl8;
 #pragma unroll
-      for (int i = 0; i < PA; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(abuf + (wid + 4 * i) * 1024),
-                                                 16, va[i], sa, 0, 0);
+        for (int i = 0; i < PA; ++i) {
+          const int iy = ciy[i] + ky, ix = cix[i] + kx;
+          const bool ok = (unsigned)iy < (unsigned)la.Hi && (unsigned)ix < (unsigned)la.Wi;
+          const int off = (((crb[i] + (iy >> la.ushift)) * la.Ws + (ix >> la.ushift)) * Cx + coff) * 2;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(first ? ra : ra2,
+                                                   (__attribute__((address_space(3))) void*)(abuf + (wid + 4 * i) * 1024),
+                                                   16, ok ? (unsigned)off : 0x80000000u, 0, 0, 0);
+        }
+        c0 += BK;  // next stage's tap cursor (LdConvF::step_sh)
+        if (c0 >= la.Ctot) {
+          c0 -= la.Ctot;
+          if (++kx == la.KS) {
+            kx = 0;
+            ++ky;
+          }
+        }
+      } else {
+        const unsigned sa = oa + (unsigned)t * da;
+#pragma unroll
+        for (int i = 0; i < PA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ra,
+                                                   (__attribute__((address_space(3))) void*)(abuf + (wid + 4 * i) * 1024),
+                                                   16, va[i], sa, 0, 0);
+      }
 #pragma unroll
       for (int i = 0; i < PB; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(bbuf + (wid + 4 * i) * 1024),
@@ -1040,8 +1116,10 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
   using C = GemmCore<T, BM, BN, LA, LB, IsConvWF<LB>::value ? HVIT_WF_STAGES : 2>;
   constexpr int WM = C::WM, WN = C::WN, WTM = C::WTM, WTN = C::WTN, FM = C::FM, FN = C::FN;
   // LDS-DMA K loop (DMAK kernels): dense bf16 operands, no row sums
-  constexpr bool DMA = sizeof(T) == 2 && IsDenseBf16<LA>::value && IsDenseBf16<LB>::value && !RS;
-  constexpr int SM_LOOP = DMAK == 1 ? GemmCoreDma<BM, BN, LA::KC, LB::KC, 1>::SM_LOOP : C::SM_LOOP;
+  constexpr bool DMA =
+      sizeof(T) == 2 && (IsDenseBf16<LA>::value || IsConvFBf16<LA>::value) && IsDenseBf16<LB>::value && !RS;
+  constexpr int SM_DMA = DMAK ? GemmCoreDma<BM, BN, LA::KC, LB::KC, DMAK == 1 ? 1 : 2>::SM_LOOP : 0;
+  constexpr int SM_LOOP = DMAK == 1 ? SM_DMA : (C::SM_LOOP > SM_DMA ? C::SM_LOOP : SM_DMA);
   constexpr int SM_EPI = (64 * (BN + 4) + (GEMM_THREADS / (BN / 4)) * BN) * 4;
   // the wide (8-column) epilogue's column-sum scratch follows the 64-row tile image
   constexpr int SM_W8 = DMAK ? (64 * (BN + 4) + (GEMM_THREADS / (BN / 8)) * BN) * 4 : 0;
@@ -1102,7 +1180,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
   // stores of the 4-column layout made the epilogue store-issue bound:
   // measured 5.2 us of a 12 us fc1 tile).  Masks, math and results are the
   // 4-column epilogue's.
-  constexpr bool W8 = DMAK && (EK == EK_GELU_DUAL || EK == EK_GELU_BWD || EK == EK_STORE || EK == EK_RESID);
+  constexpr bool W8 = DMAK && IsDenseBf16<LA>::value && (EK == EK_GELU_DUAL || EK == EK_GELU_BWD || EK == EK_STORE || EK == EK_RESID);
   constexpr int C8 = BN / 8, RS8 = GEMM_THREADS / C8, NR8 = 64 / RS8;
   const int c8 = tid % C8, q0 = tid / C8;
   const int n8 = n0 + c8 * 8;
@@ -1620,14 +1698,22 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
   }
   // DMA-only kernel: dense bf16 operands, every tile interior (M, N multiples of
   // the tile, every K slice a multiple of 64, vector-aligned operands)
-  constexpr bool DMA_OK = sizeof(T) == 2 && IsDenseBf16<LA>::value && IsDenseBf16<LB>::value;
+  // (or the implicit-im2col conv A loader, LdConvF: every 64-channel stage in
+  // one tap and one source, byte offsets < 2^31 -- conv_fast_ok)
+  constexpr bool CONV_A = IsConvFBf16<LA>::value;
+  constexpr bool DMA_OK = sizeof(T) == 2 && (IsDenseBf16<LA>::value || CONV_A) && IsDenseBf16<LB>::value;
   bool all_in = false;
   if constexpr (DMA_OK) {
     const int bm = tile == 128 || tile == 12864 ? 128 : 64, bn = tile == 128 ? 128 : 64;
     // both operands k-major (the weight gradients): the register path measured
     // faster (1.04 vs 0.82 ms/step); HVIT_DMA_MNMN=1 forces DMA there (A/B only)
     static const bool mnmn = getenv("HVIT_DMA_MNMN") && atoi(getenv("HVIT_DMA_MNMN"));
-    all_in = ep.dma && M % bm == 0 && N % bn == 0 && kps % 64 == 0 && K % kps == 0 && la.vok && lb.vok &&
+    // HVIT_CONV_DMA=0: conv A operands on the register-staged loop (A/B only)
+    static const bool conv_dma = !getenv("HVIT_CONV_DMA") || atoi(getenv("HVIT_CONV_DMA"));
+    bool a_ok;
+    if constexpr (CONV_A) a_ok = conv_dma;
+    else a_ok = la.vok;
+    all_in = ep.dma && M % bm == 0 && N % bn == 0 && kps % 64 == 0 && K % kps == 0 && a_ok && lb.vok &&
              !ep.rs_ptr && (LA::KC || LB::KC || mnmn);
   }
   auto go = [&](auto ekc) {
@@ -1645,7 +1731,7 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
             // prefetch spills at 168 VGPRs: dgrad 0.737 -> 0.780).  HVIT_DMA1=0
             // disables (A/B only)
             static const bool nb1 = !getenv("HVIT_DMA1") || atoi(getenv("HVIT_DMA1"));
-            if constexpr (BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
+            if constexpr (!CONV_A && BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
               if (nb1) {
                 hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 1>), g, dim3(GEMM_THREADS), 0, st,
                                    la, lb, M, N, K, kps, ep);
