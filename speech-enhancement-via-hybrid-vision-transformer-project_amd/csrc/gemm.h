@@ -1731,8 +1731,11 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
             // prefetch spills at 168 VGPRs: dgrad 0.737 -> 0.780).  HVIT_DMA1=0
             // disables (A/B only)
             static const bool nb1 = !getenv("HVIT_DMA1") || atoi(getenv("HVIT_DMA1"));
-            if constexpr (!CONV_A && BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
-              if (nb1) {
+            // conv forward (BN statistics epilogue) too: conv_fwd 0.471 -> 0.447 ms/step;
+            // not the conv data gradient (0.346 -> 0.362).  HVIT_DMA1_CONV=0 disables (A/B)
+            static const bool nb1c = !getenv("HVIT_DMA1_CONV") || atoi(getenv("HVIT_DMA1_CONV"));
+            if constexpr (BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
+              if (CONV_A ? (nb1c && ep.stats) : nb1) {
                 hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 1>), g, dim3(GEMM_THREADS), 0, st,
                                    la, lb, M, N, K, kps, ep);
                 return;

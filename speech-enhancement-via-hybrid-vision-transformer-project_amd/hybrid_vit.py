@@ -310,9 +310,21 @@ class HybridViT(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("hvit: the HIP path needs GPU tensors (call .to('cuda')); there is no CPU path")
         lib = L.lib()  # noqa: F841  (fails loudly when libhvit.so is missing)
-        for n, t in self.named_parameters():
-            if t.device != x.device:
+        # the (name, parameter) list is cached (walking the module tree every
+        # forward was ~0.4 ms of host time per step); _apply (.to / .cuda / ...)
+        # drops it
+        named = self.__dict__.get("_hvit_named_params")
+        if named is None:
+            named = list(self.named_parameters())
+            self.__dict__["_hvit_named_params"] = named
+        dev = x.device
+        for n, t in named:
+            if t.device != dev:
                 raise RuntimeError(f"hvit: input on {x.device} but parameter {n} on {t.device}")
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__.pop("_hvit_named_params", None)
+        return super()._apply(fn, *args, **kwargs)
 
     def _seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0

@@ -118,6 +118,7 @@ class FusedAdamW(torch.optim.Optimizer):
         for group in self.param_groups:
             b1, b2 = group["betas"]
             by_step: Dict[float, list] = {}
+            ps_live = []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -126,8 +127,14 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                by_step.setdefault(float(st["step"]), []).append(p)
+                ps_live.append(p)
+            # per-parameter step counters stay CPU tensors (torch.optim.AdamW's
+            # state_dict format); one multi-tensor add instead of one op each
+            steps = [self.state[p]["step"] for p in ps_live]
+            if steps:
+                torch._foreach_add_(steps, 1.0)
+            for p, t in zip(ps_live, steps):
+                by_step.setdefault(t.item(), []).append(p)
             for step, ps in by_step.items():
                 items = (L.AdamWItem * len(ps))()
                 for i, p in enumerate(ps):
