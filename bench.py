@@ -42,8 +42,12 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--graph", type=int, default=None, choices=[0, 1],
+                    help="1: capture one whole step (fwd + loss + bwd + clip + AdamW, device-side dropout seeds and "
+                         "AdamW step counters) in a hipGraph and replay it; 0: eager launches.  Default 1 at one "
+                         "GPU, 0 under DP")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 32; 16 for --variant large)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -59,6 +63,8 @@ def parse():
     ap.add_argument("--roofline-op", default="vit_linear_wgrad",
                     help="op class for --roofline-only (functional.timed tag with a recorded replay)")
     a = ap.parse_args()
+    if a.graph is None:
+        a.graph = 1 if int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("HVIT_FORCE_DIST") != "1" else 0
     if a.batch is None:
         a.batch = 16 if a.variant == "large" else 32
     return a
@@ -158,7 +164,11 @@ def cpu_baseline(batch, budget_s):
     from oracle import closed_form as CF
     from oracle import hvit_oracle as O
 
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1))))
+    # every core this process may run on; OMP_NUM_THREADS caps it if set
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if os.environ.get("HVIT_CPU_THREADS"):
+        cores = int(os.environ["HVIT_CPU_THREADS"])
+    torch.set_num_threads(cores)
     cfg = O.HViTConfig()
     shapes = O.state_dict_shapes(cfg)
     sd = O.make_state(shapes, CF.weights(shapes), requires_grad=True)
@@ -175,15 +185,19 @@ def cpu_baseline(batch, budget_s):
         opt.zero_grad(set_to_none=True)
 
     step()  # warmup
-    n, t0 = 0, time.perf_counter()
-    while n < 3 and (time.perf_counter() - t0) < budget_s:
+    times = []
+    t0 = time.perf_counter()
+    while len(times) < 3 and (time.perf_counter() - t0) < budget_s:
+        t1 = time.perf_counter()
         step()
-        n += 1
-    dt = (time.perf_counter() - t0) / n
+        times.append(time.perf_counter() - t1)
+    times.sort()
+    dt = times[len(times) // 2]
     return {"value": round(batch * FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": torch.get_num_threads(),
             "kind": "port", "cpu": cpu_model(),
             "sample": f"oracle/hvit_oracle.py fp32 train step (fwd+CombinedLoss+bwd+clip+AdamW), B={batch}, "
-                      f"1x256x256 synthetic spectrograms, 1 warmup + {n} timed steps, {dt:.2f} s/step"}
+                      f"1x256x256 synthetic spectrograms, 1 warmup + {len(times)} timed steps, median "
+                      f"{dt:.2f} s/step (all: {', '.join(f'{t:.2f}' for t in times)})"}
 
 
 def main():
@@ -191,7 +205,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # HVIT_FORCE_DIST=1: the DP branch (process group + GradAllReducer) even at
+    # world size 1 -- exercises the RCCL path on a one-GPU box
+    use_dist = world > 1 or os.environ.get("HVIT_FORCE_DIST") == "1"
+    if use_dist:
         # one process per GPU over RCCL; HVIT_DIST_BACKEND=gloo (with ranks sharing the
         # visible GPUs round-robin) only rehearses the DP path on a one-GPU box
         backend = os.environ.get("HVIT_DIST_BACKEND", "nccl")
@@ -212,11 +229,13 @@ def main():
     model = hv.HybridViT(precision=args.precision, attention_precision="fp8" if args.attn == "fp8" else None,
                          **arch).cuda().train()
     reducer = None
-    if world > 1:
+    if use_dist:
         broadcast_module(model)
         reducer = GradAllReducer(model, bucket_mb=25, sliced={"pos_encoding.pos_embed": FRAMES})
-    # AdamW (training/optimizer.py:53-61) with clip_grad_norm_(1.0) (trainer.py:170-174) fused into it
-    opt = hv.FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, max_grad_norm=1.0)
+    # AdamW (training/optimizer.py:53-61) with clip_grad_norm_(1.0) (trainer.py:170-174) fused into it;
+    # capturable: device step counters, so the captured step replays with the right bias corrections
+    opt = hv.FusedAdamW(model.parameters(), lr=1e-4, weight_decay=0.01, max_grad_norm=1.0,
+                        capturable=bool(args.graph))
     crit = hv.CombinedLoss()
     noisy, clean = spectrogram_batch(args.batch, seed=1234 + rank * args.batch)
     noisy, clean = noisy.cuda(), clean.cuda()
@@ -243,19 +262,47 @@ def main():
             step()
         print(json.dumps(roofline_loop(step, args.roofline_op)), flush=True)
         return
+    eager_step = step
+    graph = None
+    if args.graph:
+        # warm up eagerly on a side stream (allocator pools, weight shadows,
+        # optimizer state, device step counters), then capture one whole step;
+        # every replay is a full step: new dropout masks (device seed stream),
+        # AdamW bias corrections from the device step counters
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(2, args.warmup // 2)):
+                step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = step()
+
+        def step():
+            graph.replay()
+            return static_loss
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step HIP events on the stream (no host sync inside the timed region)
+    # give the median step; the wall clock around all K steps gives the mean
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         loss = step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    ms_median = per_step[len(per_step) // 2]
+    if use_dist:
         te = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = te.item()
@@ -273,12 +320,23 @@ def main():
         step()
     host_ms = (time.perf_counter() - t1) / 3 * 1e3
     torch.cuda.synchronize()
-    # instrumented repeat of the timed steps: HIP events around every launch of
-    # each op class (functional.timed), for the per-op roofline table
+    eager_ms = None
+    if graph is not None:
+        # the same step launched eagerly (for the record: host-launch bound or not)
+        for _ in range(2):
+            eager_step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(5):
+            eager_step()
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - t1) / 5 * 1e3
+    # instrumented repeat of the timed steps (eager: HIP events around every
+    # launch of each op class, functional.timed) for the per-op roofline table
     isteps = min(args.steps, 10)
     HF.OP_TIMES = {}
     for _ in range(isteps):
-        step()
+        eager_step()
     torch.cuda.synchronize()
     table = op_table(HF.OP_TIMES, isteps)
     HF.OP_TIMES = None
@@ -298,6 +356,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
+            "ms_per_step_median": round(ms_median, 3),
+            "launch": "hipGraph replay of the whole step" if graph is not None else "eager",
+            "ms_per_step_eager": round(eager_ms, 3) if eager_ms is not None else round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -309,18 +370,20 @@ def main():
                                     + (" train step: fwd + CombinedLoss + bwd + clip + AdamW" if args.mode == "train"
                                        else " inference forward (eval, no grad)")),
                        "global_batch": world * args.batch, "seq_len": 256, "input": [args.batch, 1, 256, 256],
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "dist_backend": dist.get_backend() if use_dist else None},
             "spectrograms_per_s": round(spectros, 2),
             "frames_per_s_per_gpu": round(value / world, 1),
             "value_is": "aggregate spectrogram frames/s over all n_gpus (per-GPU figure: frames_per_s_per_gpu)",
             "host_enqueue_ms_per_step": round(host_ms, 3),
+            "host_enqueue_is": "graph replay call" if graph is not None else "eager launches of one step",
             "final_loss": round(loss.item(), 6),
             "roofline": roof,
             "op_table": {k: {kk: vv for kk, vv in v.items() if kk != "work_per_launch"} for k, v in table.items()},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

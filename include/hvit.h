@@ -37,11 +37,15 @@ enum { HVIT_ACC_ZEROED = 1 };
 
 /* Counter-based dropout: element i is kept iff a 16-bit hash of (seed, site, i)
  * is >= round(p * 65536); kept values are scaled by 1/(1-p).  Forward and
- * backward regenerate identical masks.  p = 0 disables. */
+ * backward regenerate identical masks.  p = 0 disables.  seed_ptr (nullable,
+ * device memory): the effective seed is seed ^ *seed_ptr, read by the kernel
+ * at run time, so a captured hipGraph draws new masks each replay once the
+ * word is advanced on the stream (hvit_rng_advance). */
 typedef struct {
   float p;
   unsigned long long seed;
   unsigned int site;
+  const unsigned long long* seed_ptr;
 } hvit_dropout_t;
 
 /* Fused GEMM epilogue (applied in this order):
@@ -245,10 +249,13 @@ typedef struct {
   float* exp_avg_sq;
   void* shadow_bf16;
   long long numel;
+  const float* step; /* nullable device step counter: when set, this tensor's bias corrections come from
+                        *step on the device (torch.optim.AdamW capturable=True semantics; advance it with
+                        hvit_step_bump); NULL: hyper bc1 / bc2 */
 } hvit_adamw_item_t;
 typedef struct {
   float lr, beta1, beta2, eps, weight_decay;
-  float bc1, bc2; /* 1 - beta1^step, 1 - beta2^step */
+  float bc1, bc2; /* 1 - beta1^step, 1 - beta2^step (items without a device step) */
 } hvit_adamw_hyper_t;
 long long hvit_clip_ws_elems(int count);
 int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_norm, float* ws, long long ws_elems, float* out,
@@ -256,6 +263,13 @@ int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_norm, float*
 int hvit_scale_tensors(int count, const hvit_tensor_t* tensors, const float* coef, void* stream);
 int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp, const float* coef,
                void* stream);
+/* Device-resident training counters, advanced on the stream (so a captured train
+ * step, hipGraph, replays with fresh values): hvit_rng_advance steps the dropout
+ * state {base, counter} and writes the next forward's seed to *seed_out (what
+ * that forward's hvit_dropout_t.seed_ptr points at; the model calls it once per
+ * training forward); hvit_step_bump adds inc to n f32 step counters. */
+int hvit_rng_advance(unsigned long long* state, unsigned long long* seed_out, void* stream);
+int hvit_step_bump(float* steps, int n, float inc, void* stream);
 
 #ifdef __cplusplus
 }

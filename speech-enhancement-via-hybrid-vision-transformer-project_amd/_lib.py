@@ -28,7 +28,7 @@ f32 = C.c_float
 
 
 class Dropout(C.Structure):
-    _fields_ = [("p", C.c_float), ("seed", C.c_ulonglong), ("site", C.c_uint)]
+    _fields_ = [("p", C.c_float), ("seed", C.c_ulonglong), ("site", C.c_uint), ("seed_ptr", C.c_void_p)]
 
 
 class Epilogue(C.Structure):
@@ -62,7 +62,7 @@ class TensorRef(C.Structure):
 
 class AdamWItem(C.Structure):
     _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("shadow_bf16", vp),
-                ("numel", i64)]
+                ("numel", i64), ("step", vp)]
 
 
 class AdamWHyper(C.Structure):
@@ -115,6 +115,8 @@ _SIGS = {
     "hvit_clip_coef": ([i32, P(TensorRef), f32, vp, i64, vp, vp], i32),
     "hvit_scale_tensors": ([i32, P(TensorRef), vp, vp], i32),
     "hvit_adamw": ([i32, P(AdamWItem), P(AdamWHyper), vp, vp], i32),
+    "hvit_rng_advance": ([vp, vp, vp], i32),
+    "hvit_step_bump": ([vp, i32, f32, vp], i32),
 }
 
 EXPORTED = sorted(k for k in _SIGS)
@@ -185,5 +187,11 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
-def dropout(p=0.0, seed=0, site=0) -> Dropout:
-    return Dropout(float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(site) & 0xFFFFFFFF)
+def dropout(p=0.0, seed=0, site=0, seed_t=None) -> Dropout:
+    """A dropout site.  ``seed_t`` (optional int64 device tensor of one word,
+    a forward's seed written by hvit_rng_advance): the kernels use
+    ``seed ^ seed_t[0]``; the struct keeps a reference so the word outlives it."""
+    d = Dropout(float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(site) & 0xFFFFFFFF,
+                None if seed_t is None else seed_t.data_ptr())
+    d.keep = seed_t
+    return d

@@ -90,8 +90,9 @@ template <typename T, int HD>
 __global__ __launch_bounds__(AT_THREADS) void mhsa_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ o,
                                                              float* __restrict__ lse, int B, int N,
                                                              int H, float scale, uint32_t thr,
-                                                             float dscale, unsigned long long seed,
+                                                             float dscale, DSeed seed_,
                                                              uint32_t site) {
+  const unsigned long long seed = seed_;
   using GH = RowGeo<T, HD>;        // rows of hd elements
   using GK = RowGeo<T, AT_TILE>;   // rows of 64 keys
   constexpr int NT = HD / 16;      // output 16-col blocks
@@ -238,7 +239,8 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dq_kernel(const T* __restrict
                                                             const float* __restrict__ delta,
                                                             T* __restrict__ dqkv, float* __restrict__ probs,
                                                             int B, int N, int H, float scale, uint32_t thr,
-                                                            float dscale, unsigned long long seed, uint32_t site) {
+                                                            float dscale, DSeed seed_, uint32_t site) {
+  const unsigned long long seed = seed_;
   using GH = RowGeo<T, HD>;
   using GK = RowGeo<T, AT_TILE>;
   constexpr int NT = HD / 16;
@@ -347,7 +349,8 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_kernel(const T* __restric
                                                              const float* __restrict__ delta,
                                                              T* __restrict__ dqkv, int B, int N, int H,
                                                              float scale, uint32_t thr, float dscale,
-                                                             unsigned long long seed, uint32_t site) {
+                                                             DSeed seed_, uint32_t site) {
+  const unsigned long long seed = seed_;
   using GH = RowGeo<T, HD>;
   using GK = RowGeo<T, AT_TILE>;
   constexpr int NT = HD / 16;
@@ -582,8 +585,9 @@ __device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uin
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int N, int H, float scale,
-                                                         uint32_t thr, float dscale, unsigned long long seed,
+                                                         uint32_t thr, float dscale, DSeed seed_,
                                                          uint32_t site) {
+  const unsigned long long seed = seed_;
   __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
   char* Ks = smem;
   char* Vs = smem + V2_KMAX * V2_ROWB;
@@ -683,8 +687,9 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
                                                         const bf16_t* __restrict__ dout,
                                                         const float* __restrict__ lse, float* __restrict__ delta,
                                                         bf16_t* __restrict__ dqkv, int N, int H, float scale,
-                                                        uint32_t thr, float dscale, unsigned long long seed,
+                                                        uint32_t thr, float dscale, DSeed seed_,
                                                         uint32_t site) {
+  const unsigned long long seed = seed_;
   __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
   char* Ks = smem;
   char* Vs = smem + V2_KMAX * V2_ROWB;
@@ -773,7 +778,8 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
                                                          const float* __restrict__ lse,
                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                          int N, int H, float scale, uint32_t thr, float dscale,
-                                                         unsigned long long seed, uint32_t site) {
+                                                         DSeed seed_, uint32_t site) {
+  const unsigned long long seed = seed_;
   __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4];
   char* Qs = smem;
   char* Ds = smem + V2_KMAX * V2_ROWB;
@@ -892,7 +898,7 @@ static int mhsa_fwd_t(const void* qkv, void* o, float* lse, float* probs, int B,
                       float scale, const hvit_dropout_t* dr, hipStream_t st) {
   uint32_t thr = dr ? drop_threshold(dr->p) : 0;
   float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-  unsigned long long seed = dr ? dr->seed : 0;
+  const DSeed seed = dseed(dr);
   uint32_t site = dr ? dr->site : 0;
   dim3 g(cdiv(N, AT_TILE), H, B);
   hipLaunchKernelGGL((mhsa_fwd_kernel<T, HD>), g, dim3(AT_THREADS), 0, st, (const T*)qkv, (T*)o, lse, B,
@@ -913,7 +919,7 @@ static int mhsa_bwd_t(const void* qkv, const void* o, const void* dout, const fl
                       const hvit_dropout_t* dr, hipStream_t st) {
   uint32_t thr = dr ? drop_threshold(dr->p) : 0;
   float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-  unsigned long long seed = dr ? dr->seed : 0;
+  const DSeed seed = dseed(dr);
   uint32_t site = dr ? dr->site : 0;
   long rows = (long)B * N * H;
   hipLaunchKernelGGL((mhsa_delta_kernel<T, HD>), dim3(cdiv(rows, 4)), dim3(256), 0, st, (const T*)o,
@@ -958,7 +964,7 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
     const int wv = v2_waves(B * H);
     auto go = [&](auto kern, int waves) {
       hipLaunchKernelGGL(kern, dim3(cdiv(N, 16 * waves), H, B), dim3(64 * waves), 0, st, (const bf16_t*)qkv,
-                         (bf16_t*)o, lse, N, H, scale, thr, ds, dr ? dr->seed : 0ull, dr ? dr->site : 0u);
+                         (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dr), dr ? dr->site : 0u);
     };
     if (wv == 16) go(mhsa_fwd_v2<16>, 16);
     else if (wv == 8) go(mhsa_fwd_v2<8>, 8);
@@ -983,7 +989,7 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
     const hvit_dropout_t* dr = dropout;
     const uint32_t thr = dr ? drop_threshold(dr->p) : 0;
     const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-    const unsigned long long seed = dr ? dr->seed : 0ull;
+    const DSeed seed = dseed(dr);
     const uint32_t site = dr ? dr->site : 0u;
     auto go = [&](auto dqk, auto dkvk, int waves) {
       dim3 g(cdiv(N, 16 * waves), H, B);

@@ -73,8 +73,9 @@ template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* __restrict__ qkv,
                                                                   bf16_t* __restrict__ o, float* __restrict__ lse,
                                                                   int N, int H, float scale, uint32_t thr,
-                                                                  float dscale, unsigned long long seed,
+                                                                  float dscale, DSeed seed_,
                                                                   uint32_t site) {
+  const unsigned long long seed = seed_;
   constexpr int NT = WAVES * 64;
   constexpr int PER = F8_KMAX * 8 / NT;  // 16-byte chunks of K (and of V) per thread
   __shared__ __attribute__((aligned(16))) char Ks[F8_KMAX * F8_KP];
@@ -236,6 +237,10 @@ extern "C" int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, f
   HVIT_CHECK(hd == 64, "hvit_mhsa_fwd_fp8: head_dim %d unsupported (64)", hd);
   HVIT_CHECK(N <= F8_KMAX, "hvit_mhsa_fwd_fp8: N=%d exceeds %d tokens", N, F8_KMAX);
   HVIT_CHECK(aligned16(qkv) && aligned16(o), "hvit_mhsa_fwd_fp8: qkv/o must be 16-byte aligned");
+  // P is held as 256 * P * 1/(1-p) in e4m3 (max 448): kept probabilities near 1
+  // would saturate above p = 0.4
+  HVIT_CHECK(!dropout || dropout->p <= 0.4f, "hvit_mhsa_fwd_fp8: attention dropout p=%g > 0.4 unsupported",
+             dropout ? dropout->p : 0.f);
   const uint32_t thr = dropout ? drop_threshold(dropout->p) : 0;
   const float ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
   // one 16-wave workgroup per (b, h) (measured faster than two 8-wave ones at
@@ -243,7 +248,7 @@ extern "C" int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, f
   constexpr int WAVES = 16;
   hipLaunchKernelGGL(mhsa_fwd_fp8_kernel<WAVES>, dim3(cdiv(N, 16 * WAVES), H, B), dim3(64 * WAVES), 0,
                      (hipStream_t)stream, (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds,
-                     dropout ? dropout->seed : 0ull, dropout ? dropout->site : 0u);
+                     dseed(dropout), dropout ? dropout->site : 0u);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

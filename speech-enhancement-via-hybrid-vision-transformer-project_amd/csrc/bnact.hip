@@ -42,7 +42,14 @@ struct BnArgs {
   const float* beta;
   uint32_t thr;
   float dscale;
-  uint32_t key;  // rng_key(seed, site)
+  uint32_t key;  // rng_key(seed, site) (host-resolved when seedp is NULL)
+  const unsigned long long* seedp;  // device seed word (hvit_dropout_t.seed_ptr)
+  unsigned long long seed;
+  uint32_t site;
+  // at kernel entry: fold in the device seed word (one scalar load)
+  __device__ __forceinline__ void resolve() {
+    if (seedp && thr) key = rng_key(seed ^ *seedp, site);
+  }
 };
 
 // CV per-channel constants p[c .. c+CV-1] as 16-byte vector loads (c is a
@@ -78,7 +85,9 @@ __device__ __forceinline__ void drop_mask(const BnArgs& a, int n, int c, float* 
 
 // forward: y[n, oy, ox, c..] over full windows
 template <typename T, typename TO>
-__global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z, TO* __restrict__ y, BnArgs a) {
+__global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z, TO* __restrict__ y, BnArgs a_) {
+  BnArgs a = a_;
+  a.resolve();
   constexpr int CV = V16<T>::N;
   const int G = a.C / CV;
   const int Ho = a.H / a.pool, Wo = a.W / a.pool;
@@ -133,8 +142,10 @@ __global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z,
 // made tied bf16 inputs differ by an ulp and move the gradient)
 template <typename T, typename TD, bool APPLY>
 __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z, const TD* __restrict__ dy,
-                                                       BnArgs a, float* __restrict__ sums, int training,
+                                                       BnArgs a_, float* __restrict__ sums, int training,
                                                        T* __restrict__ dz) {
+  BnArgs a = a_;
+  a.resolve();
   constexpr int CV = V16<T>::N;
   constexpr int MAXW = 4;  // pool <= 2
   __shared__ float red[2][256][CV];
@@ -288,7 +299,9 @@ __device__ __forceinline__ float raw_elem(const u32x4& u, int e) {
 
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void bnact_sums_kernel(const T* __restrict__ z, const TD* __restrict__ dy,
-                                                        BnArgs a, float* __restrict__ sums) {
+                                                        BnArgs a_, float* __restrict__ sums) {
+  BnArgs a = a_;
+  a.resolve();
   constexpr int CV = V16<T>::N;
   constexpr int MAXW = 4;  // pool <= 2
   __shared__ float red[2][256][CV];
@@ -423,6 +436,9 @@ static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const floa
   a.thr = dr ? drop_threshold(dr->p) : 0;
   a.dscale = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
   a.key = dr ? rng_key(dr->seed, dr->site) : 0u;
+  a.seedp = dr ? dr->seed_ptr : nullptr;
+  a.seed = dr ? dr->seed : 0ull;
+  a.site = dr ? dr->site : 0u;
   return HVIT_OK;
 }
 

@@ -122,6 +122,18 @@ __device__ __forceinline__ f32x4 keep4_at(uint32_t key, uint64_t i0, uint32_t th
   const uint32_t h0 = rng_pair(key, i0), h1 = rng_pair(key, i0 + 2);
   return (f32x4){keep_lo(h0, thr, ds), keep_hi(h0, thr, ds), keep_lo(h1, thr, ds), keep_hi(h1, thr, ds)};
 }
+// Dropout seed as a kernel argument: the host value, XOR the 64-bit word at p
+// when p is non-NULL (a device-resident seed the model advances once per
+// training forward, so a captured hipGraph draws fresh masks on every replay).
+// Resolved once at kernel entry (a scalar load).
+struct DSeed {
+  unsigned long long s;
+  const unsigned long long* p;
+  __device__ __forceinline__ operator unsigned long long() const { return p ? (s ^ *p) : s; }
+};
+static inline DSeed dseed(const hvit_dropout_t* d) {
+  return d ? DSeed{d->seed, d->seed_ptr} : DSeed{0ull, nullptr};
+}
 static inline uint32_t drop_threshold(float p) {
   if (p <= 0.f) return 0;
   double t = (double)p * 65536.0 + 0.5;

@@ -57,8 +57,9 @@ __global__ void conv_unpack_kernel(const float* dwp, int Cout, int Cin, int KS, 
 
 // out[m][n] = g[m][n] * keep(m*N+n)/(1-p) * rowscale[m / rps]
 __global__ void dropout_scale_kernel(const void* g, int gdt, void* out, int odt, long M, int N, uint32_t thr,
-                                     float ds, unsigned long long seed, uint32_t site, const float* rowscale,
+                                     float ds, DSeed seed_, uint32_t site, const float* rowscale,
                                      int rps) {
+  const unsigned long long seed = seed_;
   long total = M * N;
   GRID_STRIDE(i, total) {
     float v = ld_dt(g, i, gdt);
@@ -70,8 +71,9 @@ __global__ void dropout_scale_kernel(const void* g, int gdt, void* out, int odt,
 
 // vectorised form: 4 consecutive elements per thread, N % 4 == 0, 32-bit indices
 __global__ void dropout_scale4_kernel(const void* g, int gdt, void* out, int odt, int M, int N, uint32_t thr,
-                                      float ds, unsigned long long seed, uint32_t site, const float* rowscale,
+                                      float ds, DSeed seed_, uint32_t site, const float* rowscale,
                                       int rps) {
+  const unsigned long long seed = seed_;
   const int total4 = M * (N / 4);
   for (int i4 = blockIdx.x * blockDim.x + threadIdx.x; i4 < total4; i4 += gridDim.x * blockDim.x) {
     const int i = i4 * 4;
@@ -108,9 +110,10 @@ __global__ void dropout_scale4_kernel(const void* g, int gdt, void* out, int odt
 constexpr int DSC_THREADS = 256, DSC_BLOCKS = 1024;
 __global__ __launch_bounds__(DSC_THREADS) void dropout_scale4_colsum_kernel(const void* g, int gdt, void* out, int odt, int M,
                                                                     int N, uint32_t thr, float ds,
-                                                                    unsigned long long seed, uint32_t site,
+                                                                    DSeed seed_, uint32_t site,
                                                                     const float* rowscale, int rps,
                                                                     float* __restrict__ part) {
+  const unsigned long long seed = seed_;
   __shared__ f32x4 red[DSC_THREADS];
   const int total4 = M * (N / 4);
   const int stride = gridDim.x * blockDim.x;
@@ -311,8 +314,9 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
   }
 }
 
-__global__ void droppath_scale_kernel(int B, uint32_t thr, float ds, unsigned long long seed, uint32_t site,
+__global__ void droppath_scale_kernel(int B, uint32_t thr, float ds, DSeed seed_, uint32_t site,
                                       float* out) {
+  const unsigned long long seed = seed_;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) out[b] = rng_keep(seed, site, (uint64_t)b, thr) ? ds : 0.f;
 }
@@ -367,7 +371,7 @@ extern "C" int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, c
         ws && aligned16(ws) && ws_elems >= hvit_dropout_colsum_ws_elems(N)) {
       hipLaunchKernelGGL(dropout_scale4_colsum_kernel, dim3(DSC_BLOCKS), dim3(DSC_THREADS), 0,
                          (hipStream_t)stream, g, g_dt, out, out_dt, (int)M, N, thr, ds,
-                         dropout ? dropout->seed : 0ull, dropout ? dropout->site : 0u, rowscale, rows_per_sample,
+                         dseed(dropout), dropout ? dropout->site : 0u, rowscale, rows_per_sample,
                          ws);
       HVIT_LAUNCH_CHECK();
       return hvit_reduce_rows(ws, HVIT_F32, DSC_BLOCKS, N, N, 1, colsum, stream);
@@ -380,13 +384,13 @@ extern "C" int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, c
   }
   if (N % 4 == 0 && total < (1L << 31) && aligned16(g) && aligned16(out)) {
     hipLaunchKernelGGL(dropout_scale4_kernel, dim3(grid_for(total, 4)), dim3(256), 0, (hipStream_t)stream, g,
-                       g_dt, out, out_dt, (int)M, N, thr, ds, dropout ? dropout->seed : 0ull,
+                       g_dt, out, out_dt, (int)M, N, thr, ds, dseed(dropout),
                        dropout ? dropout->site : 0u, rowscale, rows_per_sample);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
   hipLaunchKernelGGL(dropout_scale_kernel, dim3(grid_for(total, 4)), dim3(256), 0, (hipStream_t)stream, g, g_dt,
-                     out, out_dt, (long)M, N, thr, ds, dropout ? dropout->seed : 0ull,
+                     out, out_dt, (long)M, N, thr, ds, dseed(dropout),
                      dropout ? dropout->site : 0u, rowscale, rows_per_sample);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
@@ -510,7 +514,7 @@ extern "C" int hvit_droppath_scale(int B, const hvit_dropout_t* dropout, float* 
   uint32_t thr = drop_threshold(dropout->p);
   float ds = dropout->p > 0.f ? 1.f / (1.f - dropout->p) : 1.f;
   hipLaunchKernelGGL(droppath_scale_kernel, dim3(cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, B, thr, ds,
-                     dropout->seed, dropout->site, out);
+                     dseed(dropout), dropout->site, out);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

@@ -358,7 +358,10 @@ struct Epi {
   long ldaux = 0;
   uint32_t drop_thr = 0;  // dropout keep test (0 = off)
   float drop_scale = 1.f;
-  uint32_t drop_key = 0;  // rng_key(seed, site)
+  uint32_t drop_key = 0;  // rng_key(seed, site) (host-resolved when drop_seedp is NULL)
+  const unsigned long long* drop_seedp = nullptr;  // device seed word (hvit_dropout_t.seed_ptr)
+  unsigned long long drop_seed = 0;
+  uint32_t drop_site = 0;
   const float* resid = nullptr;  // v = resid[m][n] + rowscale[m / rps] * v
   long ldr = 0;
   const float* rowscale = nullptr;
@@ -460,9 +463,13 @@ __device__ __forceinline__ f32x4 load4v(const void* p, long off, int nv, int dt)
 
 // dropout multipliers of 4 adjacent elements (index i0 = m*N + n, i0 even):
 // two pair hashes give the four 16-bit uniforms
-__device__ __forceinline__ f32x4 keep4(const Epi& ep, int m, int n, int N) {
+__device__ __forceinline__ f32x4 keep4(const Epi& ep, uint32_t key, int m, int n, int N) {
   const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-  return keep4_at(ep.drop_key, i0, ep.drop_thr, ep.drop_scale);
+  return keep4_at(key, i0, ep.drop_thr, ep.drop_scale);
+}
+// the dropout key of a launch: folds in the device seed word (one scalar load)
+__device__ __forceinline__ uint32_t epi_key(const Epi& ep) {
+  return (ep.drop_seedp && ep.drop_thr) ? rng_key(ep.drop_seed ^ *ep.drop_seedp, ep.drop_site) : ep.drop_key;
 }
 
 // Inputs the epilogue reads besides the accumulator, loaded for all of a
@@ -485,20 +492,20 @@ __device__ __forceinline__ void epi_load4(const Epi& ep, int m, int n, int nv, b
 }
 
 template <bool FAST>
-__device__ __forceinline__ void epi_apply4(const Epi& ep, int m, int n, int nv, int N, f32x4& v, const f32x4& bias,
-                                           const EpiIn& in) {
+__device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, int n, int nv, int N, f32x4& v,
+                                           const f32x4& bias, const EpiIn& in) {
   v += bias;
   if (ep.rowadd) v += in.rowadd;
   float keep[4] = {1.f, 1.f, 1.f, 1.f};
   if (ep.drop_thr) {
     const uint64_t i0 = (uint64_t)m * (uint64_t)N + (uint64_t)n;
     if (FAST || (i0 & 1) == 0) {
-      const f32x4 k = keep4_at(ep.drop_key, i0, ep.drop_thr, ep.drop_scale);
+      const f32x4 k = keep4_at(dkey, i0, ep.drop_thr, ep.drop_scale);
 #pragma unroll
       for (int e = 0; e < 4; ++e) keep[e] = k[e];
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) keep[e] = rng_u16k(ep.drop_key, i0 + e) >= ep.drop_thr ? ep.drop_scale : 0.f;
+      for (int e = 0; e < 4; ++e) keep[e] = rng_u16k(dkey, i0 + e) >= ep.drop_thr ? ep.drop_scale : 0.f;
     }
   } else if (ep.drop_scale != 1.f) {
 #pragma unroll
@@ -1131,6 +1138,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
   const int wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const TileId tid3 = tile_of(ep.xcd_remap);
+  const uint32_t dkey = epi_key(ep);
   const int m0 = tid3.mt * BM;
   const int n0 = tid3.nt * BN;
   const int kbeg = tid3.z * kps;
@@ -1287,8 +1295,8 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = wide8(va, vb);
           f32x4 ka = {1.f, 1.f, 1.f, 1.f}, kb = ka;
           if (ep.drop_thr) {
-            ka = keep4(ep, m, n8, N);
-            kb = keep4(ep, m, n8 + 4, N);
+            ka = keep4(ep, dkey, m, n8, N);
+            kb = keep4(ep, dkey, m, n8 + 4, N);
           }
           f32x4 ga, gb;
 #pragma unroll
@@ -1299,8 +1307,8 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = wide8(ga, gb);
         } else {
           if (EK != EK_STORE && ep.drop_thr) {
-            va *= keep4(ep, m, n8, N);
-            vb *= keep4(ep, m, n8 + 4, N);
+            va *= keep4(ep, dkey, m, n8, N);
+            vb *= keep4(ep, dkey, m, n8 + 4, N);
           }
           if constexpr (EK == EK_GELU_BWD) {
             f32x4 ha, hb;
@@ -1431,7 +1439,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int m = mbase + row;
           const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
           store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
-          const f32x4 k = ep.drop_thr ? keep4(ep, m, n, N) : (f32x4){1.f, 1.f, 1.f, 1.f};
+          const f32x4 k = ep.drop_thr ? keep4(ep, dkey, m, n, N) : (f32x4){1.f, 1.f, 1.f, 1.f};
           f32x4 g;
 #pragma unroll
           for (int e = 0; e < 4; ++e) g[e] = gelu_f(v[e]) * k[e];
@@ -1452,7 +1460,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int row = r0 + i * RSTEP;
           const int m = mbase + row;
           f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
-          if (ep.drop_thr) v *= keep4(ep, m, n, N);
+          if (ep.drop_thr) v *= keep4(ep, dkey, m, n, N);
           v = r[i] + rs[i] * v;
           store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
         }
@@ -1475,7 +1483,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int row = r0 + i * RSTEP;
           const int m = mbase + row;
           f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
-          if (ep.drop_thr) v *= keep4(ep, m, n, N);
+          if (ep.drop_thr) v *= keep4(ep, dkey, m, n, N);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(h[i][e]);
           store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
@@ -1513,7 +1521,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int m = mbase + row;
           if (PRED && (m >= M || !nok)) continue;
           f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4);
-          epi_apply4<!PRED>(ep, m, n, PRED ? nv : 4, N, v, bias4, in[i]);
+          epi_apply4<!PRED>(ep, dkey, m, n, PRED ? nv : 4, N, v, bias4, in[i]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (!PRED || e < nv) {

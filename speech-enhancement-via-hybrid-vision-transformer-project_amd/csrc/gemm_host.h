@@ -34,6 +34,9 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
     ep.drop_thr = drop_threshold(e->dropout.p);
     ep.drop_scale = 1.f / (1.f - e->dropout.p);
     ep.drop_key = rng_key(e->dropout.seed, e->dropout.site);
+    ep.drop_seedp = e->dropout.seed_ptr;
+    ep.drop_seed = e->dropout.seed;
+    ep.drop_site = e->dropout.site;
   }
   ep.resid = e->resid;
   ep.ldr = ldo;

@@ -273,6 +273,7 @@ struct AdamArgs {
   float* m[MT_MAX];
   float* v[MT_MAX];
   bf16_t* shadow[MT_MAX];
+  const float* step[MT_MAX];  // device step counters (nullable: the host bias corrections)
 };
 
 struct AdamHyper {
@@ -290,12 +291,24 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= (h.lr / h.bc1) * (m / denom);
 }
 
-__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a, AdamHyper h, const float* __restrict__ coef) {
+__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a, AdamHyper h0, const float* __restrict__ coef) {
   const float c = coef ? coef[1] : 1.f;
   const long total = a.start[a.count];
-  int j = 0;
+  int j = 0, jh = -1;
+  AdamHyper h = h0;
   for (long u = (long)blockIdx.x * 256 + threadIdx.x; u < total; u += (long)gridDim.x * 256) {
     while (u >= a.start[j + 1]) ++j;
+    if (j != jh) {  // a new tensor: its bias corrections (device step counter, capturable mode)
+      jh = j;
+      if (a.step[j]) {
+        const float st = *a.step[j];
+        h.bc1 = 1.f - powf(h0.beta1, st);
+        h.bc2_sqrt = sqrtf(1.f - powf(h0.beta2, st));
+      } else {
+        h.bc1 = h0.bc1;
+        h.bc2_sqrt = h0.bc2_sqrt;
+      }
+    }
     const long e = 4 * (u - a.start[j]), n = a.n[j];
     float *P = a.p[j], *M = a.m[j], *V = a.v[j];
     const float* G = a.g[j];
@@ -332,6 +345,26 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a, AdamHyper h, con
       }
     }
   }
+}
+
+// Device-resident training counters, advanced on the stream so that a captured
+// train step (hipGraph) sees fresh values on every replay:
+//  * dropout seed (HybridViT training forward): st[0] = base seed, st[1] =
+//    forward counter; each forward's seed goes to its own word `out` (read by
+//    every dropout kernel of that forward and its backward through
+//    hvit_dropout_t.seed_ptr, so two forwards before one backward keep their
+//    own masks);
+//  * AdamW step counters (torch.optim.AdamW capturable semantics).
+__global__ void rng_advance_kernel(unsigned long long* __restrict__ st, unsigned long long* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    const unsigned long long c = st[1] + 1ull;
+    st[1] = c;
+    *out = mix64(st[0] ^ mix64(c));
+  }
+}
+__global__ void step_bump_kernel(float* __restrict__ steps, int n, float inc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) steps[i] += inc;
 }
 
 static int grid_for_units(long units, int cap) {
@@ -440,8 +473,11 @@ extern "C" int hvit_scale_tensors(int count, const hvit_tensor_t* tensors, const
 extern "C" int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp,
                           const float* coef, void* stream) {
   HVIT_CHECK(count >= 0 && (count == 0 || items) && hp, "hvit_adamw: bad args");
-  HVIT_CHECK(hp->bc1 > 0.f && hp->bc2 > 0.f, "hvit_adamw: bias corrections must be positive");
-  const AdamHyper h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, hp->bc1, sqrtf(hp->bc2)};
+  bool host_bc = false;
+  for (int k = 0; k < count; ++k) host_bc = host_bc || !items[k].step;
+  HVIT_CHECK(!host_bc || (hp->bc1 > 0.f && hp->bc2 > 0.f), "hvit_adamw: bias corrections must be positive");
+  const AdamHyper h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, host_bc ? hp->bc1 : 1.f,
+                    host_bc ? sqrtf(hp->bc2) : 1.f};
   for (int base = 0; base < count; base += MT_MAX) {
     AdamArgs a;
     a.count = std::min(MT_MAX, count - base);
@@ -458,6 +494,7 @@ extern "C" int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_
       a.m[k] = it.exp_avg;
       a.v[k] = it.exp_avg_sq;
       a.shadow[k] = (bf16_t*)it.shadow_bf16;
+      a.step[k] = it.step;
       a.n[k] = (long)it.numel;
       a.start[k + 1] = a.start[k] + (long)((it.numel + 3) / 4);
     }
@@ -466,5 +503,21 @@ extern "C" int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_
                        (hipStream_t)stream, a, h, coef);
     HVIT_LAUNCH_CHECK();
   }
+  return HVIT_OK;
+}
+
+extern "C" int hvit_rng_advance(unsigned long long* state, unsigned long long* seed_out, void* stream) {
+  HVIT_CHECK(state && seed_out && (((uintptr_t)state) & 7) == 0 && (((uintptr_t)seed_out) & 7) == 0,
+             "hvit_rng_advance: null or misaligned pointer");
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state, seed_out);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_step_bump(float* steps, int n, float inc, void* stream) {
+  HVIT_CHECK(steps && n >= 0, "hvit_step_bump: bad args");
+  if (n == 0) return HVIT_OK;
+  hipLaunchKernelGGL(step_bump_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, steps, n, inc);
+  HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

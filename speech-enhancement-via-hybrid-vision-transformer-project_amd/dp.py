@@ -54,6 +54,7 @@ class GradAllReducer:
         for n in self.sliced:
             if n not in dict(named):
                 raise KeyError(f"hvit GradAllReducer: no parameter {n!r} to slice")
+        self.bucket_mb = bucket_mb
         cap = int(bucket_mb * 1024 * 1024)
         self.buckets: List[List[torch.nn.Parameter]] = []
         cur, size = [], 0
@@ -80,7 +81,6 @@ class GradAllReducer:
         self._fwd_hook = model.register_forward_hook(self._on_forward)
         self._syncing = True
         self.broadcast_buffers = broadcast_buffers
-        self._bufs = [b for b in model.buffers() if b.is_floating_point()]
         self._max_tokens = 0
         self.reset()
 
@@ -106,7 +106,7 @@ class GradAllReducer:
         if name not in self.sliced:
             raise KeyError(name)
         self.remove()
-        self.__init__(self.model, group=self.group, sliced={**self.sliced, name: rows},
+        self.__init__(self.model, bucket_mb=self.bucket_mb, group=self.group, sliced={**self.sliced, name: rows},
                       broadcast_buffers=self.broadcast_buffers)
 
     def reset(self):
@@ -154,10 +154,22 @@ class GradAllReducer:
         unused parameters or a step taken under no_sync, and re-launching stale
         ones), install the averaged gradients, broadcast rank 0's buffers, and
         reset for the next step."""
-        for name, rows in self.sliced.items():
-            if self._max_tokens > rows:
-                raise RuntimeError(f"hvit GradAllReducer: a forward used {self._max_tokens} tokens but only "
-                                   f"{rows} rows of {name} are reduced; raise sliced[{name!r}]")
+        if self.sliced:
+            # agree on the largest token count over the group first, so that a
+            # rank whose batch exceeds the row bound makes EVERY rank raise here,
+            # before any of them enters the bucket collectives below
+            mt = self._max_tokens
+            if self.world > 1:
+                dev = self.params[0].device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+                t = torch.tensor([mt], dtype=torch.int64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                mt = int(t.item())
+            for name, rows in self.sliced.items():
+                if mt > rows:
+                    self._max_tokens = 0
+                    self.reset()
+                    raise RuntimeError(f"hvit GradAllReducer: a forward used {mt} tokens but only "
+                                       f"{rows} rows of {name} are reduced; raise sliced[{name!r}]")
         for b, ps in enumerate(self.buckets):
             if self.works[b] is not None and not self.stale[b]:
                 continue
@@ -177,12 +189,16 @@ class GradAllReducer:
                     v.copy_(flat[o:o + v.numel()].view_as(v))
                 else:
                     p.grad = flat[o:o + p.numel()].view_as(p)
-        if self.broadcast_buffers and self.world > 1 and self._bufs:
+        # the module's current buffers (a .to() / .cuda() since construction
+        # replaces them); the source is the group's rank 0 as a global rank
+        bufs = [b for b in self.model.buffers() if b.is_floating_point()]
+        if self.broadcast_buffers and self.world > 1 and bufs:
+            src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
             with torch.no_grad():
-                fb = torch.cat([t.reshape(-1).float() for t in self._bufs])
-                dist.broadcast(fb, 0, group=self.group)
+                fb = torch.cat([t.reshape(-1).float() for t in bufs])
+                dist.broadcast(fb, src, group=self.group)
                 o = 0
-                for t in self._bufs:
+                for t in bufs:
                     t.copy_(fb[o:o + t.numel()].view_as(t))
                     o += t.numel()
         self._max_tokens = 0

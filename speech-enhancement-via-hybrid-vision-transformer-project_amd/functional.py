@@ -305,13 +305,17 @@ def conv_wgrad(dt, g: L.ConvGeom, dz, wshape) -> torch.Tensor:
 
 @dataclass
 class Drop:
-    """A dropout site: probability, per-forward seed and site id."""
+    """A dropout site: probability, seed and site id.  ``seed_t`` (optional): the
+    forward's device seed word (HybridViT._forward_seed); the kernels then use
+    ``seed ^ seed_t[0]``, read on the device, so a captured train step draws new
+    masks on every replay."""
     p: float = 0.0
     seed: int = 0
     site: int = 0
+    seed_t: Optional[torch.Tensor] = None
 
     def c(self):
-        return L.dropout(self.p, self.seed, self.site)
+        return L.dropout(self.p, self.seed, self.site, self.seed_t)
 
 
 # ----------------------------------------------------------------------------
@@ -526,11 +530,13 @@ def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):
 def droppath_scales(B, p, seed, dev):
     """DropPath (components.py:407-427) multipliers of a block's two residual
     branches from one launch: keep(seed, site 1, b) for the attention branch,
-    keep(seed, site 1, B + b) for the MLP branch."""
+    keep(seed, site 1, B + b) for the MLP branch.  ``seed``: an int, or a Drop
+    whose (seed, seed_t) are used (site 1, its p ignored)."""
     if p <= 0:
         return None, None
     out = torch.empty(2 * B, dtype=torch.float32, device=dev)
-    call("hvit_droppath_scale", 2 * B, L.dropout(p, seed, 1), out.data_ptr(), stream_ptr())
+    d = L.dropout(p, seed.seed, 1, seed.seed_t) if isinstance(seed, Drop) else L.dropout(p, seed, 1)
+    call("hvit_droppath_scale", 2 * B, d, out.data_ptr(), stream_ptr())
     return out[:B], out[B:]
 
 

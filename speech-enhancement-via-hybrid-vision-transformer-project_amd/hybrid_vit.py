@@ -242,7 +242,11 @@ class HybridViT(nn.Module):
             raise ValueError(f"hvit: attention_precision must be None or 'fp8', got {attention_precision!r}")
         # "fp8": e4m3 QK^T / PV MFMAs in the attention forward of the bf16 path
         # (BASELINE config 5); the attention backward stays bf16
+        if attention_precision == "fp8" and precision in ("fp32", "float32"):
+            raise ValueError("hvit: attention_precision='fp8' runs inside the bf16 path; precision='fp32' "
+                             "cannot use it (use precision='bf16' or 'auto' under autocast)")
         self.attention_precision = attention_precision
+        self._fp8_warned = False
         self.last_num_tokens = 0  # patch tokens N of the latest forward (dp.GradAllReducer checks it)
 
         self.encoder = nn.ModuleList()
@@ -326,8 +330,50 @@ class HybridViT(nn.Module):
         self.__dict__.pop("_hvit_named_params", None)
         return super()._apply(fn, *args, **kwargs)
 
-    def _seed(self) -> int:
-        return int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
+    def _seed(self) -> Optional[torch.Tensor]:
+        """This training forward's dropout seed, as a one-word device tensor
+        (None in eval).  The seed stream lives on the device: a state
+        {base, counter} that hvit_rng_advance steps once per training forward,
+        writing the new seed to a fresh word that this forward's dropout sites
+        (and their backward) read.  So a captured train step (hipGraph) draws new
+        masks on every replay, and the masks of a replay sequence equal those of
+        the same number of eager steps from the same state.  ``base`` is drawn
+        from torch's host generator whenever that generator was re-seeded or
+        used since the previous draw (checked on eager forwards only), so
+        ``torch.manual_seed`` makes the dropout of the next forward
+        reproducible as with the reference's torch dropout."""
+        if not self.training:
+            return None
+        dev = torch.device("cuda", torch.cuda.current_device())
+        st = self.__dict__.get("_rng_state")
+        if st is None or st.device != dev:
+            st = torch.zeros(2, dtype=torch.int64, device=dev)
+            self.__dict__["_rng_state"] = st
+            self.__dict__["_rng_host"] = None
+        if not torch.cuda.is_current_stream_capturing():
+            gen = torch.default_generator
+            hs = self.__dict__.get("_rng_host")
+            if hs is None or not torch.equal(gen.get_state(), hs):
+                base = int(torch.randint(0, 2 ** 62, (1,)).item())
+                st[0].fill_(base)  # fill kernels: no host-device synchronisation
+                st[1].zero_()
+                self.__dict__["_rng_host"] = gen.get_state()
+        seed_t = torch.empty(1, dtype=torch.int64, device=dev)
+        L.call("hvit_rng_advance", st.data_ptr(), seed_t.data_ptr(), L.stream_ptr())
+        return seed_t
+
+    def set_dropout_state(self, base: int, counter: int = 0) -> None:
+        """Reset the device dropout seed stream (see _seed) to {base, counter}."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        st = torch.tensor([int(base) & 0x7FFFFFFFFFFFFFFF, int(counter)], dtype=torch.int64).to(dev)
+        self.__dict__["_rng_state"] = st
+        self.__dict__["_rng_host"] = torch.default_generator.get_state()
+
+    def dropout_state(self) -> Optional[torch.Tensor]:
+        """A copy of the device dropout seed state {base, counter} (None before
+        the first training forward)."""
+        st = self.__dict__.get("_rng_state")
+        return None if st is None else st.clone()
 
     def _prep_weights(self, dt: int, dev) -> None:
         """Cast / pack every weight this forward (and its backward) will use
@@ -369,7 +415,7 @@ class HybridViT(nn.Module):
             bn = blk.bn
             h = HF.ConvBNActFn.apply(h, None, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                      bn.num_batches_tracked, 1, blk.pool, self.training,
-                                     HF.Drop(blk.p, seed, 100 + i), bn.momentum, bn.eps, dt)
+                                     HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt)
             skips.append(h)
         return h, skips
 
@@ -379,7 +425,7 @@ class HybridViT(nn.Module):
         hw = (feat.shape[1] // P, feat.shape[2] // P)
         if self.cls_token is None:  # hot path: pos-embed add and dropout fused into the GEMM epilogue
             t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, self.pos_encoding.pos_embed, P,
-                                      HF.Drop(self.dropout_p, seed, 200), self.training, dt)
+                                      HF.Drop(self.dropout_p, 0, 200, seed), self.training, dt)
             self.last_num_tokens = t.shape[1]
             return t, hw
         t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, None, P, HF.Drop(), False, dt)
@@ -391,15 +437,21 @@ class HybridViT(nn.Module):
         if self.cls_token is not None:
             t = torch.cat([self.cls_token.expand(t.shape[0], -1, -1).float(), t.float()], 1)
         self.last_num_tokens = t.shape[1]
-        return HF.PosDropFn.apply(t, self.pos_encoding.pos_embed, HF.Drop(self.dropout_p, seed, 200), self.training)
+        return HF.PosDropFn.apply(t, self.pos_encoding.pos_embed, HF.Drop(self.dropout_p, 0, 200, seed), self.training)
 
     def _vit(self, t, dt, seed, want_attn=False):
         attns = []
+        if self.attention_precision == "fp8" and dt != L.BF16 and not self._fp8_warned:
+            import warnings
+            warnings.warn("hvit: attention_precision='fp8' is ignored: this forward runs the fp32 path "
+                          "(precision='auto' outside an autocast region)")
+            self._fp8_warned = True
         for l, blk in enumerate(self.transformer.blocks):
             a, m = blk.attn, blk.mlp.net
             base = 300 + 10 * l
-            drops = (HF.Drop(blk.p_attn, seed, base), HF.Drop(blk.p, seed, base + 1),
-                     HF.Drop(blk.p, seed, base + 2), HF.Drop(blk.p, seed, base + 3), seed ^ (base << 20))
+            drops = (HF.Drop(blk.p_attn, 0, base, seed), HF.Drop(blk.p, 0, base + 1, seed),
+                     HF.Drop(blk.p, 0, base + 2, seed), HF.Drop(blk.p, 0, base + 3, seed),
+                     HF.Drop(0.0, base << 20, 1, seed))
             t, probs = HF.ViTBlockFn.apply(t, blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias,
                                            a.proj.weight, a.proj.bias, blk.norm2.weight, blk.norm2.bias,
                                            m[0].weight, m[0].bias, m[3].weight, m[3].bias, a.num_heads, drops,
@@ -427,7 +479,7 @@ class HybridViT(nn.Module):
             bn = blk.bn
             x = HF.ConvBNActFn.apply(x, s, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                      bn.num_batches_tracked, blk.up, 1, self.training,
-                                     HF.Drop(blk.p, seed, 500 + i), bn.momentum, bn.eps, dt)
+                                     HF.Drop(blk.p, 0, 500 + i, seed), bn.momentum, bn.eps, dt)
         raise RuntimeError("hvit: decoder has no final layer")
 
     # -------------------------------------------------------- reference API --

@@ -80,7 +80,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
-                 max_grad_norm: Optional[float] = None, **unused):
+                 max_grad_norm: Optional[float] = None, capturable: bool = False, **unused):
         if amsgrad or maximize:
             raise NotImplementedError("hvit FusedAdamW: amsgrad / maximize are not implemented")
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
@@ -89,6 +89,32 @@ class FusedAdamW(torch.optim.Optimizer):
                                       maximize=False))
         self.max_grad_norm = max_grad_norm
         self.last_grad_norm: Optional[torch.Tensor] = None
+        # capturable (torch.optim.AdamW's flag): step counters live on the device
+        # (0-dim views of one buffer per group, bumped by one launch) and the bias
+        # corrections are computed there, so a captured step (hipGraph) replays
+        # with the right step count; otherwise CPU counters as torch's default
+        self.capturable = capturable
+        self._step_bufs: Dict[int, torch.Tensor] = {}
+
+    def _device_steps(self, gi: int, ps: list) -> torch.Tensor:
+        """The group's device step buffer, state["step"] of every parameter a
+        0-dim view of it (rebuilt eagerly from the current values when the
+        views were replaced, e.g. by load_state_dict)."""
+        buf = self._step_bufs.get(gi)
+        ok = buf is not None and buf.numel() == len(ps) and buf.device == ps[0].device
+        if ok:
+            base = buf.data_ptr()
+            ok = all(isinstance(self.state[p].get("step"), torch.Tensor) and self.state[p]["step"].data_ptr() == base + 4 * i
+                     for i, p in enumerate(ps))
+        if not ok:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("hvit FusedAdamW(capturable=True): run one eager step before capturing")
+            vals = [float(self.state[p]["step"]) if "step" in self.state[p] else 0.0 for p in ps]
+            buf = torch.tensor(vals, dtype=torch.float32).to(ps[0].device)
+            self._step_bufs[gi] = buf
+            for i, p in enumerate(ps):
+                self.state[p]["step"] = buf[i]
+        return buf
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -107,7 +133,7 @@ class FusedAdamW(torch.optim.Optimizer):
             # the kernel walks p, grad, exp_avg and exp_avg_sq as flat arrays: all
             # four must share one dense layout (a channels_last parameter with a
             # contiguous grad would pair the wrong elements)
-            if not p.is_contiguous() or p.grad.stride() != p.stride():
+            if not p.is_contiguous() or not p.grad.is_contiguous():
                 raise ValueError("hvit FusedAdamW: parameters and their gradients must be contiguous "
                                  "(a strided / channels_last parameter is not supported)")
         coef = None
@@ -115,7 +141,7 @@ class FusedAdamW(torch.optim.Optimizer):
             coef = _clip_coef([p.grad for p in live], self.max_grad_norm)
             self.last_grad_norm = coef[0]
         stream = L.stream_ptr(live[0].device)
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             by_step: Dict[float, list] = {}
             ps_live = []
@@ -123,18 +149,29 @@ class FusedAdamW(torch.optim.Optimizer):
                 if p.grad is None:
                     continue
                 st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0)
+                if "exp_avg" not in st:
+                    st.setdefault("step", torch.tensor(0.0))
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 ps_live.append(p)
-            # per-parameter step counters stay CPU tensors (torch.optim.AdamW's
-            # state_dict format); one multi-tensor add instead of one op each
-            steps = [self.state[p]["step"] for p in ps_live]
-            if steps:
-                torch._foreach_add_(steps, 1.0)
-            for p, t in zip(ps_live, steps):
-                by_step.setdefault(t.item(), []).append(p)
+            if self.capturable:
+                # device counters: one bump launch, bias corrections on the device
+                gp = [p for p in group["params"] if p.requires_grad]
+                buf = self._device_steps(gi, gp)
+                if len(ps_live) == len(gp):
+                    L.call("hvit_step_bump", buf.data_ptr(), buf.numel(), 1.0, stream)
+                else:
+                    for p in ps_live:
+                        L.call("hvit_step_bump", self.state[p]["step"].data_ptr(), 1, 1.0, stream)
+                by_step = {None: ps_live} if ps_live else {}
+            else:
+                # per-parameter step counters stay CPU tensors (torch.optim.AdamW's
+                # state_dict format); one multi-tensor add instead of one op each
+                steps = [self.state[p]["step"] for p in ps_live]
+                if steps:
+                    torch._foreach_add_(steps, 1.0)
+                for p, t in zip(ps_live, steps):
+                    by_step.setdefault(t.item(), []).append(p)
             for step, ps in by_step.items():
                 items = (L.AdamWItem * len(ps))()
                 for i, p in enumerate(ps):
@@ -143,9 +180,9 @@ class FusedAdamW(torch.optim.Optimizer):
                     sh = HF.shadow_of(p)
                     items[i] = L.AdamWItem(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
                                            st["exp_avg_sq"].data_ptr(), sh.data_ptr() if sh is not None else None,
-                                           p.numel())
-                hp = L.AdamWHyper(float(group["lr"]), b1, b2, group["eps"], group["weight_decay"],
-                                  1.0 - b1 ** step, 1.0 - b2 ** step)
+                                           p.numel(), st["step"].data_ptr() if step is None else None)
+                bc1, bc2 = (1.0, 1.0) if step is None else (1.0 - b1 ** step, 1.0 - b2 ** step)
+                hp = L.AdamWHyper(float(group["lr"]), b1, b2, group["eps"], group["weight_decay"], bc1, bc2)
                 L.call("hvit_adamw", len(ps), items, hp, coef.data_ptr() if coef is not None else None, stream)
                 for p in ps:
                     if _bump is not None:

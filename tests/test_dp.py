@@ -172,7 +172,20 @@ def _worker_accum(rank, world, port, mode, q):
             red.finish()
         except RuntimeError:
             raised = True
-        q.put((rank, max(errs), raised))
+        # only rank 0 exceeds the bound: the ranks agree on the maximum first,
+        # so EVERY rank raises (none is left waiting in a bucket collective)
+        raised_one = False
+        model.zero_grad(set_to_none=True)
+        model(torch.randn(4, 20 if rank == 0 else 10, 8)).backward()
+        try:
+            red.finish()
+        except RuntimeError:
+            raised_one = True
+        # and the reducer still works afterwards
+        model.zero_grad(set_to_none=True)
+        model(torch.randn(4, 10, 8)).backward()
+        red.finish()
+        q.put((rank, max(errs), raised and raised_one))
     finally:
         dist.destroy_process_group()
 

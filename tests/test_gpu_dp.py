@@ -109,3 +109,26 @@ def test_dp_hybridvit_two_ranks_on_one_gpu():
         assert beyond == 0.0
         assert bn_same             # rank 0's running statistics on every rank
     assert torch.equal(out[0][6], out[1][6])  # bit-identical replicas after 3 optimizer steps
+
+
+def test_rccl_world1_bench_dp_branch():
+    """BASELINE config 4's code path on RCCL: bench.py's DP branch
+    (init_process_group("nccl", device_id=cuda:0), broadcast_module,
+    GradAllReducer over RCCL every step, FusedAdamW) launched through
+    torch.distributed.run at world size 1 on the box's one GPU
+    (HVIT_FORCE_DIST=1).  The 8-GPU scaling run is the driver's."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, HVIT_FORCE_DIST="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--steps", "3",
+           "--warmup", "1", "--batch", "4", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["config"]["dist_backend"] == "nccl"
+    assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1"
+    assert out["launch"] == "eager"
+    assert out["value"] > 0 and abs(out["final_loss"]) < 1e3

@@ -185,3 +185,147 @@ def test_train_step_cuda_graph_capture(hv):
     torch.cuda.synchronize()
     assert static_loss.item() < l_first
     assert any(not torch.equal(p.detach(), q) for p, q in zip(ma.parameters(), p0))
+
+
+def test_train_step_graph_with_dropout_and_device_counters(hv):
+    """The bench's graph mode: a whole bf16 train step WITH dropout (p = 0.1
+    everywhere, DropPath 0.1) and FusedAdamW(capturable=True) captured once and
+    replayed.  The dropout seed stream and the AdamW step counters live on the
+    device, so every replay draws new masks and applies its own bias
+    corrections: the parameters after each replay match an eager copy driven
+    through the same number of steps from the same seed state."""
+    kw = dict(KW, precision="bf16")
+    torch.manual_seed(0)
+    ma = hv.HybridViT(**kw).to(DEV).train()
+    mb = copy.deepcopy(ma)
+    oa = hv.FusedAdamW(ma.parameters(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, capturable=True)
+    ob = hv.FusedAdamW(mb.parameters(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, capturable=True)
+    crit = hv.CombinedLoss()
+    x, t = _batches(1, 4)[0]
+
+    def step(m, o):
+        loss = crit(m(x), t)
+        loss.backward()
+        o.step()
+        o.zero_grad(set_to_none=True)
+        return loss
+
+    ma.set_dropout_state(12345)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step(ma, oa)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_loss = step(ma, oa)
+    mb.set_dropout_state(12345)
+    for _ in range(2):
+        step(mb, ob)
+    losses = []
+    for r in range(5):
+        g.replay()
+        lb = step(mb, ob)
+        torch.cuda.synchronize()
+        losses.append(static_loss.item())
+        assert abs(static_loss.item() - lb.item()) <= 2e-3 * abs(lb.item()), (r, static_loss.item(), lb.item())
+        for (k, pa), pb in zip(ma.named_parameters(), mb.parameters()):
+            tol = 2e-3 * pb.detach().abs().max().item() + 1e-6
+            assert (pa.detach() - pb.detach()).abs().max().item() <= tol, (r, k)
+    assert len(set(losses)) == len(losses)  # every replay is a new step
+    assert torch.equal(ma.dropout_state(), mb.dropout_state())
+    assert int(ma.dropout_state()[1]) == 7  # 2 warm-up forwards + 5 replays (capture runs nothing)
+    st = oa.state[next(ma.parameters())]["step"]
+    assert st.is_cuda and float(st) == 7.0
+
+
+def test_graph_replays_draw_new_dropout_masks(hv):
+    """Forward-only capture in train mode (fp32): two replays give different
+    outputs (new masks), equal bit for bit to two eager forwards from the same
+    device seed state; two forwards before one backward keep their own masks
+    (each forward's seed has its own device word)."""
+    kw = dict(KW, precision="fp32")
+    torch.manual_seed(1)
+    m = hv.HybridViT(**kw).to(DEV).train()
+    x, _ = _batches(1, 5)[0]
+    m.set_dropout_state(999)
+    with torch.no_grad():
+        e1 = m(x).clone()
+        e2 = m(x).clone()
+    assert not torch.equal(e1, e2)
+    m.set_dropout_state(999)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side), torch.no_grad():
+        with torch.cuda.graph(g):
+            y = m(x)
+    torch.cuda.current_stream().wait_stream(side)
+    g.replay()
+    r1 = y.clone()
+    g.replay()
+    r2 = y.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(r1, e1) and torch.equal(r2, e2)
+    # two forwards, then one backward through both: each uses its own masks
+    mb = copy.deepcopy(m)
+    m.set_dropout_state(5)
+    mb.set_dropout_state(5)
+    xa = x.clone().requires_grad_(True)
+    (m(xa).sum() + 2.0 * m(xa).sum()).backward()
+    xb = x.clone().requires_grad_(True)
+    mb(xb).sum().backward()
+    ga = xb.grad.clone()
+    xb.grad = None
+    (2.0 * mb(xb).sum()).backward()
+    gb = ga + xb.grad
+    torch.cuda.synchronize()
+    assert (xa.grad - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
+
+
+def test_fused_adamw_capturable_matches_torch(hv):
+    """FusedAdamW(capturable=True) step captured once, replayed 5 times with
+    fresh gradients each time: device step counters give torch.optim.AdamW's
+    bias corrections step by step."""
+    torch.manual_seed(2)
+    shapes = [(64, 32), (128,), (3, 5, 7)]
+    pa = [torch.randn(s, device=DEV, requires_grad=True) for s in shapes]
+    pb = [p.detach().clone().requires_grad_(True) for p in pa]
+    oa = hv.FusedAdamW(pa, lr=1e-2, betas=(0.9, 0.99), weight_decay=0.05, capturable=True)
+    ob = torch.optim.AdamW(pb, lr=1e-2, betas=(0.9, 0.99), weight_decay=0.05)
+    grads = [[torch.randn(s, device=DEV) for s in shapes] for _ in range(7)]
+    static = [torch.zeros(s, device=DEV) for s in shapes]
+    for p, s in zip(pa, static):
+        p.grad = s
+    # one eager step (device counters created), then capture
+    for s, gsrc in zip(static, grads[0]):
+        s.copy_(gsrc)
+    oa.step()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g):
+            oa.step()
+    torch.cuda.current_stream().wait_stream(side)
+    for p, gsrc in zip(pb, grads[0]):
+        p.grad = gsrc.clone()
+    ob.step()
+    for i in range(1, 6):
+        for s, gsrc in zip(static, grads[i]):
+            s.copy_(gsrc)
+        g.replay()
+        for p, gsrc in zip(pb, grads[i]):
+            p.grad = gsrc.clone()
+        ob.step()
+        torch.cuda.synchronize()
+        for a, b in zip(pa, pb):
+            assert (a.detach() - b.detach()).abs().max().item() <= 2e-6 * (1 + b.detach().abs().max().item()), i
+    assert float(oa.state[pa[0]]["step"]) == 6.0
+    # state_dict round trip keeps counting on the device
+    sd = oa.state_dict()
+    oc = hv.FusedAdamW([p.detach().clone().requires_grad_(True) for p in pa], lr=1e-2, betas=(0.9, 0.99),
+                       weight_decay=0.05, capturable=True)
+    oc.load_state_dict(sd)
+    assert float(oc.state_dict()["state"][0]["step"]) == 6.0
