@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-3 GPU-box session: steps run in order, each under its own time limit;
+# the script stops at the first crash / timeout.  Usage: tools/r3_check.sh TAG step...
+#   tests[:file,...]  GPU test files (default: all tests/test_gpu_*.py)
+#   bench             default bench.py line (graph mode, CPU baseline)
+#   benchq            bench.py without the CPU baseline
+#   eager             bench.py --graph 0 --no-cpu-baseline
+#   prof              rocprofv3 kernel stats of a short bench
+#   gemm              tools/gemm_bench.py
+cd "$(dirname "$0")/.."
+TAG=${1:-run}; shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for s in "$@"; do
+  case $s in
+    tests*)
+      files=${s#tests}; files=${files#:}
+      if [ -z "$files" ]; then files=$(ls tests/test_gpu_*.py); else files=$(echo $files | tr ',' ' '); fi
+      for f in $files; do
+        timeout -k 10 900 python -u -m pytest "$f" -q -m gpu -rf --maxfail=40 -p no:cacheprovider \
+          --timeout 300 --timeout-method thread > "gpurun_out/${TAG}_$(basename $f .py).log" 2>&1
+        rc=$?
+        tail -5 "gpurun_out/${TAG}_$(basename $f .py).log"
+        if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $f exited $rc"; exit $rc; fi
+      done ;;
+    bench) timeout -k 10 600 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 || exit $? ;;
+    benchq) timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/${TAG}_benchq.log 2>&1 || exit $? ;;
+    eager) timeout -k 10 400 python -u bench.py --graph 0 --no-cpu-baseline > gpurun_out/${TAG}_eager.log 2>&1 || exit $? ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
+    gemm) timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/${TAG}_gemm.log 2>&1 || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  echo "step $s ok"
+done
