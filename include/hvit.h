@@ -93,6 +93,19 @@ int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int
 int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, int N, int K, void* dx, int dx_dt,
                       const hvit_epilogue_t* epi, void* stream);                 /* dx[M,K] = dy[M,N] w */
 long long hvit_wgrad_workspace(int M, int N, int K);                              /* f32 elements */
+/* The same with the split-K partial sums reduced inside the GEMM launch (the
+ * last K slice of each output tile sums the slabs; no separate reduction
+ * launch): tickets = hvit_wgrad_tickets(M, N, K) uint32 arrival counters, zeroed
+ * by the caller when flags has HVIT_ACC_ZEROED (else the call clears them);
+ * they are left zeroed.  Falls back to the two-launch form where the ring
+ * kernels do not apply. */
+long long hvit_wgrad_tickets(int M, int N, int K);
+int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db, float* ws,
+                         long long ws_elems, unsigned* tickets, long long tickets_elems, int flags, void* stream);
+/* Tuning knob (A/B measurements): what 0 = GEMM pipeline of the bf16 linears
+ * (0: two-stage kernels; 1-4: LDS-ring configurations, gemm_ring.h).  Returns
+ * the previous value (-1 for an unknown knob). */
+int hvit_gemm_tune(int what, int value);
 int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                       float* ws, long long ws_elems, void* stream);  /* dw[N,K] = dy^T x; db[N] = colsum(dy)
                                                                         (nullable; fused when db == dw + N*K) */                        /* dw[N,K] = dy^T x */

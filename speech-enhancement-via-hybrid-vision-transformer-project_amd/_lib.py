@@ -78,6 +78,8 @@ _SIGS = {
     "hvit_linear_dgrad": ([i32, vp, vp, i32, i32, i32, vp, i32, P(Epilogue), vp], i32),
     "hvit_wgrad_workspace": ([i32, i32, i32], i64),
     "hvit_linear_wgrad": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp], i32),
+    "hvit_wgrad_tickets": ([i32, i32, i32], i64),
+    "hvit_linear_wgrad_tk": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp, i64, i32, vp], i32),
     "hvit_conv_fwd": ([i32, P(ConvGeom), vp, vp, vp, i32, vp, P(Epilogue), vp], i32),
     "hvit_conv_dgrad": ([i32, P(ConvGeom), vp, vp, vp, i32, vp], i32),
     "hvit_conv_wgrad_workspace": ([P(ConvGeom)], i64),
@@ -116,6 +118,7 @@ _SIGS = {
     "hvit_scale_tensors": ([i32, P(TensorRef), vp, vp], i32),
     "hvit_adamw": ([i32, P(AdamWItem), P(AdamWHyper), vp, vp], i32),
     "hvit_rng_advance": ([vp, vp, vp], i32),
+    "hvit_gemm_tune": ([i32, i32], i32),
     "hvit_step_bump": ([vp, i32, f32, vp], i32),
 }
 
@@ -136,7 +139,10 @@ def lib():
                         f"hvit: native library not found at {LIB_PATH}; run __graft_entry__.build() "
                         "(there is no CPU or PyTorch fallback for the HIP path)")
                 h = C.CDLL(LIB_PATH)
+                alt = "HVIT_LIB" in os.environ  # an older in-tree build for A/B: tolerate missing entry points
                 for name, (args, res) in _SIGS.items():
+                    if alt and not hasattr(h, name):
+                        continue
                     fn = getattr(h, name)
                     fn.argtypes = args
                     fn.restype = res

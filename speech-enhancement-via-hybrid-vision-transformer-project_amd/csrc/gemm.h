@@ -369,6 +369,8 @@ struct Epi {
   float* stats = nullptr;   // BN partials [64-row tile][N][2] = (mean, M2)
   float* colsum = nullptr;  // atomic column sums of the final v
   long slab_stride = 0;     // EPI_SLAB: elements between split-K slabs (0: M * ldo)
+  unsigned* tickets = nullptr;  // EPI_SLAB (ring kernels): per-tile arrival counters, zeroed; the last
+  float* red_out = nullptr;     //   slice of a tile sums the slabs into red_out (ld = ldo) in-kernel
   float* rs_ptr = nullptr;  // row sums of the A operand (wgrad bias grad): rs_ptr[z * rs_stride + m]
   long rs_stride = 0;
   bool vec_ok = false;      // N % 4 == 0, every operand 16-B aligned with ld % 4 == 0
@@ -556,14 +558,16 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
 
 // k-major ("MN") bf16 tile, [64 k][R rows] with 2R-byte rows and no padding:
 // the 16-byte chunk c of row k sits at chunk c ^ swz(k), swz(k) = 2(k&3) ^
-// 8((k>>3)&1) (R = 128) or 2((k>>1)&1) ^ 4((k>>3)&1) (R = 64).  Conflict-free
+// 8((k>>3)&1) (R = 128 and 256: every row starts a 256-B bank row, so the 8
+// rows of one 32-lane half of a transposed read land on 8 distinct even 16-B
+// slots) or 2((k>>1)&1) ^ 4((k>>3)&1) (R = 64).  Conflict-free
 // for the 16x16x32 operand fragments read with two ds_read_b64_tr_b16 (checked
 // exhaustively) and for the ds_write_b128 of 8 lanes filling one row; the same
 // layout as the LDS-DMA MN image (DmaImg), which applies the swizzle on the
 // source side.
 template <int R>
 struct MnSwz {
-  static_assert(R == 64 || R == 128, "MN tile: 64 or 128 rows");
+  static_assert(R == 64 || R == 128 || R == 256, "MN tile: 64, 128 or 256 rows");
   static constexpr int ROWB = 2 * R;
   __device__ __forceinline__ static int swz(int k) {
     return R >= 128 ? ((2 * (k & 3)) ^ (8 * ((k >> 3) & 1))) : ((2 * ((k >> 1) & 1)) ^ (4 * ((k >> 3) & 1)));
@@ -845,7 +849,7 @@ struct DmaImg {
   static constexpr int BYTES = R * KSTAGE;          // one stage: 64 k x R rows x 2 B
   static constexpr int PIECES = BYTES / 1024;       // DMA wave-instructions per stage
   static constexpr int RPP = 1024 / ROWB;           // LDS rows per piece
-  static_assert(KC || R == 64 || R == 128, "MN DMA image: 64 or 128 rows");
+  static_assert(KC || R == 64 || R == 128 || R == 256, "MN DMA image: 64, 128 or 256 rows");
   __device__ __forceinline__ static int swz(int k) { return MnSwz<KC ? 128 : R>::swz(k); }
   // byte offset (from the tile's origin element) that `lane` fetches for piece pc
   __device__ __forceinline__ static unsigned src_off(int pc, int lane, long ld) {
@@ -957,7 +961,7 @@ struct GemmCoreDma {
     auto issue = [&](int t) {
       char* abuf = smem + (NB == 2 ? (t & 1) : 0) * (IA::BYTES + IB::BYTES);
       char* bbuf = abuf + IA::BYTES;
-      const unsigned sb = ob + (unsigned)t * db;
+      const unsigned sb = ob + (unsigned)(t < nk ? t : nk - 1) * db;
       if constexpr (CONV) {
         const bool first = c0 < la.C1;  // uniform
         const int Cx = first ? la.C1 : la.C2;
@@ -980,7 +984,7 @@ struct GemmCoreDma {
           }
         }
       } else {
-        const unsigned sa = oa + (unsigned)t * da;
+        const unsigned sa = oa + (unsigned)(t < nk ? t : nk - 1) * da;
 #pragma unroll
         for (int i = 0; i < PA; ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(ra,
@@ -1042,22 +1046,48 @@ struct GemmCoreDma {
       }
       return;
     }
+    // Two buffers, one barrier per stage: stage t+1's DMA is issued inside
+    // stage t's compute, spread over k-step 0's MFMAs (an LDS-DMA piece costs
+    // its wave ~60-180 issue cycles: issued as one block they left the matrix
+    // pipe idle), into the buffer every wave released before the barrier that
+    // opened stage t (its reads of stage t-1 were waited for before its
+    // MFMAs).  The last stage issues a never-read stage (zeros past the
+    // operand or the next slice's bytes) into that free buffer, so the loop
+    // body is uniform; it is drained before the epilogue reuses LDS.
+    // Measured (tools/ring_bench.py probes, 8192x2048, K = 2048): 853 -> 1042
+    // TFLOP/s against the two-barrier loop with the DMA issued in a block.
+    constexpr int MPD = (FM * FN) / INFLIGHT > 0 ? (FM * FN) / INFLIGHT : 1;
     issue(0);
     for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) {
-        issue(t + 1);
-        __builtin_amdgcn_s_waitcnt(0x0F70 | INFLIGHT);  // vmcnt(INFLIGHT): stage t landed (for this wave)
-      } else {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): stage t landed (for this wave)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // ... for every wave; buffer (t+1) & 1 is free
+      asm volatile("" ::: "memory");
+      const char* at = smem + (t & 1) * (IA::BYTES + IB::BYTES);
+      const char* bt = at + IA::BYTES;
+      u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+      load(at, bt, 0, fa0, fb0);
+      lgkm_wait0();
+      lds_pin(fa0);
+      lds_pin(fb0);
+      load(at, bt, 1, fa1, fb1);
+      issue(t + 1);
+      mma(fa0, fb0);
+      __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);  // k-step 1 fragment reads first
+#pragma unroll
+      for (int k = 0; k < INFLIGHT && MPD * (k + 1) <= FM * FN; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MPD, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // one DMA piece
       }
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's stage-t pieces have landed
-      asm volatile("" ::: "memory");
-      compute(t);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // buffer t & 1 is free for stage t + 2
-      asm volatile("" ::: "memory");
+      lgkm_wait0();
+      lds_pin(fa1);
+      lds_pin(fb1);
+      mma(fa1, fb1);
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // the trailing stage's DMA
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
 };
 

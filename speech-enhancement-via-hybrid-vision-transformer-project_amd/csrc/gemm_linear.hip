@@ -1,5 +1,6 @@
 // C-ABI Linear fwd / dgrad / wgrad on the MFMA GEMM (see gemm_host.h).
 #include "gemm_host.h"
+#include "gemm_ring.h"
 
 extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int M, int N, int K,
                                void* y, int y_dt, const hvit_epilogue_t* epi, void* stream) {
@@ -9,6 +10,12 @@ extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float
   if (int rc = check_epi(epi)) return rc;
   Epi ep = to_epi(epi, y, y_dt, N);
   ep.bias = bias;
+  if (dt == HVIT_BF16) {
+    int rc = 0;
+    if (try_ring(dense<bf16_t, true>(x, K, M, K), dense<bf16_t, true>(w, K, N, K), M, N, K, 1, ep,
+                 (hipStream_t)stream, &rc))
+      return rc;
+  }
   DT_DISPATCH(dt, {
     HVIT_CHECK(K % Elem<T>::PER16 == 0, "hvit_linear_fwd: K=%d must be a multiple of %d", K, Elem<T>::PER16);
     return launch_gemm<T>(dense<T, true>(x, K, M, K), dense<T, true>(w, K, N, K), M, N, K, 1, ep,
@@ -23,6 +30,12 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
   HVIT_CHECK(aligned16(dy) && aligned16(w), "hvit_linear_dgrad: alignment");
   if (int rc = check_epi(epi)) return rc;
   Epi ep = to_epi(epi, dx, dx_dt, K);
+  if (dt == HVIT_BF16 && N % 8 == 0) {
+    int rc = 0;
+    if (try_ring(dense<bf16_t, true>(dy, N, M, N), dense<bf16_t, false>(w, K, K, N), M, K, N, 1, ep,
+                 (hipStream_t)stream, &rc))
+      return rc;
+  }
   DT_DISPATCH(dt, {
     HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_dgrad: N, K alignment");
     return launch_gemm<T>(dense<T, true>(dy, N, M, N), dense<T, false>(w, K, K, N), M, K, N, 1, ep,
@@ -32,16 +45,40 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
 
 extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
   // dw is [N_out x K_in] reduced over M rows; slabs only when splitting, each
-  // slab followed by N_out bias partials
-  int s = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
+  // slab followed by N_out bias partials (enough for every tile configuration
+  // the entry point may pick: gemm.h's 128x128, the ring's 128x128 / 128x64)
+  int s = std::max(wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN), wgrad_splits(N, K, M, 128, 64));
   return s > 1 ? (long long)s * ((long long)N * K + N) : 0;
+}
+
+// per-tile arrival counters of the in-kernel split-K reduction (ring kernels;
+// the smallest tile any configuration uses, 128x64)
+extern "C" long long hvit_wgrad_tickets(int M, int N, int K) {
+  (void)M;
+  return (long long)cdiv(N, 128) * cdiv(K, 64);
 }
 
 // db (nullable): bias gradient sum_m dy[m][n].  The fused path (bf16, db ==
 // dw + N*K) takes it from the A tiles the wgrad GEMM already stages (row sums
 // over the token reduction); otherwise a column reduction of dy.
+static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                             float* ws, long long ws_elems, unsigned* tickets, long long tickets_elems, int flags,
+                             void* stream);
+
 extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                                  float* ws, long long ws_elems, void* stream) {
+  return linear_wgrad_impl(dt, dy, x, M, N, K, dw, db, ws, ws_elems, nullptr, 0, 0, stream);
+}
+
+extern "C" int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                                    float* ws, long long ws_elems, unsigned* tickets, long long tickets_elems, int flags,
+                                    void* stream) {
+  return linear_wgrad_impl(dt, dy, x, M, N, K, dw, db, ws, ws_elems, tickets, tickets_elems, flags, stream);
+}
+
+static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                             float* ws, long long ws_elems, unsigned* tickets, long long tickets_elems, int flags,
+                             void* stream) {
   HVIT_CHECK(dy && x && dw, "hvit_linear_wgrad: null pointer");
   HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_wgrad: bad shape");
   HVIT_CHECK(aligned16(dy) && aligned16(x), "hvit_linear_wgrad: alignment");
@@ -57,6 +94,35 @@ extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, i
   // HVIT_NO_RS=1: bias grad by a separate column reduction (A/B measurements only)
   static const bool no_rs = getenv("HVIT_NO_RS") && atoi(getenv("HVIT_NO_RS"));
   const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK && !no_rs;
+  // ring-pipelined kernels (gemm_ring.h) for bf16 without fused bias row sums
+  const int rcfg = ring_default_cfg() >= 0 ? ring_default_cfg() : ring_pick(false, false, N, K, M);
+  if (dt == HVIT_BF16 && !fused_db && N % 8 == 0 && K % 8 == 0 && rcfg > 0) {
+    const RingCfg r = ring_cfg(rcfg);
+    int s = wgrad_splits(N, K, M, r.bm, r.bn);
+    if ((long long)s * (NK + N) > ws_elems || !ws) s = 1;
+    s = plan_splits<bf16_t>(M, s);
+    Epi e;
+    e.out_dt = HVIT_F32;
+    e.ldo = K;
+    e.mode = s > 1 ? EPI_SLAB : EPI_STORE;
+    e.out = s > 1 ? (void*)ws : (void*)dw;
+    e.slab_stride = NK + N;
+    // in-kernel reduction when the caller provides the ticket counters
+    const bool tk = s > 1 && tickets && tickets_elems >= (long long)(N / r.bm) * (K / r.bn);
+    if (tk) {
+      e.tickets = tickets;
+      e.red_out = dw;
+      if (!(flags & HVIT_ACC_ZEROED)) (void)hipMemsetAsync(tickets, 0, sizeof(unsigned) * (N / r.bm) * (K / r.bn), st);
+    }
+    int rc = 0;
+    if (try_ring(dense<bf16_t, false>(dy, N, N, M), dense<bf16_t, false>(x, K, K, M), N, K, M, s, e, st, &rc, rcfg)) {
+      if (rc) return rc;
+      if (s > 1 && !tk)
+        if (int rc2 = hvit_sum_slabs_strided(ws, s, NK + N, NK, dw, stream)) return rc2;
+      if (db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
+      return HVIT_OK;
+    }
+  }
   Epi ep;
   ep.out_dt = HVIT_F32;
   ep.ldo = K;
@@ -90,3 +156,14 @@ extern "C" int hvit_debug_gemm_stamps(unsigned long long* host, int n) {
              : 1;
 }
 #endif
+
+// Tuning knob for A/B measurements (tools/ring_bench.py): what 0 = the ring
+// GEMM configuration of the bf16 linears (-1 = automatic per shape, 0 =
+// gemm.h's kernels only, 1-5 = one ring configuration; see gemm_ring.h).
+// Returns the previous value.
+extern "C" int hvit_gemm_tune(int what, int value) {
+  if (what != 0) return -1;
+  const int old = ring_cfg_ref();
+  ring_cfg_ref() = value;
+  return old;
+}

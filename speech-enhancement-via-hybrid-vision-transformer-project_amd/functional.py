@@ -235,9 +235,17 @@ def col_sum(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
     return out
 
 
-def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad"):
+def wgrad_tickets(M, N, K) -> int:
+    """uint32 counters the in-kernel split-K reduction of linear_wgrad needs."""
+    return int(L.lib().hvit_wgrad_tickets(M, N, K))
+
+
+def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=None):
     """dw [N, K] = dy^T x (f32); with ``bias`` also db [N] = colsum(dy), which
-    the bf16 path fuses into the GEMM (db stored right after dw)."""
+    the bf16 path fuses into the GEMM (db stored right after dw).  ``tickets``
+    (a zeroed f32 tensor of at least wgrad_tickets(M, N, K) elements, e.g. a
+    slice of the forward's zero pool): the split-K partials are reduced inside
+    the GEMM launch (no second launch, no slab re-read pass)."""
     buf = torch.empty(N * K + (N if bias else 0), dtype=torch.float32, device=dy.device)
     dw = buf[:N * K].view(N, K)
     db = buf[N * K:] if bias else None
@@ -245,8 +253,12 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad"):
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
 
     def launch():
-        call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db), ws.data_ptr(),
-             ws_n, stream_ptr())
+        if tickets is not None:
+            call("hvit_linear_wgrad_tk", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db),
+                 ws.data_ptr(), ws_n, tickets.data_ptr(), tickets.numel(), L.ACC_ZEROED, stream_ptr())
+        else:
+            call("hvit_linear_wgrad", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ptr(db),
+                 ws.data_ptr(), ws_n, stream_ptr())
 
     with timed(tag, 2.0 * M * N * K):
         launch()
