@@ -188,6 +188,27 @@ int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const flo
                     const void* dy, int dy_dt, int training, void* dz, int dz_dt, float* sums, int flags,
                     void* stream);
 
+/* ---- The first encoder ConvBlock fused (hybrid_vit.py:196-208 -> components.py:
+ * 55-85 with Cin = 1: Conv3x3 no bias -> BatchNorm2d -> ReLU -> Dropout2d ->
+ * MaxPool2d(pool)), the conv output z never stored: hvit_c1block_stats writes
+ * the BatchNorm partials of z (hvit_conv_fwd's layout, tile rows =
+ * hvit_conv_bn_tile_rows) for hvit_bn_finalize; hvit_c1block_fwd recomputes z
+ * and writes the pooled output y [N, H/pool, W/pool, Cout]; hvit_c1block_bwd
+ * recomputes z, forms dz (hvit_bn_act_bwd's arithmetic) and reduces it straight
+ * into the weight gradient dw_packed [Cout][9] f32 (sums as in hvit_bn_act_bwd,
+ * ws = hvit_c1block_bwd_ws floats).  g: C1 = 1, C2 = 0, U = 1, KS = 3, stride 1,
+ * pad 1, Cout a power of two <= 256.  There is no input gradient (the model
+ * input). */
+int hvit_c1block_stats(int dt, const hvit_conv_geom_t* g, const void* w_packed, float* bn_partials, void* stream);
+int hvit_c1block_fwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* mean,
+                     const float* invstd, const float* gamma, const float* beta, const hvit_dropout_t* dropout2d,
+                     int pool, void* y, int y_dt, void* stream);
+long long hvit_c1block_bwd_ws(const hvit_conv_geom_t* g, int pool);
+int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* mean, const float* invstd,
+                     const float* gamma, const float* beta, const hvit_dropout_t* dropout2d, int pool, const void* dy,
+                     int dy_dt, int training, float* sums, int flags, float* dw_packed, float* ws,
+                     long long ws_elems, void* stream);
+
 /* ---- Resampling (F.interpolate bilinear align_corners=False, hybrid_vit.py:
  * 381-386 and :459-465; nearest x2 backward + concat split, components.py:146,
  * hybrid_vit.py:389).  NHWC. */

@@ -98,6 +98,11 @@ _SIGS = {
     "hvit_bn_act_bwd": ([i32, vp, i32, i32, i32, i32, vp, vp, vp, vp, P(Dropout), i32, vp, i32, i32, vp,
                          i32, vp, i32, vp], i32),
     "hvit_bn_act_bwd_sums_elems": ([i32], i64),
+    "hvit_c1block_stats": ([i32, P(ConvGeom), vp, vp, vp], i32),
+    "hvit_c1block_fwd": ([i32, P(ConvGeom), vp, vp, vp, vp, vp, P(Dropout), i32, vp, i32, vp], i32),
+    "hvit_c1block_bwd_ws": ([P(ConvGeom), i32], i64),
+    "hvit_c1block_bwd": ([i32, P(ConvGeom), vp, vp, vp, vp, vp, P(Dropout), i32, vp, i32, i32, vp, i32, vp, vp,
+                          i64, vp], i32),
     "hvit_bilinear_fwd":([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_bilinear_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "hvit_upsample_split_bwd": ([vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp], i32),

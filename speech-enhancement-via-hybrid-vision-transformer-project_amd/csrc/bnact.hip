@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
   }
 }
 
-// backward reduce pass (training): per-channel sums of the routed gradient g
+// backward reduce pass (both modes): per-channel sums of the routed gradient g
 // and of g * xhat over full pooling windows.  Software-pipelined: the next
 // window's z taps and dy are loaded (raw) before the current one is reduced,
 // so every thread keeps two windows of loads in flight.
@@ -478,7 +478,7 @@ static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* su
   const long total = (long)a.N * ((a.H + P - 1) / P) * ((a.W + P - 1) / P) * (a.C / cv);
   if (total <= 0) return HVIT_OK;
   dim3 g(grid_for(total, BN_GRID_SUMS)), ga(grid_for(total, BN_GRID_APPLY));
-  if (training) {
+  {  // the sums are dbeta / dgamma in both modes; only training-mode dz uses them
     const long tsum = (long)a.N * (a.H / P) * (a.W / P) * (a.C / cv);
     if (tsum > 0)
       hipLaunchKernelGGL((bnact_sums_kernel<T, TD>), dim3(grid_for(tsum, BN_GRID_SUMS)), dim3(256), 0, st,

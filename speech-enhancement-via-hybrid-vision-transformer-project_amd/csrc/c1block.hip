@@ -1,0 +1,571 @@
+// The first encoder ConvBlock (components.py:15-99 via hybrid_vit.py:196-208:
+// Conv3x3 Cin=1 no-bias -> BatchNorm2d -> ReLU -> Dropout2d -> MaxPool2d) as
+// one fused block that never stores the conv output z (gfx950).
+//
+// At B=32 z is [32, 256, 256, 64] = 268 MB in bf16; the unfused path wrote it
+// once and read it three times (BN apply, the backward's two passes), then
+// wrote and re-read the same volume again as dz for the weight gradient.  A
+// Cin = 1 3x3 conv is 9 MACs per output, so recomputing z from the 4 MB input
+// inside each pass costs far less than moving it:
+//   stats : z on the fly -> BatchNorm (mean, M2) tile partials   (thinconv.hip c1_fwd, no z store)
+//   apply : z on the fly -> BN, ReLU, Dropout2d, max-pool -> y    (reads x, writes y)
+//   sums  : z on the fly + dy -> per-channel (sum g, sum g xhat)  (training backward)
+//   bwd   : z on the fly + dy -> dz in registers -> dW += dz * x  (no dz in HBM)
+// A workgroup owns RB pooled rows of one sample: it stages the RB*P + 2 input
+// rows they need (zero padded) in LDS; a thread owns CV channels with their
+// 9*CV weights in registers and walks pooling windows, reading each window's
+// (P+2)^2 input patch from LDS once.  Dropout2d multipliers are bnact.hip's
+// counter hash of (sample, channel) and the max-pool routing is its
+// first-maximum rule, so the fused and unfused paths implement the same
+// function (z is kept in f32 here instead of being rounded to bf16 in HBM).
+#include <type_traits>
+
+#include "common.h"
+
+namespace hvit_c1 {
+
+constexpr int BN_SLOTS = 32;  // the hvit_bn_act_bwd_sums_elems layout (bnact.hip)
+constexpr int THREADS = 256;
+
+struct Args {
+  const void* x;  // [N, H, W] (Cin = 1), dtype dt
+  const void* w;  // packed [Cout][9], dtype dt
+  int N, H, W, C;
+  int RB;  // pooled rows per workgroup
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  uint32_t thr;
+  float dscale;
+  uint32_t key;
+  const unsigned long long* seedp;
+  unsigned long long seed;
+  uint32_t site;
+  __device__ __forceinline__ void resolve() {
+    if (seedp && thr) key = rng_key(seed ^ *seedp, site);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ float ldv(const void* p, long i) {
+  return Elem<T>::to_f(((const T*)p)[i]);
+}
+
+// rows [y_lo, y_lo + nrows) of sample n, each W + 2 floats with a zero column
+// on both sides; rows outside the image are zeros
+template <typename T>
+__device__ __forceinline__ void stage_rows(const Args& a, int n, int y_lo, int nrows, float* xs) {
+  const int pitch = a.W + 2;
+  const int tot = nrows * pitch;
+  for (int i = threadIdx.x; i < tot; i += THREADS) {
+    const int r = i / pitch, c = i - r * pitch;
+    const int y = y_lo + r, x = c - 1;
+    const bool ok = y >= 0 && y < a.H && x >= 0 && x < a.W;
+    const float v = ldv<T>(a.x, ok ? ((long)n * a.H + y) * a.W + x : 0);
+    xs[i] = ok ? v : 0.f;
+  }
+  __syncthreads();
+}
+
+// the (P+2)^2 input patch of the window whose top-left pixel is staged row r*P,
+// column ox*P (staged row 0 = image row oy0*P - 1, column 0 = x = -1)
+template <int P>
+__device__ __forceinline__ void load_patch(const float* xs, int pitch, int r, int ox, float (&pt)[P + 2][P + 2]) {
+  const float* b = xs + r * P * pitch + ox * P;
+#pragma unroll
+  for (int i = 0; i < P + 2; ++i)
+#pragma unroll
+    for (int j = 0; j < P + 2; ++j) pt[i][j] = b[i * pitch + j];
+}
+
+template <int P, int CV>
+__device__ __forceinline__ void conv_at(const float (&pt)[P + 2][P + 2], int qy, int qx, const float (&wr)[9][CV],
+                                        float* z) {
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s += pt[qy + k / 3][qx + k % 3] * wr[k][e];
+    z[e] = s;
+  }
+}
+
+template <typename T, int CV>
+__device__ __forceinline__ void load_w(const Args& a, int c, float (&wr)[9][CV]) {
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < CV; ++e) wr[t][e] = ldv<T>(a.w, (c + e) * 9 + t);
+}
+
+template <int CV>
+__device__ __forceinline__ void loadc(const float* p, int c, float* o) {
+#pragma unroll
+  for (int e = 0; e < CV; ++e) o[e] = p[c + e];
+}
+
+// relu(bn(z)) = max(z*sc + sh, 0); xhat = (z - mu)*is
+template <int CV>
+__device__ __forceinline__ void bn_consts(const Args& a, int c, float* sc, float* sh, float* mu, float* is) {
+  float ga[CV], be[CV];
+  loadc<CV>(a.mean, c, mu);
+  loadc<CV>(a.invstd, c, is);
+  loadc<CV>(a.gamma, c, ga);
+  loadc<CV>(a.beta, c, be);
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    sc[e] = is[e] * ga[e];
+    sh[e] = be[e] - mu[e] * sc[e];
+  }
+}
+
+// Dropout2d multipliers of channels c .. c+CV-1 of sample n (bnact.hip drop_mask)
+template <int CV>
+__device__ __forceinline__ void drop_cv(const Args& a, int n, int c, float* m) {
+#pragma unroll
+  for (int e = 0; e < CV; ++e) m[e] = 1.f;
+  if (!a.thr) return;
+  const uint64_t i0 = (uint64_t)n * a.C + c;
+#pragma unroll
+  for (int e4 = 0; e4 < CV; e4 += 4) {
+    const f32x4 k = keep4_at(a.key, i0 + e4, a.thr, a.dscale);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e4 + e] = k[e];
+  }
+}
+
+template <typename TO, int CV>
+__device__ __forceinline__ void store_cv(TO* p, const float* v) {
+  if constexpr (sizeof(TO) == 2) {
+    uint32_t u[CV / 2];
+#pragma unroll
+    for (int i = 0; i < CV / 2; ++i) u[i] = f2bf2(v[2 * i], v[2 * i + 1]);
+    if constexpr (CV == 8) *(u32x4*)p = (u32x4){u[0], u[1], u[2], u[3]};
+    else *(uint2*)p = make_uint2(u[0], u[1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < CV; i += 4) *(f32x4*)(p + i) = (f32x4){v[i], v[i + 1], v[i + 2], v[i + 3]};
+  }
+}
+template <typename TD, int CV>
+__device__ __forceinline__ void load_cv(const TD* p, float* v) {
+  if constexpr (sizeof(TD) == 2) {
+    uint32_t u[CV / 2];
+    if constexpr (CV == 8) {
+      const u32x4 q = *(const u32x4*)p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u[i] = q[i];
+    } else {
+      const uint2 q = *(const uint2*)p;
+      u[0] = q.x;
+      u[1] = q.y;
+    }
+#pragma unroll
+    for (int i = 0; i < CV / 2; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < CV; i += 4) {
+      const f32x4 q = *(const f32x4*)(p + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i + j] = q[j];
+    }
+  }
+}
+
+// forward apply: y[n, oy, ox, c..] = Dropout2d(max over the window of relu(bn(z)))
+template <typename T, typename TO, int P, int CV>
+__global__ __launch_bounds__(THREADS) void c1_apply_kernel(Args a_, TO* __restrict__ y) {
+  Args a = a_;
+  a.resolve();
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int Ho = a.H / P, Wo = a.W / P;
+  const int chunks = (Ho + a.RB - 1) / a.RB;
+  const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
+  const int pitch = a.W + 2;
+  stage_rows<T>(a, n, oy0 * P - 1, a.RB * P + 2, xs);
+  const int CC = a.C / CV, c = (threadIdx.x % CC) * CV, lanes = THREADS / CC;
+  float wr[9][CV], sc[CV], sh[CV], mu[CV], is[CV], m[CV];
+  load_w<T, CV>(a, c, wr);
+  bn_consts<CV>(a, c, sc, sh, mu, is);
+  drop_cv<CV>(a, n, c, m);
+  const int rows = min(a.RB, Ho - oy0);
+  for (int it = threadIdx.x / CC; it < rows * Wo; it += lanes) {
+    const int r = it / Wo, ox = it - r * Wo;
+    float pt[P + 2][P + 2];
+    load_patch<P>(xs, pitch, r, ox, pt);
+    float best[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) best[e] = 0.f;  // the relu floor
+#pragma unroll
+    for (int q = 0; q < P * P; ++q) {
+      float z[CV];
+      conv_at<P, CV>(pt, q / P, q % P, wr, z);
+#pragma unroll
+      for (int e = 0; e < CV; ++e) best[e] = fmaxf(best[e], __builtin_fmaf(z[e], sc[e], sh[e]));
+    }
+#pragma unroll
+    for (int e = 0; e < CV; ++e) best[e] *= m[e];
+    store_cv<TO, CV>(y + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c, best);
+  }
+}
+
+// routed gradient of one full window: the first maximum of relu(bn(z)) over the
+// window (torch's max-pool rule) gets g = dy * mask where the relu is open;
+// arg = its position, zs = its z
+template <int P, int CV>
+__device__ __forceinline__ void route(const float (&zq)[P * P][CV], const float* sc, const float* sh, const float* d,
+                                      const float* m, int* arg, float* g, float* zs) {
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    float best = fmaxf(__builtin_fmaf(zq[0][e], sc[e], sh[e]), 0.f);
+    float z = zq[0][e];
+    int ai = 0;
+#pragma unroll
+    for (int q = 1; q < P * P; ++q) {
+      const float v = fmaxf(__builtin_fmaf(zq[q][e], sc[e], sh[e]), 0.f);
+      const bool gt = v > best;
+      best = gt ? v : best;
+      z = gt ? zq[q][e] : z;
+      ai = gt ? q : ai;
+    }
+    arg[e] = ai;
+    g[e] = best > 0.f ? d[e] * m[e] : 0.f;
+    zs[e] = z;
+  }
+}
+
+// backward reduce pass: per-channel sum g (dbeta), sum g * xhat (dgamma) over the
+// full windows; workgroup partials spread over the BN_SLOTS slot copies of sums
+template <typename T, typename TD, int P, int CV>
+__global__ __launch_bounds__(THREADS) void c1_sums_kernel(Args a_, const TD* __restrict__ dy, float* __restrict__ sums) {
+  Args a = a_;
+  a.resolve();
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int Ho = a.H / P, Wo = a.W / P;
+  const int chunks = (Ho + a.RB - 1) / a.RB;
+  const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
+  const int pitch = a.W + 2;
+  const int nrows = a.RB * P + 2;
+  stage_rows<T>(a, n, oy0 * P - 1, nrows, xs);
+  float* red = xs + nrows * pitch;  // [4 waves][2][C]
+  const int CC = a.C / CV, c = (threadIdx.x % CC) * CV, lanes = THREADS / CC;
+  float wr[9][CV], sc[CV], sh[CV], mu[CV], is[CV], m[CV], acc1[CV], acc2[CV];
+  load_w<T, CV>(a, c, wr);
+  bn_consts<CV>(a, c, sc, sh, mu, is);
+  drop_cv<CV>(a, n, c, m);
+#pragma unroll
+  for (int e = 0; e < CV; ++e) acc1[e] = acc2[e] = 0.f;
+  const int rows = min(a.RB, Ho - oy0);
+  for (int it = threadIdx.x / CC; it < rows * Wo; it += lanes) {
+    const int r = it / Wo, ox = it - r * Wo;
+    float d[CV];
+    load_cv<TD, CV>(dy + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c, d);
+    float pt[P + 2][P + 2];
+    load_patch<P>(xs, pitch, r, ox, pt);
+    float zq[P * P][CV];
+#pragma unroll
+    for (int q = 0; q < P * P; ++q) conv_at<P, CV>(pt, q / P, q % P, wr, zq[q]);
+    int arg[CV];
+    float g[CV], zs[CV];
+    route<P, CV>(zq, sc, sh, d, m, arg, g, zs);
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      acc1[e] += g[e];
+      acc2[e] += g[e] * ((zs[e] - mu[e]) * is[e]);
+    }
+  }
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int e = 0; e < CV; ++e) {
+    float v1 = acc1[e], v2 = acc2[e];
+    for (int o = CC; o < 64; o <<= 1) {
+      v1 += __shfl_xor(v1, o, 64);
+      v2 += __shfl_xor(v2, o, 64);
+    }
+    if (ln < CC) {
+      red[(wv * 2) * a.C + c + e] = v1;
+      red[(wv * 2 + 1) * a.C + c + e] = v2;
+    }
+  }
+  __syncthreads();
+  float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+  for (int i = threadIdx.x; i < 2 * a.C; i += THREADS)
+    atomicAdd(slot + i, red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i]);
+}
+
+__global__ void slots_reduce_kernel(float* sums, int n2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n2) return;
+  float s = 0.f;
+  for (int k = 1; k <= BN_SLOTS; ++k) s += sums[(size_t)k * n2 + i];
+  sums[i] = s;
+}
+
+// backward apply + weight gradient: dz of every pixel (all windows, the
+// partial ones at odd edges included: training-mode BN gives them ca + cb z),
+// accumulated straight into dW[c][tap] += dz * x_tap; partials part[blk][C*9]
+template <typename T, typename TD, int P, int CV, int CC>
+__global__ __launch_bounds__(THREADS) void c1_bwd_kernel(Args a_, const TD* __restrict__ dy,
+                                                         const float* __restrict__ sums, int training,
+                                                         float* __restrict__ part) {
+  Args a = a_;
+  a.resolve();
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  constexpr int lanes = THREADS / CC;
+  const int Ho = a.H / P, Wo = a.W / P;
+  const int Hw = (a.H + P - 1) / P, Ww = (a.W + P - 1) / P;
+  const int chunks = (Hw + a.RB - 1) / a.RB;
+  const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
+  const int pitch = a.W + 2;
+  const int nrows = a.RB * P + 2;
+  stage_rows<T>(a, n, oy0 * P - 1, nrows, xs);
+  float* red = xs + nrows * pitch;  // [4 waves][C * 9]
+  const int c = (threadIdx.x % CC) * CV;
+  const float invM = 1.f / (float)((long)a.N * a.H * a.W);
+  float wr[9][CV], sc[CV], sh[CV], m[CV], ca[CV], cb[CV];
+  load_w<T, CV>(a, c, wr);
+  {
+    float mu[CV], is[CV], s1v[CV], s2v[CV];
+    bn_consts<CV>(a, c, sc, sh, mu, is);
+    loadc<CV>(sums, c, s1v);
+    loadc<CV>(sums + a.C, c, s2v);
+    // dz = sc*(g - s1 - xhat*s2) = sc*g + ca + cb*z  (bnact.hip's apply pass)
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      const float s1 = training ? s1v[e] * invM : 0.f, s2 = training ? s2v[e] * invM : 0.f;
+      cb[e] = -sc[e] * s2 * is[e];
+      ca[e] = -sc[e] * s1 - cb[e] * mu[e];
+    }
+  }
+  drop_cv<CV>(a, n, c, m);
+  float acc[9][CV];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < CV; ++e) acc[t][e] = 0.f;
+  const int rows = min(a.RB, Hw - oy0);
+  for (int it = threadIdx.x / CC; it < rows * Ww; it += lanes) {
+    const int r = it / Ww, ox = it - r * Ww;
+    const int oy = oy0 + r;
+    const bool full = oy < Ho && ox < Wo;
+    float d[CV];
+#pragma unroll
+    for (int e = 0; e < CV; ++e) d[e] = 0.f;
+    if (full) load_cv<TD, CV>(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c, d);
+    float pt[P + 2][P + 2];
+    load_patch<P>(xs, pitch, r, ox, pt);
+    float zq[P * P][CV];
+#pragma unroll
+    for (int q = 0; q < P * P; ++q) conv_at<P, CV>(pt, q / P, q % P, wr, zq[q]);
+    int arg[CV];
+    float g[CV], zs[CV];
+    route<P, CV>(zq, sc, sh, d, m, arg, g, zs);  // d = 0 outside full windows -> g = 0
+#pragma unroll
+    for (int q = 0; q < P * P; ++q) {
+      const int qy = q / P, qx = q % P;
+      // pixels past an odd edge belong to no window but still have a dz
+      const float inb = (oy * P + qy < a.H && ox * P + qx < a.W) ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < CV; ++e) {
+        const float gq = arg[e] == q ? g[e] : 0.f;
+        const float dz = inb * (training ? sc[e] * gq + ca[e] + cb[e] * zq[q][e] : sc[e] * gq);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t][e] += dz * pt[qy + t / 3][qx + t % 3];
+      }
+    }
+  }
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      float v = acc[t][e];
+#pragma unroll
+      for (int o = CC; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (ln < CC) red[wv * a.C * 9 + (c + e) * 9 + t] = v;
+    }
+  __syncthreads();
+  const int R = a.C * 9;
+  for (int i = threadIdx.x; i < R; i += THREADS)
+    part[(size_t)blockIdx.x * R + i] = red[i] + red[R + i] + red[2 * R + i] + red[3 * R + i];
+}
+
+// pooled rows per workgroup: the staged rows stay within 32 KiB of LDS
+inline int rows_per_block(int W, int P) {
+  const int maxrows = (32768 / 4) / (W + 2);
+  int rb = (maxrows - 2) / P;
+  return rb > 4 ? 4 : rb;
+}
+
+int make_args(Args& a, int dt, const hvit_conv_geom_t* g, const void* w, const float* mean, const float* invstd,
+              const float* gamma, const float* beta, const hvit_dropout_t* dr, int pool) {
+  HVIT_CHECK(g && g->src1 && w && mean && invstd && gamma && beta, "c1block: null pointer");
+  HVIT_CHECK(g->C1 == 1 && g->C2 == 0 && g->U == 1 && g->KS == 3 && g->stride == 1 && g->pad == 1,
+             "c1block: Cin = 1 3x3 same conv only");
+  HVIT_CHECK(g->Cout >= 8 && g->Cout <= 256 && (g->Cout & (g->Cout - 1)) == 0,
+             "c1block: Cout=%d must be a power of two in [8, 256]", g->Cout);
+  HVIT_CHECK(pool == 1 || pool == 2, "c1block: pool must be 1 or 2");
+  HVIT_CHECK(dt == HVIT_BF16 || dt == HVIT_F32, "c1block: bad dtype");
+  a.x = g->src1;
+  a.w = w;
+  a.N = g->N;
+  a.H = g->Hs;
+  a.W = g->Ws;
+  a.C = g->Cout;
+  a.RB = rows_per_block(g->Ws, pool);
+  HVIT_CHECK(a.RB >= 1, "c1block: W=%d too wide for the staged rows", g->Ws);
+  a.mean = mean;
+  a.invstd = invstd;
+  a.gamma = gamma;
+  a.beta = beta;
+  a.thr = dr ? drop_threshold(dr->p) : 0;
+  a.dscale = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
+  a.key = dr ? rng_key(dr->seed, dr->site) : 0u;
+  a.seedp = dr ? dr->seed_ptr : nullptr;
+  a.seed = dr ? dr->seed : 0ull;
+  a.site = dr ? dr->site : 0u;
+  return HVIT_OK;
+}
+
+// fn(std::integral_constant<int, P>) for the runtime pool size
+template <typename F>
+void with_pool(int pool, F&& fn) {
+  if (pool == 2) fn(std::integral_constant<int, 2>());
+  else fn(std::integral_constant<int, 1>());
+}
+
+}  // namespace hvit_c1
+
+using namespace hvit_c1;
+
+int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats,
+                     hipStream_t st);
+
+extern "C" int hvit_c1block_stats(int dt, const hvit_conv_geom_t* g, const void* w_packed, float* bn_partials,
+                                  void* stream) {
+  HVIT_CHECK(g && g->src1 && w_packed && bn_partials, "hvit_c1block_stats: null pointer");
+  HVIT_CHECK(g->C1 == 1 && g->C2 == 0 && g->U == 1 && g->KS == 3 && g->stride == 1 && g->pad == 1,
+             "hvit_c1block_stats: Cin = 1 3x3 same conv only");
+  return hvit_thin_c1_fwd(dt, g, w_packed, nullptr, dt, bn_partials, (hipStream_t)stream);
+}
+
+extern "C" int hvit_c1block_fwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* mean,
+                                const float* invstd, const float* gamma, const float* beta,
+                                const hvit_dropout_t* dropout2d, int pool, void* y, int y_dt, void* stream) {
+  Args a;
+  if (int rc = make_args(a, dt, g, w_packed, mean, invstd, gamma, beta, dropout2d, pool)) return rc;
+  HVIT_CHECK(y && aligned16(y), "hvit_c1block_fwd: y null or misaligned");
+  HVIT_CHECK(y_dt == HVIT_BF16 || y_dt == HVIT_F32, "hvit_c1block_fwd: bad y dtype");
+  const int Ho = a.H / pool;
+  if (Ho <= 0 || a.W / pool <= 0 || a.N <= 0) return HVIT_OK;
+  const int blocks = a.N * ((Ho + a.RB - 1) / a.RB);
+  const size_t lds = sizeof(float) * (a.RB * pool + 2) * (a.W + 2);
+  hipStream_t st = (hipStream_t)stream;
+  with_pool(pool, [&](auto pc) {
+    constexpr int P = decltype(pc)::value;
+    if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
+      hipLaunchKernelGGL((c1_apply_kernel<bf16_t, bf16_t, P, 8>), dim3(blocks), dim3(THREADS), lds, st, a,
+                         (bf16_t*)y);
+    else if (dt == HVIT_BF16)
+      hipLaunchKernelGGL((c1_apply_kernel<bf16_t, float, P, 8>), dim3(blocks), dim3(THREADS), lds, st, a, (float*)y);
+    else if (y_dt == HVIT_F32)
+      hipLaunchKernelGGL((c1_apply_kernel<float, float, P, 8>), dim3(blocks), dim3(THREADS), lds, st, a, (float*)y);
+    else
+      hipLaunchKernelGGL((c1_apply_kernel<float, bf16_t, P, 8>), dim3(blocks), dim3(THREADS), lds, st, a,
+                         (bf16_t*)y);
+  });
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" long long hvit_c1block_bwd_ws(const hvit_conv_geom_t* g, int pool) {
+  if (!g || (pool != 1 && pool != 2) || g->Ws <= 0 || g->N <= 0) return 0;
+  const int rb = rows_per_block(g->Ws, pool);
+  if (rb < 1) return 0;
+  const int Hw = (g->Hs + pool - 1) / pool;
+  return (long long)g->N * ((Hw + rb - 1) / rb) * g->Cout * 9;
+}
+
+int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream);
+
+extern "C" int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w_packed, const float* mean,
+                                const float* invstd, const float* gamma, const float* beta,
+                                const hvit_dropout_t* dropout2d, int pool, const void* dy, int dy_dt, int training,
+                                float* sums, int flags, float* dw_packed, float* ws, long long ws_elems,
+                                void* stream) {
+  Args a;
+  if (int rc = make_args(a, dt, g, w_packed, mean, invstd, gamma, beta, dropout2d, pool)) return rc;
+  HVIT_CHECK(dy && sums && dw_packed && ws, "hvit_c1block_bwd: null pointer");
+  HVIT_CHECK(dy_dt == HVIT_BF16 || dy_dt == HVIT_F32, "hvit_c1block_bwd: bad dy dtype");
+  HVIT_CHECK(aligned16(dy), "hvit_c1block_bwd: dy alignment");
+  HVIT_CHECK(ws_elems >= hvit_c1block_bwd_ws(g, pool), "hvit_c1block_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int C = a.C;
+  if (!(flags & HVIT_ACC_ZEROED)) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * (1 + BN_SLOTS), st);
+  if (a.N <= 0 || a.H <= 0 || a.W <= 0) {
+    (void)hipMemsetAsync(dw_packed, 0, sizeof(float) * C * 9, st);
+    return HVIT_OK;
+  }
+  const int Ho = a.H / pool;
+  const size_t lds_rows = sizeof(float) * (a.RB * pool + 2) * (a.W + 2);
+  constexpr int CV = 4;
+  if (Ho > 0 && a.W / pool > 0) {  // dbeta / dgamma in both modes; training-mode dz also uses them
+    const int blocks = a.N * ((Ho + a.RB - 1) / a.RB);
+    const size_t lds = lds_rows + sizeof(float) * 8 * C;
+    with_pool(pool, [&](auto pc) {
+      constexpr int P = decltype(pc)::value;
+      if (dt == HVIT_BF16 && dy_dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1_sums_kernel<bf16_t, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const bf16_t*)dy, sums);
+      else if (dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1_sums_kernel<bf16_t, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const float*)dy, sums);
+      else if (dy_dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1_sums_kernel<float, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const bf16_t*)dy, sums);
+      else
+        hipLaunchKernelGGL((c1_sums_kernel<float, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const float*)dy, sums);
+    });
+    HVIT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(slots_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, sums, 2 * C);
+    HVIT_LAUNCH_CHECK();
+  }
+  const int Hw = (a.H + pool - 1) / pool;
+  const int blocks = a.N * ((Hw + a.RB - 1) / a.RB);
+  const size_t lds = lds_rows + sizeof(float) * 4 * C * 9;
+  HVIT_CHECK(lds <= 64 * 1024, "hvit_c1block_bwd: LDS %zu too large", lds);
+  auto go = [&](auto ccc) {
+    constexpr int CC = decltype(ccc)::value;
+    with_pool(pool, [&](auto pc) {
+      constexpr int P = decltype(pc)::value;
+      if (dt == HVIT_BF16 && dy_dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1_bwd_kernel<bf16_t, bf16_t, P, CV, CC>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const bf16_t*)dy, sums, training, ws);
+      else if (dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1_bwd_kernel<bf16_t, float, P, CV, CC>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const float*)dy, sums, training, ws);
+      else if (dy_dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1_bwd_kernel<float, bf16_t, P, CV, CC>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const bf16_t*)dy, sums, training, ws);
+      else
+        hipLaunchKernelGGL((c1_bwd_kernel<float, float, P, CV, CC>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const float*)dy, sums, training, ws);
+    });
+  };
+  switch (C / CV) {
+    case 2: go(std::integral_constant<int, 2>()); break;
+    case 4: go(std::integral_constant<int, 4>()); break;
+    case 8: go(std::integral_constant<int, 8>()); break;
+    case 16: go(std::integral_constant<int, 16>()); break;
+    case 32: go(std::integral_constant<int, 32>()); break;
+    case 64: go(std::integral_constant<int, 64>()); break;
+    default: hvit_set_error("hvit_c1block_bwd: Cout=%d unsupported", C); return HVIT_ERR_ARG;
+  }
+  HVIT_LAUNCH_CHECK();
+  return hvit_sum_slabs(ws, blocks, (long long)C * 9, dw_packed, stream);
+}

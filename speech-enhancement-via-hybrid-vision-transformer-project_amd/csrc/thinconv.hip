@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void c1_fwd_kernel(const T* __restrict__ x, co
       for (int t = 0; t < 9; ++t) acc += xv[t] * wr[t][e];
       o[e] = acc;
     }
-    Vec8<TO>::store(z + (size_t)p * Cout + cc * 8, o);
+    if (z) Vec8<TO>::store(z + (size_t)p * Cout + cc * 8, o);  // null: statistics only (c1block.hip)
     cnt += 1.f;
     const float inv = __builtin_amdgcn_rcpf(cnt);
 #pragma unroll

@@ -10,6 +10,7 @@ LayerNorm statistics, BatchNorm statistics and all parameter gradients are f32.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -426,6 +427,90 @@ class ConvBNActFn(torch.autograd.Function):
                 call("hvit_upsample_split_bwd", du.data_ptr(), dt, N, Hs, Ws, U, C1, C2, dx1.data_ptr(), dt,
                      ptr(dx2), dt, s)
         return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 10
+
+
+C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path
+
+
+def c1block_ok(x1, x2, w, U, pool) -> bool:
+    """The fused first block (hvit_c1block_*) applies: a single-channel input that
+    needs no gradient, 3x3 same conv, power-of-two Cout <= 256, rows that fit
+    the kernel's LDS staging."""
+    if not C1BLOCK or x2 is not None or U != 1 or pool not in (1, 2) or x1.requires_grad:
+        return False
+    co, ci, ks, _ = w.shape
+    return ci == 1 and ks == 3 and 8 <= co <= 256 and co & (co - 1) == 0 and x1.shape[2] + 2 <= 8192 // (pool + 2)
+
+
+class C1BlockFn(torch.autograd.Function):
+    """The first encoder ConvBlock (hybrid_vit.py:196-208 -> components.py:55-85,
+    Cin = 1) fused so that the conv output z never reaches HBM: BatchNorm
+    statistics, the BN/ReLU/Dropout2d/MaxPool apply, and the backward
+    (BN backward + conv weight gradient, dz kept in registers) each recompute
+    z from the single-channel input (csrc/c1block.hip).  Same arguments and
+    result as ConvBNActFn for that block; the input gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, x1, w, gamma, beta, rmean, rvar, nbt, pool, training, drop: Drop, momentum, eps, dt):
+        N, H, W, _ = x1.shape
+        Cout = w.shape[0]
+        dev = x1.device
+        s = stream_ptr()
+        wp = pack_conv(w, 0, dt)
+        g = geom(x1, 1, None, 0, N, H, W, 1, 3, 1, 1, Cout)
+        mean = torch.empty(Cout, dtype=torch.float32, device=dev)
+        invstd = torch.empty_like(mean)
+        P = N * H * W
+        es = 4 if dt == F32 else 2
+        if training:
+            tr = L.lib().hvit_conv_bn_tile_rows(C.byref(g))
+            nt = (P + tr - 1) // tr
+            part = torch.empty((nt, Cout, 2), dtype=torch.float32, device=dev)
+            with timed("c1block_stats", float(P * x1.element_size())):  # reads x
+                call("hvit_c1block_stats", dt, g, wp.data_ptr(), part.data_ptr(), s)
+            call("hvit_bn_finalize", part.data_ptr(), nt, tr, P, Cout, mean.data_ptr(), invstd.data_ptr(),
+                 ptr(rmean), ptr(rvar), ptr(nbt), momentum, eps, s)
+        else:
+            call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
+                 invstd.data_ptr(), s)
+        y = _empty((N, H // pool, W // pool, Cout), dt, dev)
+        dr = drop.c() if training else L.dropout()
+        with timed("c1block_fwd", float(P * x1.element_size() + y.numel() * es)):  # read x, write y
+            call("hvit_c1block_fwd", dt, g, wp.data_ptr(), mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+                 beta.data_ptr(), dr, pool, y.data_ptr(), dt, s)
+        ctx.save_for_backward(x1, w, gamma, beta)
+        ctx.mean, ctx.invstd = mean, invstd
+        ctx.meta = (pool, training, dr, dt)
+        ctx.zs = _zs(ctx, L.lib().hvit_bn_act_bwd_sums_elems(Cout))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x1, w, gamma, beta = ctx.saved_tensors
+        pool, training, dr, dt = ctx.meta
+        N, H, W, _ = x1.shape
+        Cout = w.shape[0]
+        dev = x1.device
+        s = stream_ptr()
+        dy = dy.contiguous()
+        g = geom(x1, 1, None, 0, N, H, W, 1, 3, 1, 1, Cout)
+        wp = pack_conv(w, 0, dt)
+        sums = ctx.zs.take(dev)
+        dwp = torch.empty(w.numel(), dtype=torch.float32, device=dev)
+        ws_n = L.lib().hvit_c1block_bwd_ws(C.byref(g), pool)
+        ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
+        passes = 2
+
+        def launch():
+            call("hvit_c1block_bwd", dt, g, wp.data_ptr(), ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
+                 gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
+                 sums.data_ptr(), L.ACC_ZEROED, dwp.data_ptr(), ws.data_ptr(), ws_n, s)
+
+        with timed("c1block_bwd", float(passes * (dy.numel() * dy.element_size() + x1.numel() * x1.element_size()))):
+            launch()
+        dbeta, dgamma = sums[:Cout], sums[Cout:2 * Cout]
+        # mode-0 packing of a Cin = 1 weight is the torch layout [Cout][1][3][3]
+        return (None, dwp.view(w.shape), dgamma, dbeta) + (None,) * 9
 
 
 class PatchEmbedFn(torch.autograd.Function):

@@ -413,9 +413,14 @@ class HybridViT(nn.Module):
         h = xh
         for i, blk in enumerate(self.encoder):
             bn = blk.bn
-            h = HF.ConvBNActFn.apply(h, None, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                     bn.num_batches_tracked, 1, blk.pool, self.training,
-                                     HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt)
+            if HF.c1block_ok(h, None, blk.conv.weight, 1, blk.pool):
+                h = HF.C1BlockFn.apply(h, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                       bn.num_batches_tracked, blk.pool, self.training,
+                                       HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt)
+            else:
+                h = HF.ConvBNActFn.apply(h, None, blk.conv.weight, bn.weight, bn.bias, bn.running_mean,
+                                         bn.running_var, bn.num_batches_tracked, 1, blk.pool, self.training,
+                                         HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt)
             skips.append(h)
         return h, skips
 

@@ -7,6 +7,7 @@
 #   eager             bench.py --graph 0 --no-cpu-baseline
 #   prof              rocprofv3 kernel stats of a short bench
 #   gemm              tools/gemm_bench.py
+#   env:VAR=VAL,...   benchq under extra environment variables (A/B knobs)
 cd "$(dirname "$0")/.."
 TAG=${1:-run}; shift
 mkdir -p gpurun_out
@@ -27,6 +28,10 @@ for s in "$@"; do
     benchq) timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/${TAG}_benchq.log 2>&1 || exit $? ;;
     eager) timeout -k 10 400 python -u bench.py --graph 0 --no-cpu-baseline > gpurun_out/${TAG}_eager.log 2>&1 || exit $? ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
+    env:*)  # env:VAR=VAL[,VAR=VAL]: bench.py --no-cpu-baseline under those variables
+      kv=${s#env:}; tagv=$(echo "$kv" | tr ',=' '__')
+      env $(echo "$kv" | tr ',' ' ') timeout -k 10 400 python -u bench.py --no-cpu-baseline \
+        > gpurun_out/${TAG}_env_${tagv}.log 2>&1 || exit $? ;;
     gemm) timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/${TAG}_gemm.log 2>&1 || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
