@@ -102,9 +102,10 @@ long long hvit_wgrad_workspace(int M, int N, int K);                            
 long long hvit_wgrad_tickets(int M, int N, int K);
 int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db, float* ws,
                          long long ws_elems, unsigned* tickets, long long tickets_elems, int flags, void* stream);
-/* Tuning knob (A/B measurements): what 0 = GEMM pipeline of the bf16 linears
- * (0: two-stage kernels; 1-4: LDS-ring configurations, gemm_ring.h).  Returns
- * the previous value (-1 for an unknown knob). */
+/* Tuning knobs (A/B measurements, tests): what 0 = GEMM pipeline of the bf16
+ * linears (-1 automatic, 0: two-stage kernels; 1-5: LDS-ring configurations,
+ * gemm_ring.h); what 1 = the fused first block's matrix-core kernels (1 on, 0:
+ * the VALU kernels).  Returns the previous value (-1 for an unknown knob). */
 int hvit_gemm_tune(int what, int value);
 int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                       float* ws, long long ws_elems, void* stream);  /* dw[N,K] = dy^T x; db[N] = colsum(dy)

@@ -18,6 +18,8 @@
 // counter hash of (sample, channel) and the max-pool routing is its
 // first-maximum rule, so the fused and unfused paths implement the same
 // function (z is kept in f32 here instead of being rounded to bf16 in HBM).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -52,18 +54,28 @@ __device__ __forceinline__ float ldv(const void* p, long i) {
   return Elem<T>::to_f(((const T*)p)[i]);
 }
 
-// rows [y_lo, y_lo + nrows) of sample n, each W + 2 floats with a zero column
-// on both sides; rows outside the image are zeros
+// rows [y_lo, y_lo + nrows) of sample n, `pitch` floats each: column c holds
+// x = c - 1 (zero outside [0, W)); rows outside the image are zeros.  Loads go
+// out in batches of UB per thread (one load -> store chain per element would
+// serialise the staging on memory latency).
 template <typename T>
-__device__ __forceinline__ void stage_rows(const Args& a, int n, int y_lo, int nrows, float* xs) {
-  const int pitch = a.W + 2;
+__device__ __forceinline__ void stage_rows(const Args& a, int n, int y_lo, int nrows, int pitch, float* xs) {
   const int tot = nrows * pitch;
-  for (int i = threadIdx.x; i < tot; i += THREADS) {
-    const int r = i / pitch, c = i - r * pitch;
-    const int y = y_lo + r, x = c - 1;
-    const bool ok = y >= 0 && y < a.H && x >= 0 && x < a.W;
-    const float v = ldv<T>(a.x, ok ? ((long)n * a.H + y) * a.W + x : 0);
-    xs[i] = ok ? v : 0.f;
+  constexpr int UB = 8;
+  for (int i0 = threadIdx.x; i0 < tot; i0 += THREADS * UB) {
+    float v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int i = i0 + u * THREADS;
+      const int r = i / pitch, c = i - r * pitch;
+      const int y = y_lo + r, x = c - 1;
+      const bool ok = i < tot && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      const float e = ldv<T>(a.x, ok ? ((long)n * a.H + y) * a.W + x : 0);
+      v[u] = ok ? e : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+      if (i0 + u * THREADS < tot) xs[i0 + u * THREADS] = v[u];
   }
   __syncthreads();
 }
@@ -186,7 +198,7 @@ __global__ __launch_bounds__(THREADS) void c1_apply_kernel(Args a_, TO* __restri
   const int chunks = (Ho + a.RB - 1) / a.RB;
   const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
   const int pitch = a.W + 2;
-  stage_rows<T>(a, n, oy0 * P - 1, a.RB * P + 2, xs);
+  stage_rows<T>(a, n, oy0 * P - 1, a.RB * P + 2, pitch, xs);
   const int CC = a.C / CV, c = (threadIdx.x % CC) * CV, lanes = THREADS / CC;
   float wr[9][CV], sc[CV], sh[CV], mu[CV], is[CV], m[CV];
   load_w<T, CV>(a, c, wr);
@@ -250,7 +262,7 @@ __global__ __launch_bounds__(THREADS) void c1_sums_kernel(Args a_, const TD* __r
   const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
   const int pitch = a.W + 2;
   const int nrows = a.RB * P + 2;
-  stage_rows<T>(a, n, oy0 * P - 1, nrows, xs);
+  stage_rows<T>(a, n, oy0 * P - 1, nrows, pitch, xs);
   float* red = xs + nrows * pitch;  // [4 waves][2][C]
   const int CC = a.C / CV, c = (threadIdx.x % CC) * CV, lanes = THREADS / CC;
   float wr[9][CV], sc[CV], sh[CV], mu[CV], is[CV], m[CV], acc1[CV], acc2[CV];
@@ -322,7 +334,7 @@ __global__ __launch_bounds__(THREADS) void c1_bwd_kernel(Args a_, const TD* __re
   const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
   const int pitch = a.W + 2;
   const int nrows = a.RB * P + 2;
-  stage_rows<T>(a, n, oy0 * P - 1, nrows, xs);
+  stage_rows<T>(a, n, oy0 * P - 1, nrows, pitch, xs);
   float* red = xs + nrows * pitch;  // [4 waves][C * 9]
   const int c = (threadIdx.x % CC) * CV;
   const float invM = 1.f / (float)((long)a.N * a.H * a.W);
@@ -394,11 +406,480 @@ __global__ __launch_bounds__(THREADS) void c1_bwd_kernel(Args a_, const TD* __re
     part[(size_t)blockIdx.x * R + i] = red[i] + red[R + i] + red[2 * R + i] + red[3 * R + i];
 }
 
-// pooled rows per workgroup: the staged rows stay within 32 KiB of LDS
+// ============================================================================
+// bf16 throughput path on the matrix cores (pool 2, Cout in {16, 32, 64}).
+//
+// The VALU kernels above spend 9 FMAs per output recomputing z and are
+// VALU-bound (60-105 us per pass at B=32).  Here z comes from one
+// v_mfma_f32_16x16x32_bf16 per 16 pixels x 16 channels: A = the 16 pixels' 9
+// taps (k 0..8, the other 23 k zero), B = the weights [tap][channel].  Rows are
+// ordered window-major -- row 4*wi + q is position q = 2*qy + qx of window wi
+// -- so the accumulator layout (lane l: rows 4*(l>>4) + j, column l & 15) puts
+// one whole pooling window of one channel in each lane's 4 registers: max-pool
+// routing, BatchNorm and ReLU need no lane exchange.  Column n of channel block
+// cb is channel NCB*n + cb, so a lane's NCB channels are contiguous in NHWC
+// (one 8-byte store of 4 bf16 for Cout = 64).
+//
+// The weight gradient dW[tap][c] = sum_px x_tap[px] dz[px][c] is a second
+// MFMA with K = pixels: a lane's dz registers of two 16-pixel groups ARE its
+// B fragment (k = 8*(l>>4) + j <-> group j>>2, row 4*(l>>4) + (j&3): any k
+// order works for a sum, as long as A uses the same), and A = the taps of those
+// pixels read from LDS.  dz enters as bf16 hi + lo (two MFMAs), so the product
+// keeps ~16 mantissa bits of dz; x is exact in bf16.
+// BatchNorm statistics: per lane sums (sum z, sum z^2) over its <= 64 values of
+// a 1024-pixel tile, turned into (mean, M2) and merged with Chan's formula, in
+// the tile layout of hvit_conv_bn_tile_rows (thinconv.hip c1_fwd).
+constexpr int STATS_TILE = 1024;  // == hvit_thin_c1_bn_tile_rows()
+
+__device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, a), __builtin_bit_cast(s16x8, b), c, 0,
+                                                 0, 0);
+}
+
+// A fragment of a 16 x 32 tap matrix: lane l holds row l & 15, k = 8*(l>>4)+j;
+// taps 0..7 on lanes 0-15, tap 8 on lanes 16-31 (j = 0), zeros elsewhere
+__device__ __forceinline__ u32x4 tap_frag(const float* t, int l) {
+  const u32x4 lo = {f2bf2(t[0], t[1]), f2bf2(t[2], t[3]), f2bf2(t[4], t[5]), f2bf2(t[6], t[7])};
+  const u32x4 hi = {f2bf2(t[8], 0.f), 0u, 0u, 0u};
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  return l < 16 ? lo : (l < 32 ? hi : zero);
+}
+
+// B fragments of the weights: channel block cb, column n = l & 15 -> channel NCB*n + cb
+template <int NCB>
+__device__ __forceinline__ void weight_frags(const bf16_t* w, int l, u32x4 (&bw)[NCB]) {
+  const int n = l & 15;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const bf16_t* wc = w + (NCB * n + cb) * 9;
+    float t[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) t[k] = bf2f(wc[k]);
+    bw[cb] = tap_frag(t, l);
+  }
+}
+
+// per-lane channel constants of channels c0 .. c0+NCB-1
+template <int NCB>
+struct ChanConsts {
+  float sc[NCB], sh[NCB], mu[NCB], is[NCB], m[NCB];
+  __device__ __forceinline__ void load(const Args& a, int n, int c0) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      const int c = c0 + cb;
+      mu[cb] = a.mean[c];
+      is[cb] = a.invstd[c];
+      sc[cb] = is[cb] * a.gamma[c];
+      sh[cb] = a.beta[c] - mu[cb] * sc[cb];
+      m[cb] = a.thr ? (rng_u16k(a.key, (uint64_t)n * a.C + c) >= a.thr ? a.dscale : 0.f) : 1.f;
+    }
+  }
+};
+
+template <typename TD, int NCB>
+__device__ __forceinline__ void load_ncb(const TD* p, float* v) {
+  if constexpr (sizeof(TD) == 2) {
+    if constexpr (NCB == 4) {
+      const uint2 q = *(const uint2*)p;
+      v[0] = __uint_as_float(q.x << 16);
+      v[1] = __uint_as_float(q.x & 0xffff0000u);
+      v[2] = __uint_as_float(q.y << 16);
+      v[3] = __uint_as_float(q.y & 0xffff0000u);
+    } else if constexpr (NCB == 2) {
+      const uint32_t q = *(const uint32_t*)p;
+      v[0] = __uint_as_float(q << 16);
+      v[1] = __uint_as_float(q & 0xffff0000u);
+    } else {
+      v[0] = bf2f(p[0]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < NCB; ++e) v[e] = p[e];
+  }
+}
+template <typename TO, int NCB>
+__device__ __forceinline__ void store_ncb(TO* p, const float* v) {
+  if constexpr (sizeof(TO) == 2) {
+    if constexpr (NCB == 4) *(uint2*)p = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+    else if constexpr (NCB == 2) *(uint32_t*)p = f2bf2(v[0], v[1]);
+    else p[0] = f2bf(v[0]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < NCB; ++e) p[e] = v[e];
+  }
+}
+
+// z of the 16 rows of window group g (windows 4g .. 4g+3 of the block, row-major
+// over rows x ww windows per row), one accumulator per channel block.  Windows
+// past nwin are clamped (their results are discarded by the caller).
+template <int NCB>
+__device__ __forceinline__ void group_z(const float* xs, int pitch, int g, int nwin, int ww, int l,
+                                        const u32x4 (&bw)[NCB], f32x4 (&z)[NCB]) {
+  const int row = l & 15;
+  const int it = min(4 * g + (row >> 2), nwin - 1);
+  const int r = it / ww, ox = it - r * ww;
+  const float* b = xs + (r * 2 + ((row & 3) >> 1)) * pitch + ox * 2 + (row & 1);
+  float t[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) t[k] = b[(k / 3) * pitch + k % 3];
+  const u32x4 af = tap_frag(t, l);
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) z[cb] = mfma16(af, bw[cb], (f32x4){0.f, 0.f, 0.f, 0.f});
+}
+
+// first-maximum routing of one window (4 positions in registers): arg, relu'd
+// maximum, z at the maximum
+__device__ __forceinline__ void route4(const f32x4& z, float sc, float sh, int& arg, float& best, float& zs) {
+  best = fmaxf(__builtin_fmaf(z[0], sc, sh), 0.f);
+  zs = z[0];
+  arg = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    const float v = fmaxf(__builtin_fmaf(z[q], sc, sh), 0.f);
+    const bool gt = v > best;
+    best = gt ? v : best;
+    zs = gt ? z[q] : zs;
+    arg = gt ? q : arg;
+  }
+}
+
+template <typename TO, int NCB>
+__global__ __launch_bounds__(THREADS) void c1m_apply_kernel(Args a_, TO* __restrict__ y) {
+  Args a = a_;
+  a.resolve();
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int chunks = (Ho + a.RB - 1) / a.RB;
+  const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
+  const int pitch = a.W + 4;
+  stage_rows<bf16_t>(a, n, oy0 * 2 - 1, a.RB * 2 + 2, pitch, xs);
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = NCB * (l & 15);
+  u32x4 bw[NCB];
+  weight_frags<NCB>((const bf16_t*)a.w, l, bw);
+  ChanConsts<NCB> k;
+  k.load(a, n, c0);
+  const int nwin = min(a.RB, Ho - oy0) * Wo;
+  for (int g = wv; 4 * g < nwin; g += THREADS / 64) {
+    f32x4 z[NCB];
+    group_z<NCB>(xs, pitch, g, nwin, Wo, l, bw, z);
+    const int it = 4 * g + (l >> 4);
+    if (it < nwin) {
+      const int r = it / Wo, ox = it - r * Wo;
+      float o[NCB];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        float best = 0.f;  // the relu floor
+#pragma unroll
+        for (int q = 0; q < 4; ++q) best = fmaxf(best, __builtin_fmaf(z[cb][q], k.sc[cb], k.sh[cb]));
+        o[cb] = best * k.m[cb];
+      }
+      store_ncb<TO, NCB>(y + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c0, o);
+    }
+  }
+}
+
+template <typename TD, int NCB>
+__global__ __launch_bounds__(THREADS) void c1m_sums_kernel(Args a_, const TD* __restrict__ dy,
+                                                           float* __restrict__ sums) {
+  Args a = a_;
+  a.resolve();
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int chunks = (Ho + a.RB - 1) / a.RB;
+  const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
+  const int pitch = a.W + 4;
+  const int nrows = a.RB * 2 + 2;
+  stage_rows<bf16_t>(a, n, oy0 * 2 - 1, nrows, pitch, xs);
+  float* red = xs + nrows * pitch;  // [4 waves][2][C]
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = NCB * (l & 15);
+  u32x4 bw[NCB];
+  weight_frags<NCB>((const bf16_t*)a.w, l, bw);
+  ChanConsts<NCB> k;
+  k.load(a, n, c0);
+  float s1[NCB], s2[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) s1[cb] = s2[cb] = 0.f;
+  const int nwin = min(a.RB, Ho - oy0) * Wo;
+  for (int g = wv; 4 * g < nwin; g += THREADS / 64) {
+    f32x4 z[NCB];
+    group_z<NCB>(xs, pitch, g, nwin, Wo, l, bw, z);
+    const int it = 4 * g + (l >> 4);
+    if (it < nwin) {
+      const int r = it / Wo, ox = it - r * Wo;
+      float d[NCB];
+      load_ncb<TD, NCB>(dy + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c0, d);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        int arg;
+        float best, zs;
+        route4(z[cb], k.sc[cb], k.sh[cb], arg, best, zs);
+        const float gv = best > 0.f ? d[cb] * k.m[cb] : 0.f;
+        s1[cb] += gv;
+        s2[cb] += gv * ((zs - k.mu[cb]) * k.is[cb]);
+      }
+    }
+  }
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      s1[cb] += __shfl_xor(s1[cb], o, 64);
+      s2[cb] += __shfl_xor(s2[cb], o, 64);
+    }
+    if (l < 16) {
+      red[(wv * 2) * a.C + c0 + cb] = s1[cb];
+      red[(wv * 2 + 1) * a.C + c0 + cb] = s2[cb];
+    }
+  }
+  __syncthreads();
+  float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+  for (int i = threadIdx.x; i < 2 * a.C; i += THREADS)
+    atomicAdd(slot + i, red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i]);
+}
+
+template <typename TD, int NCB>
+__global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __restrict__ dy,
+                                                          const float* __restrict__ sums, int training,
+                                                          float* __restrict__ part) {
+  Args a = a_;
+  a.resolve();
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int Hw = (a.H + 1) / 2, Ww = (a.W + 1) / 2;
+  const int chunks = (Hw + a.RB - 1) / a.RB;
+  const int n = blockIdx.x / chunks, oy0 = (blockIdx.x - n * chunks) * a.RB;
+  const int pitch = a.W + 4;
+  const int nrows = a.RB * 2 + 2;
+  stage_rows<bf16_t>(a, n, oy0 * 2 - 1, nrows, pitch, xs);
+  float* red = xs + nrows * pitch;  // [4 waves][C * 9]
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = NCB * (l & 15);
+  u32x4 bw[NCB];
+  weight_frags<NCB>((const bf16_t*)a.w, l, bw);
+  ChanConsts<NCB> k;
+  k.load(a, n, c0);
+  // dz = sc*g + ca + cb*z  (training), sc*g (eval): bnact.hip's apply pass
+  float ca[NCB], cbz[NCB];
+  const float invM = 1.f / (float)((long)a.N * a.H * a.W);
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const float s1 = training ? sums[c0 + cb] * invM : 0.f, s2 = training ? sums[a.C + c0 + cb] * invM : 0.f;
+    cbz[cb] = -k.sc[cb] * s2 * k.is[cb];
+    ca[cb] = -k.sc[cb] * s1 - cbz[cb] * k.mu[cb];
+  }
+  f32x4 acc[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // wgrad A fragment: lane l holds tap m = l & 15 (0 past tap 8) of the pixels
+  // k = 8*(l>>4) + j -> group j>>2, window l>>4, position j&3
+  const int m = l & 15;
+  const int mo = m < 9 ? (m / 3) * pitch + m % 3 : 0;
+  const int nwin = min(a.RB, Hw - oy0) * Ww;
+  for (int g0 = 2 * wv; 4 * g0 < nwin; g0 += 2 * (THREADS / 64)) {
+    u32x4 bhi[NCB], blo[NCB];
+    float xa[8];
+#pragma unroll
+    for (int gs = 0; gs < 2; ++gs) {
+      const int g = g0 + gs;
+      f32x4 z[NCB];
+      group_z<NCB>(xs, pitch, g, nwin, Ww, l, bw, z);
+      const int it = 4 * g + (l >> 4);
+      const bool valid = it < nwin;
+      const int itc = min(it, nwin - 1);
+      const int r = itc / Ww, ox = itc - r * Ww;
+      const int oy = oy0 + r;
+      const bool full = valid && oy < Ho && ox < Wo;
+      float d[NCB];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) d[cb] = 0.f;
+      if (full) load_ncb<TD, NCB>(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c0, d);
+      // the lane's 4 pixels: inside the image and inside the block's windows?
+      float inb[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) inb[q] = (valid && oy * 2 + (q >> 1) < a.H && ox * 2 + (q & 1) < a.W) ? 1.f : 0.f;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        int arg;
+        float best, zs;
+        route4(z[cb], k.sc[cb], k.sh[cb], arg, best, zs);
+        const float gv = best > 0.f ? d[cb] * k.m[cb] : 0.f;
+        float dz[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float gq = arg == q ? gv : 0.f;
+          dz[q] = inb[q] * (training ? k.sc[cb] * gq + ca[cb] + cbz[cb] * z[cb][q] : k.sc[cb] * gq);
+        }
+        float lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lo[q] = dz[q] - bf2f(f2bf(dz[q]));
+        bhi[cb][2 * gs] = f2bf2(dz[0], dz[1]);
+        bhi[cb][2 * gs + 1] = f2bf2(dz[2], dz[3]);
+        blo[cb][2 * gs] = f2bf2(lo[0], lo[1]);
+        blo[cb][2 * gs + 1] = f2bf2(lo[2], lo[3]);
+      }
+      // taps of this lane's wgrad pixels in group gs: window (l >> 4) of the
+      // group as above, positions q = 0..3 (k = 8*(l>>4) + 4*gs + q)
+      const float* b = xs + (r * 2) * pitch + ox * 2 + mo;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xa[4 * gs + q] = m < 9 ? b[(q >> 1) * pitch + (q & 1)] : 0.f;
+    }
+    // dz of invalid / outside pixels is 0, so their (clamped) taps add nothing
+    const u32x4 aw = {f2bf2(xa[0], xa[1]), f2bf2(xa[2], xa[3]), f2bf2(xa[4], xa[5]), f2bf2(xa[6], xa[7])};
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      acc[cb] = mfma16(aw, bhi[cb], acc[cb]);
+      acc[cb] = mfma16(aw, blo[cb], acc[cb]);
+    }
+  }
+  // acc[cb]: lane l holds taps 4*(l>>4) + j of channel NCB*(l&15) + cb
+  const int R = a.C * 9;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tap = 4 * (l >> 4) + j;
+      if (tap < 9) red[wv * R + (c0 + cb) * 9 + tap] = acc[cb][j];
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < R; i += THREADS)
+    part[(size_t)blockIdx.x * R + i] = red[i] + red[R + i] + red[2 * R + i] + red[3 * R + i];
+}
+
+// BatchNorm (mean, M2) partials of z over 1024-pixel raster tiles (the layout
+// hvit_bn_finalize reads with tile_rows = STATS_TILE).  Rows of a 16-pixel group
+// are consecutive raster pixels; taps are read from the tile's staged strip
+// (pixels [p0 - W - 1, pend + W + 1)) with the image-boundary tests.
+template <int NCB>
+__global__ __launch_bounds__(THREADS) void c1m_stats_kernel(const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ w, float* __restrict__ stats,
+                                                            int N, int H, int W, int C) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  __shared__ float red[4][3][64];
+  const int P = N * H * W;
+  const int p0 = blockIdx.x * STATS_TILE, pend = min(P, p0 + STATS_TILE);
+  const long base = (long)p0 - W - 1;
+  const int ns = (pend - p0) + 2 * W + 2;
+  {
+    constexpr int UB = 8;
+    for (int i0 = threadIdx.x; i0 < ns; i0 += THREADS * UB) {
+      float v[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int i = i0 + u * THREADS;
+        const long q = base + i;
+        const bool ok = i < ns && q >= 0 && q < P;
+        const float e = bf2f(x[ok ? q : 0]);
+        v[u] = ok ? e : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+        if (i0 + u * THREADS < ns) xs[i0 + u * THREADS] = v[u];
+    }
+    __syncthreads();
+  }
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = NCB * (l & 15);
+  u32x4 bw[NCB];
+  weight_frags<NCB>(w, l, bw);
+  float s1[NCB], s2[NCB], cnt = 0.f;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) s1[cb] = s2[cb] = 0.f;
+  const int HW = H * W;
+  for (int g = wv; 16 * g < pend - p0; g += THREADS / 64) {
+    const int p = min(p0 + 16 * g + (l & 15), pend - 1);
+    const int rem = p % HW, yy = rem / W, xx = rem - yy * W;
+    const bool up = yy > 0, dn = yy + 1 < H, lf = xx > 0, rt = xx + 1 < W;
+    const float* c = xs + (p - base);
+    float t[9];
+    t[0] = (up && lf) ? c[-W - 1] : 0.f;
+    t[1] = up ? c[-W] : 0.f;
+    t[2] = (up && rt) ? c[-W + 1] : 0.f;
+    t[3] = lf ? c[-1] : 0.f;
+    t[4] = c[0];
+    t[5] = rt ? c[1] : 0.f;
+    t[6] = (dn && lf) ? c[W - 1] : 0.f;
+    t[7] = dn ? c[W] : 0.f;
+    t[8] = (dn && rt) ? c[W + 1] : 0.f;
+    const u32x4 af = tap_frag(t, l);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      const f32x4 z = mfma16(af, bw[cb], (f32x4){0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = (p0 + 16 * g + 4 * (l >> 4) + j < pend) ? z[j] : 0.f;
+        s1[cb] += v;
+        s2[cb] += v * v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cnt += (p0 + 16 * g + 4 * (l >> 4) + j < pend) ? 1.f : 0.f;
+  }
+  // per lane (n, mean, M2), then Chan merges: lanes l, l^16, l^32, l^48 share channels
+  float mu[NCB], m2[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    mu[cb] = cnt > 0.f ? s1[cb] / cnt : 0.f;
+    m2[cb] = cnt > 0.f ? fmaxf(s2[cb] - s1[cb] * mu[cb], 0.f) : 0.f;
+  }
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    const float nb = __shfl_xor(cnt, o, 64), nt = cnt + nb;
+    const float fb = nt > 0.f ? nb / nt : 0.f;
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      const float mb = __shfl_xor(mu[cb], o, 64), qb = __shfl_xor(m2[cb], o, 64);
+      const float d = mb - mu[cb];
+      m2[cb] += qb + d * d * cnt * fb;
+      mu[cb] += d * fb;
+    }
+    cnt = nt;
+  }
+  if (l < 16) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      red[wv][0][c0 + cb] = cnt;
+      red[wv][1][c0 + cb] = mu[cb];
+      red[wv][2][c0 + cb] = m2[cb];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    float na = 0.f, ma = 0.f, qa = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float nb = red[v][0][c];
+      if (nb <= 0.f) continue;
+      const float nt = na + nb, d = red[v][1][c] - ma;
+      qa += red[v][2][c] + d * d * na * nb / nt;
+      ma += d * nb / nt;
+      na = nt;
+    }
+    stats[((size_t)blockIdx.x * C + c) * 2] = ma;
+    stats[((size_t)blockIdx.x * C + c) * 2 + 1] = qa;
+  }
+}
+
+// pooled rows per workgroup: the staged rows (pitch W + 4) stay within 32 KiB of LDS
 inline int rows_per_block(int W, int P) {
-  const int maxrows = (32768 / 4) / (W + 2);
+  const int maxrows = (32768 / 4) / (W + 4);
   int rb = (maxrows - 2) / P;
   return rb > 4 ? 4 : rb;
+}
+
+// the matrix-core kernels apply (bf16 operands, pool 2, 16 <= Cout <= 64);
+// HVIT_C1MFMA=0 or hvit_gemm_tune(1, 0) forces the VALU kernels (A/B, tests)
+inline int& mfma_knob() {
+  static int knob = [] {
+    const char* e = getenv("HVIT_C1MFMA");
+    return e ? atoi(e) : 1;
+  }();
+  return knob;
+}
+inline bool use_mfma(int dt, int pool, int C) {
+  return mfma_knob() != 0 && dt == HVIT_BF16 && pool == 2 && (C == 16 || C == 32 || C == 64);
 }
 
 int make_args(Args& a, int dt, const hvit_conv_geom_t* g, const void* w, const float* mean, const float* invstd,
@@ -438,18 +919,49 @@ void with_pool(int pool, F&& fn) {
   else fn(std::integral_constant<int, 1>());
 }
 
+// fn(std::integral_constant<int, NCB>) for Cout = 16 * NCB
+template <typename F>
+void with_ncb(int C, F&& fn) {
+  if (C == 64) fn(std::integral_constant<int, 4>());
+  else if (C == 32) fn(std::integral_constant<int, 2>());
+  else fn(std::integral_constant<int, 1>());
+}
+
 }  // namespace hvit_c1
 
 using namespace hvit_c1;
 
+int hvit_c1_tune(int value) {
+  const int old = mfma_knob();
+  mfma_knob() = value;
+  return old;
+}
+
 int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats,
                      hipStream_t st);
+int hvit_thin_c1_bn_tile_rows();
 
 extern "C" int hvit_c1block_stats(int dt, const hvit_conv_geom_t* g, const void* w_packed, float* bn_partials,
                                   void* stream) {
   HVIT_CHECK(g && g->src1 && w_packed && bn_partials, "hvit_c1block_stats: null pointer");
   HVIT_CHECK(g->C1 == 1 && g->C2 == 0 && g->U == 1 && g->KS == 3 && g->stride == 1 && g->pad == 1,
              "hvit_c1block_stats: Cin = 1 3x3 same conv only");
+  const int C = g->Cout;
+  const size_t lds = sizeof(float) * (STATS_TILE + 2 * (size_t)g->Ws + 2);
+  if (use_mfma(dt, 2, C) && lds <= 48 * 1024) {
+    HVIT_CHECK(hvit_thin_c1_bn_tile_rows() == STATS_TILE, "hvit_c1block_stats: tile size mismatch");
+    const long P = (long)g->N * g->Hs * g->Ws;
+    HVIT_CHECK(P < (1L << 31), "hvit_c1block_stats: too many pixels");
+    if (P <= 0) return HVIT_OK;
+    with_ncb(C, [&](auto nc) {
+      constexpr int NCB = decltype(nc)::value;
+      hipLaunchKernelGGL((c1m_stats_kernel<NCB>), dim3(cdiv(P, STATS_TILE)), dim3(THREADS), lds,
+                         (hipStream_t)stream, (const bf16_t*)g->src1, (const bf16_t*)w_packed, bn_partials, g->N,
+                         g->Hs, g->Ws, C);
+    });
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   return hvit_thin_c1_fwd(dt, g, w_packed, nullptr, dt, bn_partials, (hipStream_t)stream);
 }
 
@@ -463,8 +975,20 @@ extern "C" int hvit_c1block_fwd(int dt, const hvit_conv_geom_t* g, const void* w
   const int Ho = a.H / pool;
   if (Ho <= 0 || a.W / pool <= 0 || a.N <= 0) return HVIT_OK;
   const int blocks = a.N * ((Ho + a.RB - 1) / a.RB);
-  const size_t lds = sizeof(float) * (a.RB * pool + 2) * (a.W + 2);
   hipStream_t st = (hipStream_t)stream;
+  if (use_mfma(dt, pool, a.C)) {
+    const size_t lds = sizeof(float) * (a.RB * 2 + 2) * (a.W + 4);
+    with_ncb(a.C, [&](auto nc) {
+      constexpr int NCB = decltype(nc)::value;
+      if (y_dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1m_apply_kernel<bf16_t, NCB>), dim3(blocks), dim3(THREADS), lds, st, a, (bf16_t*)y);
+      else
+        hipLaunchKernelGGL((c1m_apply_kernel<float, NCB>), dim3(blocks), dim3(THREADS), lds, st, a, (float*)y);
+    });
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
+  const size_t lds = sizeof(float) * (a.RB * pool + 2) * (a.W + 2);
   with_pool(pool, [&](auto pc) {
     constexpr int P = decltype(pc)::value;
     if (dt == HVIT_BF16 && y_dt == HVIT_BF16)
@@ -510,27 +1034,40 @@ extern "C" int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w
     (void)hipMemsetAsync(dw_packed, 0, sizeof(float) * C * 9, st);
     return HVIT_OK;
   }
+  const bool mf = use_mfma(dt, pool, C);
   const int Ho = a.H / pool;
-  const size_t lds_rows = sizeof(float) * (a.RB * pool + 2) * (a.W + 2);
+  const size_t lds_rows = sizeof(float) * (a.RB * pool + 2) * (a.W + (mf ? 4 : 2));
   constexpr int CV = 4;
   if (Ho > 0 && a.W / pool > 0) {  // dbeta / dgamma in both modes; training-mode dz also uses them
     const int blocks = a.N * ((Ho + a.RB - 1) / a.RB);
     const size_t lds = lds_rows + sizeof(float) * 8 * C;
-    with_pool(pool, [&](auto pc) {
-      constexpr int P = decltype(pc)::value;
-      if (dt == HVIT_BF16 && dy_dt == HVIT_BF16)
-        hipLaunchKernelGGL((c1_sums_kernel<bf16_t, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                           (const bf16_t*)dy, sums);
-      else if (dt == HVIT_BF16)
-        hipLaunchKernelGGL((c1_sums_kernel<bf16_t, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                           (const float*)dy, sums);
-      else if (dy_dt == HVIT_BF16)
-        hipLaunchKernelGGL((c1_sums_kernel<float, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                           (const bf16_t*)dy, sums);
-      else
-        hipLaunchKernelGGL((c1_sums_kernel<float, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                           (const float*)dy, sums);
-    });
+    if (mf) {
+      with_ncb(C, [&](auto nc) {
+        constexpr int NCB = decltype(nc)::value;
+        if (dy_dt == HVIT_BF16)
+          hipLaunchKernelGGL((c1m_sums_kernel<bf16_t, NCB>), dim3(blocks), dim3(THREADS), lds, st, a,
+                             (const bf16_t*)dy, sums);
+        else
+          hipLaunchKernelGGL((c1m_sums_kernel<float, NCB>), dim3(blocks), dim3(THREADS), lds, st, a,
+                             (const float*)dy, sums);
+      });
+    } else {
+      with_pool(pool, [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+        if (dt == HVIT_BF16 && dy_dt == HVIT_BF16)
+          hipLaunchKernelGGL((c1_sums_kernel<bf16_t, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                             (const bf16_t*)dy, sums);
+        else if (dt == HVIT_BF16)
+          hipLaunchKernelGGL((c1_sums_kernel<bf16_t, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                             (const float*)dy, sums);
+        else if (dy_dt == HVIT_BF16)
+          hipLaunchKernelGGL((c1_sums_kernel<float, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                             (const bf16_t*)dy, sums);
+        else
+          hipLaunchKernelGGL((c1_sums_kernel<float, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
+                             (const float*)dy, sums);
+      });
+    }
     HVIT_LAUNCH_CHECK();
     hipLaunchKernelGGL(slots_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, sums, 2 * C);
     HVIT_LAUNCH_CHECK();
@@ -539,6 +1076,19 @@ extern "C" int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w
   const int blocks = a.N * ((Hw + a.RB - 1) / a.RB);
   const size_t lds = lds_rows + sizeof(float) * 4 * C * 9;
   HVIT_CHECK(lds <= 64 * 1024, "hvit_c1block_bwd: LDS %zu too large", lds);
+  if (mf) {
+    with_ncb(C, [&](auto nc) {
+      constexpr int NCB = decltype(nc)::value;
+      if (dy_dt == HVIT_BF16)
+        hipLaunchKernelGGL((c1m_bwd_kernel<bf16_t, NCB>), dim3(blocks), dim3(THREADS), lds, st, a, (const bf16_t*)dy,
+                           sums, training, ws);
+      else
+        hipLaunchKernelGGL((c1m_bwd_kernel<float, NCB>), dim3(blocks), dim3(THREADS), lds, st, a, (const float*)dy,
+                           sums, training, ws);
+    });
+    HVIT_LAUNCH_CHECK();
+    return hvit_sum_slabs(ws, blocks, (long long)C * 9, dw_packed, stream);
+  }
   auto go = [&](auto ccc) {
     constexpr int CC = decltype(ccc)::value;
     with_pool(pool, [&](auto pc) {

@@ -161,7 +161,10 @@ extern "C" int hvit_debug_gemm_stamps(unsigned long long* host, int n) {
 // GEMM configuration of the bf16 linears (-1 = automatic per shape, 0 =
 // gemm.h's kernels only, 1-5 = one ring configuration; see gemm_ring.h).
 // Returns the previous value.
+int hvit_c1_tune(int value);  // c1block.hip
+
 extern "C" int hvit_gemm_tune(int what, int value) {
+  if (what == 1) return hvit_c1_tune(value);
   if (what != 0) return -1;
   const int old = ring_cfg_ref();
   ring_cfg_ref() = value;

@@ -53,13 +53,22 @@ CASES = [
     (2, 16, 24, 128, 1, 0.1),
     (1, 9, 8, 8, 2, 0.5),
     (2, 64, 251, 64, 2, 0.1),  # the model's 2 s clip width
+    (2, 40, 36, 32, 2, 0.2),
 ]
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.fixture
+def impl(HF, request):
+    """knob 1: the bf16 matrix-core kernels where they apply; 0: VALU kernels."""
+    old = HF.L.lib().hvit_gemm_tune(1, request.param)
+    yield request.param
+    HF.L.lib().hvit_gemm_tune(1, old)
+
+
+@pytest.mark.parametrize("dt,impl", [("f32", 1), ("bf16", 1), ("bf16", 0)], indirect=["impl"])
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("training", [True, False])
-def test_c1block_matches_torch(HF, dt, case, training):
+def test_c1block_matches_torch(HF, dt, impl, case, training):
     L = HF.L
     N, H, W, C, pool, p = case
     tdt = torch.float32 if dt == "f32" else torch.bfloat16
@@ -107,34 +116,42 @@ def test_c1block_matches_torch(HF, dt, case, training):
 
 @pytest.mark.parametrize("training", [True, False])
 def test_c1block_matches_unfused_path(HF, training):
-    """Fused and unfused library paths agree on the model's enc0 shape class
-    (eval mode included: both give the BatchNorm parameters their gradient)."""
+    """Fused and unfused library paths on the model's enc0 shape class, both
+    against the torch fp32 reference: the fused one (z and dz never rounded to
+    bf16) is at least as accurate.  Eval mode included: both paths give the
+    BatchNorm parameters their gradient."""
     L = HF.L
     N, H, W, C, pool, p = 4, 256, 256, 64, 2, 0.1
     torch.manual_seed(7)
     xa = torch.randn(N, H, W, 1, device=DEV).to(torch.bfloat16)
-    w = torch.randn(C, 1, 3, 3, device=DEV) / 3
+    w = (torch.randn(C, 1, 3, 3, device=DEV) / 3).to(torch.bfloat16).float()
     gamma = torch.rand(C, device=DEV) + 0.5
     beta = torch.randn(C, device=DEV) * 0.3
     gy = torch.randn(N, H // 2, W // 2, C, device=DEV).to(torch.bfloat16)
-    outs = []
+    seed, site = 55, 100
+    wr, gr, br = (t.clone().requires_grad_(True) for t in (w, gamma, beta))
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yr = reference(xa.float().permute(0, 3, 1, 2), wr, gr, br, rm, rv, training, p, seed, site, pool)
+    yr.backward(gy.float().permute(0, 3, 1, 2))
+    ref = (yr.detach().permute(0, 2, 3, 1), wr.grad, gr.grad, br.grad, rm, rv)
+    errs = {}
     for fused in (True, False):
         wa, ga, ba = (t.clone().requires_grad_(True) for t in (w, gamma, beta))
         rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
         nbt = torch.zeros((), dtype=torch.long, device=DEV)
-        d = HF.Drop(p, 55, 100)
+        d = HF.Drop(p, seed, site)
         if fused:
             y = HF.C1BlockFn.apply(xa, wa, ga, ba, rm, rv, nbt, pool, training, d, 0.1, 1e-5, L.BF16)
         else:
             y = HF.ConvBNActFn.apply(xa, None, wa, ga, ba, rm, rv, nbt, 1, pool, training, d, 0.1, 1e-5, L.BF16)
         y.backward(gy)
-        outs.append((y.float(), wa.grad, ga.grad, ba.grad, rm, rv))
-    (yf, wf, gf, bf, rmf, rvf), (yu, wu, gu, bu, rmu, rvu) = outs
-    # the unfused path rounds z to bf16 in HBM; the fused one keeps it in f32
-    assert rel(yf, yu) < 2e-2
-    assert rel(wf, wu) < 2e-2 and rel(gf, gu) < 2e-2 and rel(bf, bu) < 2e-2
-    assert rel(rmf, rmu) < 1e-5 and rel(rvf, rvu) < 1e-5
-    assert gf.abs().max() > 0 and bf.abs().max() > 0
+        got = (y.float(), wa.grad, ga.grad, ba.grad, rm, rv)
+        errs[fused] = [rel(a, b) for a, b in zip(got, ref)]
+    fe, ue = errs[True], errs[False]
+    assert fe[0] < 1e-2 and max(fe[1:4]) < 1e-3 and max(fe[4:]) < 1e-5, fe
+    assert max(ue[1:4]) < 1e-1, ue  # the unfused path rounds z and dz to bf16 in HBM
+    for i in range(1, 4):
+        assert fe[i] <= ue[i] * 1.5 + 1e-6, (i, fe, ue)
 
 
 def test_c1block_graph_seed_word(HF):
