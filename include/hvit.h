@@ -29,7 +29,14 @@ extern "C" {
 
 enum { HVIT_F32 = 0, HVIT_BF16 = 1 };
 enum { HVIT_OK = 0, HVIT_ERR_ARG = 1, HVIT_ERR_LAUNCH = 2 };
-enum { HVIT_ACT_NONE = 0, HVIT_ACT_GELU_DUAL = 1, HVIT_ACT_TANH = 2, HVIT_ACT_GELU_BWD = 3 };
+enum {
+  HVIT_ACT_NONE = 0,
+  HVIT_ACT_GELU_DUAL = 1,
+  HVIT_ACT_TANH = 2,
+  HVIT_ACT_GELU_BWD = 3,
+  HVIT_ACT_GELU_DUAL_D = 4, /* GELU_DUAL that stores gelu'(v) instead of v (for MUL_AUX) */
+  HVIT_ACT_MUL_AUX = 5      /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
+};
 /* flags of the backward calls that accumulate atomically: HVIT_ACC_ZEROED says
  * the caller already zeroed the accumulator outputs (one fill for a whole
  * backward pass), so the call skips its own clear. */
@@ -51,7 +58,9 @@ typedef struct {
 /* Fused GEMM epilogue (applied in this order):
  *   v  = acc (+ bias[n]) (+ rowadd[(m % rowadd_rows) * N + n])
  *   GELU_DUAL: y = v (pre-activation); out2 = dropout(gelu(v))      -> stop
+ *     (GELU_DUAL_D: y = gelu'(v) instead, the MUL_AUX operand of the backward)
  *   TANH: v = tanh(v) ; v = dropout(v) ; GELU_BWD: v *= gelu'(aux[m, n])
+ *     (MUL_AUX: v *= aux[m, n])
  *   resid: v = resid[m, n] + rowscale[m / rows_per_sample] * v     (f32)
  *   colsum[n] += sum_m v ; y[m, n] = v                                         */
 typedef struct {

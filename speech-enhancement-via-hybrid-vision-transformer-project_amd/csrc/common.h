@@ -162,6 +162,15 @@ __device__ __forceinline__ float gelu_grad(float x) {
   const float cdf = 0.5f * (1.f + erf_gauss(x * 0.70710678118654752f, e));
   return cdf + x * (0.39894228040143268f * e);
 }
+// GELU and its derivative from one erf / exp evaluation
+struct GeluGG {
+  float g, d;
+};
+__device__ __forceinline__ GeluGG gelu_gg(float x) {
+  float e;
+  const float cdf = 0.5f * (1.f + erf_gauss(x * 0.70710678118654752f, e));
+  return {x * cdf, cdf + x * (0.39894228040143268f * e)};
+}
 
 // ---------------------------------------------------------- wave reductions --
 __device__ __forceinline__ float wave_sum(float v) {

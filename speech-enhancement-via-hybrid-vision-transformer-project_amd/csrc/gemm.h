@@ -353,7 +353,8 @@ struct Epi {
   long rowadd_ld = 0;
   int rowadd_mod = 1;
   int act = ACT_NONE;
-  const void* aux = nullptr;  // GELU_BWD: pre-activation h[m][n]
+  const void* aux = nullptr;  // GELU_BWD: pre-activation h[m][n] (gd: gelu'(h) itself)
+  int gd = 0;  // GELU_DUAL: out receives gelu'(h) instead of h; GELU_BWD: aux already is gelu'(h)
   int aux_dt = HVIT_F32;
   long ldaux = 0;
   uint32_t drop_thr = 0;  // dropout keep test (0 = off)
@@ -514,10 +515,10 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
     for (int e = 0; e < 4; ++e) keep[e] = ep.drop_scale;
   }
   if (ep.act == ACT_GELU_DUAL) {
-    store4v<FAST>(ep.out, (long)m * ep.ldo + n, v, nv, ep.out_dt);
-    f32x4 g;
+    f32x4 g, d;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) g[e] = gelu_f(v[e]) * keep[e];
+    for (int e = 0; e < 4; ++e) { const GeluGG t_ = gelu_gg(v[e]); g[e] = t_.g * keep[e]; d[e] = t_.d; }
+    store4v<FAST>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, nv, ep.out_dt);
     store4v<FAST>(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
     return;
   }
@@ -529,7 +530,7 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
   for (int e = 0; e < 4; ++e) v[e] *= keep[e];
   if (ep.act == ACT_GELU_BWD) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(in.aux[e]);
+    for (int e = 0; e < 4; ++e) v[e] *= ep.gd ? in.aux[e] : gelu_grad(in.aux[e]);
   }
   if (ep.resid) {
 #pragma unroll
@@ -1322,18 +1323,18 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
         f32x4 va = *(const f32x4*)(Cs + row * CP + c8 * 8) + b8a;
         f32x4 vb = *(const f32x4*)(Cs + row * CP + c8 * 8 + 4) + b8b;
         if constexpr (EK == EK_GELU_DUAL) {
-          *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = wide8(va, vb);
           f32x4 ka = {1.f, 1.f, 1.f, 1.f}, kb = ka;
           if (ep.drop_thr) {
             ka = keep4(ep, dkey, m, n8, N);
             kb = keep4(ep, dkey, m, n8 + 4, N);
           }
-          f32x4 ga, gb;
+          f32x4 ga, gb, da, db;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            ga[e] = gelu_f(va[e]) * ka[e];
-            gb[e] = gelu_f(vb[e]) * kb[e];
+            { const GeluGG t_ = gelu_gg(va[e]); ga[e] = t_.g * ka[e]; da[e] = t_.d; }
+            { const GeluGG t_ = gelu_gg(vb[e]); gb[e] = t_.g * kb[e]; db[e] = t_.d; }
           }
+          *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? wide8(da, db) : wide8(va, vb);
           *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = wide8(ga, gb);
         } else {
           if (EK != EK_STORE && ep.drop_thr) {
@@ -1352,10 +1353,15 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
               ha = *(const f32x4*)((const float*)ep.aux + (long)m * ep.ldaux + n8);
               hb = *(const f32x4*)((const float*)ep.aux + (long)m * ep.ldaux + n8 + 4);
             }
+            if (ep.gd) {
+              va *= ha;
+              vb *= hb;
+            } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              va[e] *= gelu_grad(ha[e]);
-              vb[e] *= gelu_grad(hb[e]);
+              for (int e = 0; e < 4; ++e) {
+                va[e] *= gelu_grad(ha[e]);
+                vb[e] *= gelu_grad(hb[e]);
+              }
             }
           }
           if constexpr (EK == EK_RESID) {
@@ -1468,11 +1474,11 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int row = r0 + i * RSTEP;
           const int m = mbase + row;
           const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
-          store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
           const f32x4 k = ep.drop_thr ? keep4(ep, dkey, m, n, N) : (f32x4){1.f, 1.f, 1.f, 1.f};
-          f32x4 g;
+          f32x4 g, d;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) g[e] = gelu_f(v[e]) * k[e];
+          for (int e = 0; e < 4; ++e) { const GeluGG t_ = gelu_gg(v[e]); g[e] = t_.g * k[e]; d[e] = t_.d; }
+          store4v<true>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, 4, ep.out_dt);
           store4v<true>(ep.out2, (long)m * ep.ldo2 + n, g, 4, ep.out2_dt);
         }
       } else if constexpr (EK == EK_RESID) {
@@ -1514,8 +1520,12 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int m = mbase + row;
           f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
           if (ep.drop_thr) v *= keep4(ep, dkey, m, n, N);
+          if (ep.gd) {
+            v *= h[i];
+          } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(h[i][e]);
+            for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(h[i][e]);
+          }
           store4v<true>(ep.out, (long)m * ep.ldo + n, v, 4, ep.out_dt);
 #pragma unroll
           for (int e = 0; e < 4; ++e) csum[e] += v[e];

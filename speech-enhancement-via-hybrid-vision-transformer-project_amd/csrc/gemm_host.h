@@ -23,7 +23,9 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
   ep.out_dt = out_dt;
   ep.ldo = ldo;
   if (!e) return ep;
-  ep.act = e->act;
+  // GELU_DUAL_D / MUL_AUX: GELU_DUAL / GELU_BWD with gelu'(h) in place of h
+  ep.act = e->act == HVIT_ACT_GELU_DUAL_D ? HVIT_ACT_GELU_DUAL : e->act == HVIT_ACT_MUL_AUX ? HVIT_ACT_GELU_BWD : e->act;
+  ep.gd = e->act == HVIT_ACT_GELU_DUAL_D || e->act == HVIT_ACT_MUL_AUX;
   ep.out2 = e->out2;
   ep.out2_dt = e->out2_dt;
   ep.ldo2 = ldo;
@@ -51,9 +53,10 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
 
 int check_epi(const hvit_epilogue_t* e) {
   if (!e) return HVIT_OK;
-  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_GELU_BWD, "epilogue: bad act %d", e->act);
-  HVIT_CHECK(e->act != HVIT_ACT_GELU_DUAL || e->out2, "epilogue: GELU_DUAL needs out2");
-  HVIT_CHECK(e->act != HVIT_ACT_GELU_BWD || e->aux, "epilogue: GELU_BWD needs aux");
+  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_MUL_AUX, "epilogue: bad act %d", e->act);
+  HVIT_CHECK((e->act != HVIT_ACT_GELU_DUAL && e->act != HVIT_ACT_GELU_DUAL_D) || e->out2,
+             "epilogue: GELU_DUAL needs out2");
+  HVIT_CHECK((e->act != HVIT_ACT_GELU_BWD && e->act != HVIT_ACT_MUL_AUX) || e->aux, "epilogue: GELU_BWD needs aux");
   HVIT_CHECK(!(e->dropout.p < 0.f || e->dropout.p >= 1.f), "epilogue: dropout p out of range");
   return HVIT_OK;
 }

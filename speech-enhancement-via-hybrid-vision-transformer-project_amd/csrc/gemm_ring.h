@@ -266,18 +266,18 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
       va += b8a;
       vb += b8b;
       if constexpr (EK == EK_GELU_DUAL) {
-        *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = pack8(va, vb);
         f32x4 ka = {1.f, 1.f, 1.f, 1.f}, kb = ka;
         if (ep.drop_thr) {
           ka = keep4(ep, dkey, m, n8, N);
           kb = keep4(ep, dkey, m, n8 + 4, N);
         }
-        f32x4 ga, gb;
+        f32x4 ga, gb, da, db;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          ga[e] = gelu_f(va[e]) * ka[e];
-          gb[e] = gelu_f(vb[e]) * kb[e];
+          { const GeluGG t_ = gelu_gg(va[e]); ga[e] = t_.g * ka[e]; da[e] = t_.d; }
+          { const GeluGG t_ = gelu_gg(vb[e]); gb[e] = t_.g * kb[e]; db[e] = t_.d; }
         }
+        *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? pack8(da, db) : pack8(va, vb);
         *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = pack8(ga, gb);
         continue;
       }
@@ -288,10 +288,15 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
       if constexpr (EK == EK_GELU_BWD) {
         f32x4 ha, hb;
         unpack8(hin[i], ha, hb);
+        if (ep.gd) {
+          va *= ha;
+          vb *= hb;
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          va[e] *= gelu_grad(ha[e]);
-          vb[e] *= gelu_grad(hb[e]);
+          for (int e = 0; e < 4; ++e) {
+            va[e] *= gelu_grad(ha[e]);
+            vb[e] *= gelu_grad(hb[e]);
+          }
         }
       }
       if constexpr (EK == EK_RESID) {

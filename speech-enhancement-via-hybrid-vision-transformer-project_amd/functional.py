@@ -684,18 +684,20 @@ class ViTBlockFn(torch.autograd.Function):
                  epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), s)
         xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
         W1 = cast(f1w, dt)
-        h = _empty((M, hid), dt, dev)
+        # the fc1 epilogue keeps gelu'(h) (not h) for the backward: the fc2 dgrad
+        # epilogue then multiplies instead of re-evaluating erf / exp per element
+        gh = _empty((M, hid), dt, dev)
         a = _empty((M, hid), dt, dev)
         with timed("vit_linear_fwd", 2.0 * M * hid * D):
-            call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, h.data_ptr(), dt,
-                 epilogue(act=L.ACT_GELU_DUAL, out2=a, drop=d_fc1.c()), s)
+            call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, gh.data_ptr(), dt,
+                 epilogue(act=L.ACT_GELU_DUAL_D, out2=a, drop=d_fc1.c()), s)
         W2 = cast(f2w, dt)
         x2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_fwd", 2.0 * M * D * hid):
             call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid, x2.data_ptr(), F32,
                  epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
         ctx.save_for_backward(n1w, n2w)
-        ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2)
+        ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, gh, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
         # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
         # the GELU-backward epilogue and the two dropout passes)
@@ -707,7 +709,7 @@ class ViTBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx2, _dprobs=None):
         n1w, n2w = ctx.saved_tensors
-        (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, h, a, Wqkv, Wp, W1, W2, rs1, rs2) = ctx.t
+        (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, gh, a, Wqkv, Wp, W1, W2, rs1, rs2) = ctx.t
         B, Nt, D, H, hid, scale, dt, dra, drp, drf1, drf2 = ctx.meta
         M = B * Nt
         dev = x1.device
@@ -725,7 +727,7 @@ class ViTBlockFn(torch.autograd.Function):
         df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
         with timed("vit_linear_dgrad", 2.0 * M * D * hid):
             call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
-                 epilogue(act=L.ACT_GELU_BWD, aux=h, drop=drf1, colsum=df1b), s)
+                 epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b), s)
         df1w = linear_wgrad(dt, dh, xn2, M, hid, D, tag="vit_linear_wgrad")
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_dgrad", 2.0 * M * hid * D):

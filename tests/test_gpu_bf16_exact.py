@@ -94,6 +94,13 @@ def test_linear_fwd_kinds_exact(env, cfg):
     check_bf16(h, ref, what=f"fc1 h cfg {cfg}")
     mask = torch.as_tensor(keep_mask(21, 302, M * HID, 0.1).reshape(M, HID), device=DEV)
     check_bf16(a, F.gelu(ref) * mask / 0.9, acc=1e-4, what=f"fc1 a cfg {cfg}")  # GELU approximation <= 1.5e-7
+    # fc1 as the model runs it: GELU_DUAL_D keeps gelu'(h) for the backward
+    L.call("hvit_linear_fwd", L.BF16, x.data_ptr(), w1.data_ptr(), b1.data_ptr(), M, HID, D, h.data_ptr(), L.BF16,
+           HF.epilogue(act=L.ACT_GELU_DUAL_D, out2=a, drop=L.dropout(0.1, 21, 302)), s())
+    hp = ref.clone().requires_grad_(True)
+    F.gelu(hp).backward(torch.ones_like(hp))
+    check_bf16(h, hp.grad, acc=1e-4, what=f"fc1 gelu'(h) cfg {cfg}")
+    check_bf16(a, F.gelu(ref) * mask / 0.9, acc=1e-4, what=f"fc1 a (D) cfg {cfg}")
     # proj and fc2: f32 residual + DropPath row scale * dropout(v + b)
     res = torch.randn(M, D, device=DEV)
     rs = torch.rand(32, device=DEV) + 0.5
@@ -127,6 +134,14 @@ def test_linear_dgrad_kinds_exact(env, cfg):
     ref = (g2.float() @ w2.float()) * mk / 0.9 * hp.grad
     check_bf16(dh, ref, acc=1e-4, what=f"fc2 dgrad cfg {cfg}")
     check_f32(cs, ref.sum(0), acc=1e-4, what=f"fc2 dgrad colsum cfg {cfg}")
+    # the model's form: MUL_AUX with the stored gelu'(h) (bf16) as the multiplier
+    gd = hp.grad.to(BF)
+    cs.zero_()
+    L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh.data_ptr(), L.BF16,
+           HF.epilogue(act=L.ACT_MUL_AUX, aux=gd, drop=L.dropout(0.1, 23, 304), colsum=cs), s())
+    ref = (g2.float() @ w2.float()) * mk / 0.9 * gd.float()
+    check_bf16(dh, ref, what=f"fc2 dgrad MUL_AUX cfg {cfg}")
+    check_f32(cs, ref.sum(0), acc=1e-4, what=f"fc2 dgrad MUL_AUX colsum cfg {cfg}")
     # fc1 / qkv dgrad (f32 out), proj dgrad (bf16 out)
     for name, N, K, odt in (("fc1", HID, D, L.F32), ("qkv", 3 * D, D, L.F32), ("proj", D, D, L.BF16)):
         dy = rb(M, N)

@@ -77,6 +77,13 @@ def test_linear_fwd_epilogues(hv, dt):
     mask = torch.as_tensor(keep_mask(99, 5, M * N, 0.25).reshape(M, N), device=DEV)
     assert rel(h.float(), ref) < tol(dt)
     assert rel(a.float(), F.gelu(ref) * mask / 0.75) < tol(dt)
+    # GELU_DUAL_D: the first output is gelu'(v)
+    l.call("hvit_linear_fwd", l.dt_of(x), x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, h.data_ptr(),
+           l.dt_of(h), HF.epilogue(act=l.ACT_GELU_DUAL_D, out2=a, drop=dr), s())
+    hp = ref.clone().requires_grad_(True)
+    F.gelu(hp).backward(torch.ones_like(hp))
+    assert rel(h.float(), hp.grad) < tol(dt)
+    assert rel(a.float(), F.gelu(ref) * mask / 0.75) < tol(dt)
     # residual + per-sample scale + dropout
     resid = torch.randn(M, N, device=DEV)
     rs = torch.tensor([0.0, 1.25, 1.25, 0.5], device=DEV)
@@ -128,6 +135,11 @@ def test_linear_dgrad_gelu_bwd(hv, dt, M):
     F.gelu(hp).backward(torch.ones_like(hp))
     mask = torch.as_tensor(keep_mask(7, 3, M * K, 0.1).reshape(M, K), device=DEV)
     assert rel(dx, ref * mask / 0.9 * hp.grad) < tol(dt)
+    # MUL_AUX: the multiplier is given (the stored gelu'(h) of GELU_DUAL_D)
+    gd = hp.grad.to(tdt(dt))
+    l.call("hvit_linear_dgrad", l.dt_of(dy), dy.data_ptr(), w.data_ptr(), M, N, K, dx.data_ptr(), l.F32,
+           HF.epilogue(act=l.ACT_MUL_AUX, aux=gd, drop=dr), s())
+    assert rel(dx, ref * mask / 0.9 * gd.float()) < tol(dt)
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
