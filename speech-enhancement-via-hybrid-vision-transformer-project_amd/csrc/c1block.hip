@@ -426,9 +426,9 @@ __global__ __launch_bounds__(THREADS) void c1_bwd_kernel(Args a_, const TD* __re
 // order works for a sum, as long as A uses the same), and A = the taps of those
 // pixels read from LDS.  dz enters as bf16 hi + lo (two MFMAs), so the product
 // keeps ~16 mantissa bits of dz; x is exact in bf16.
-// BatchNorm statistics: per lane sums (sum z, sum z^2) over its <= 64 values of
-// a 1024-pixel tile, turned into (mean, M2) and merged with Chan's formula, in
-// the tile layout of hvit_conv_bn_tile_rows (thinconv.hip c1_fwd).
+// BatchNorm statistics: from the 10x10 Gram matrix of (taps, 1) over a
+// 1024-pixel tile (c1m_stats_kernel), in the tile layout of
+// hvit_conv_bn_tile_rows (thinconv.hip c1_fwd).
 constexpr int STATS_TILE = 1024;  // == hvit_thin_c1_bn_tile_rows()
 
 __device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c) {
@@ -748,15 +748,18 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
 }
 
 // BatchNorm (mean, M2) partials of z over 1024-pixel raster tiles (the layout
-// hvit_bn_finalize reads with tile_rows = STATS_TILE).  Rows of a 16-pixel group
-// are consecutive raster pixels; taps are read from the tile's staged strip
-// (pixels [p0 - W - 1, pend + W + 1)) with the image-boundary tests.
-template <int NCB>
+// hvit_bn_finalize reads with tile_rows = STATS_TILE), without forming z:
+// z_c = w_c . t over the 9 taps t of a pixel, so a tile's
+//   sum z_c = w_c . S,  sum z_c^2 = w_c^T G w_c,  S = sum_px t,  G = sum_px t t^T.
+// G (with a constant-1 tap 9, so G[9][.] = S and G[9][9] = the pixel count)
+// is one 16x16x32 MFMA per 32 pixels: A = B = the taps, lane l holding tap l&15
+// of pixels k = 8*(l>>4) + j.  Taps are exact bf16 values, the products exact
+// in f32.  Per channel the tile then needs 100 FMAs instead of 2 per pixel.
 __global__ __launch_bounds__(THREADS) void c1m_stats_kernel(const bf16_t* __restrict__ x,
                                                             const bf16_t* __restrict__ w, float* __restrict__ stats,
                                                             int N, int H, int W, int C) {
   extern __shared__ __attribute__((aligned(16))) float xs[];
-  __shared__ float red[4][3][64];
+  __shared__ float gr[4][16][17];
   const int P = N * H * W;
   const int p0 = blockIdx.x * STATS_TILE, pend = min(P, p0 + STATS_TILE);
   const long base = (long)p0 - W - 1;
@@ -780,85 +783,59 @@ __global__ __launch_bounds__(THREADS) void c1m_stats_kernel(const bf16_t* __rest
     __syncthreads();
   }
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c0 = NCB * (l & 15);
-  u32x4 bw[NCB];
-  weight_frags<NCB>(w, l, bw);
-  float s1[NCB], s2[NCB], cnt = 0.f;
-#pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) s1[cb] = s2[cb] = 0.f;
+  const int m = l & 15;  // this lane's tap: (dy, dx) = (m / 3, m % 3) for m < 9, 1 for m == 9, 0 above
+  const int dy = m < 9 ? m / 3 - 1 : 0, dx = m < 9 ? m % 3 - 1 : 0;
+  const int toff = dy * W + dx;
   const int HW = H * W;
-  for (int g = wv; 16 * g < pend - p0; g += THREADS / 64) {
-    const int p = min(p0 + 16 * g + (l & 15), pend - 1);
-    const int rem = p % HW, yy = rem / W, xx = rem - yy * W;
-    const bool up = yy > 0, dn = yy + 1 < H, lf = xx > 0, rt = xx + 1 < W;
-    const float* c = xs + (p - base);
-    float t[9];
-    t[0] = (up && lf) ? c[-W - 1] : 0.f;
-    t[1] = up ? c[-W] : 0.f;
-    t[2] = (up && rt) ? c[-W + 1] : 0.f;
-    t[3] = lf ? c[-1] : 0.f;
-    t[4] = c[0];
-    t[5] = rt ? c[1] : 0.f;
-    t[6] = (dn && lf) ? c[W - 1] : 0.f;
-    t[7] = dn ? c[W] : 0.f;
-    t[8] = (dn && rt) ? c[W + 1] : 0.f;
-    const u32x4 af = tap_frag(t, l);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int g = wv; 32 * g < pend - p0; g += THREADS / 64) {
+    // pixels p0 + 32g + 8*(l>>4) + j, j = 0..7: (y, x) of the first, then stepped
+    int p = p0 + 32 * g + 8 * (l >> 4);
+    const int rem = p % HW;
+    int yy = rem / W, xx = rem - yy * W;
+    float t[8];
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      const f32x4 z = mfma16(af, bw[cb], (f32x4){0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = (p0 + 16 * g + 4 * (l >> 4) + j < pend) ? z[j] : 0.f;
-        s1[cb] += v;
-        s2[cb] += v * v;
+    for (int j = 0; j < 8; ++j) {
+      const bool in = p < pend;
+      const bool ok = in && (unsigned)(yy + dy) < (unsigned)H && (unsigned)(xx + dx) < (unsigned)W;
+      const float v = xs[min(p, pend - 1) - base + toff];
+      t[j] = m < 9 ? (ok ? v : 0.f) : (m == 9 && in ? 1.f : 0.f);
+      ++p;
+      if (++xx == W) {
+        xx = 0;
+        if (++yy == H) yy = 0;
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cnt += (p0 + 16 * g + 4 * (l >> 4) + j < pend) ? 1.f : 0.f;
+    const u32x4 f = {f2bf2(t[0], t[1]), f2bf2(t[2], t[3]), f2bf2(t[4], t[5]), f2bf2(t[6], t[7])};
+    acc = mfma16(f, f, acc);
   }
-  // per lane (n, mean, M2), then Chan merges: lanes l, l^16, l^32, l^48 share channels
-  float mu[NCB], m2[NCB];
+  // acc: lane l holds G[4*(l>>4) + j][l & 15]; sum the four waves
 #pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) {
-    mu[cb] = cnt > 0.f ? s1[cb] / cnt : 0.f;
-    m2[cb] = cnt > 0.f ? fmaxf(s2[cb] - s1[cb] * mu[cb], 0.f) : 0.f;
-  }
-#pragma unroll
-  for (int o = 16; o < 64; o <<= 1) {
-    const float nb = __shfl_xor(cnt, o, 64), nt = cnt + nb;
-    const float fb = nt > 0.f ? nb / nt : 0.f;
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      const float mb = __shfl_xor(mu[cb], o, 64), qb = __shfl_xor(m2[cb], o, 64);
-      const float d = mb - mu[cb];
-      m2[cb] += qb + d * d * cnt * fb;
-      mu[cb] += d * fb;
-    }
-    cnt = nt;
-  }
-  if (l < 16) {
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-      red[wv][0][c0 + cb] = cnt;
-      red[wv][1][c0 + cb] = mu[cb];
-      red[wv][2][c0 + cb] = m2[cb];
-    }
+  for (int j = 0; j < 4; ++j) gr[wv][4 * (l >> 4) + j][m] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 100) {
+    const int r = threadIdx.x / 10, c = threadIdx.x % 10;
+    gr[0][r][c] = gr[0][r][c] + gr[1][r][c] + gr[2][r][c] + gr[3][r][c];
   }
   __syncthreads();
   if (threadIdx.x < C) {
     const int c = threadIdx.x;
-    float na = 0.f, ma = 0.f, qa = 0.f;
+    float wc[9];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const float nb = red[v][0][c];
-      if (nb <= 0.f) continue;
-      const float nt = na + nb, d = red[v][1][c] - ma;
-      qa += red[v][2][c] + d * d * na * nb / nt;
-      ma += d * nb / nt;
-      na = nt;
+    for (int k = 0; k < 9; ++k) wc[k] = bf2f(w[c * 9 + k]);
+    const float n = gr[0][9][9];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+      s1 += wc[a] * gr[0][9][a];
+      float ga = 0.f;
+#pragma unroll
+      for (int b = 0; b < 9; ++b) ga += gr[0][a][b] * wc[b];
+      s2 += wc[a] * ga;
     }
-    stats[((size_t)blockIdx.x * C + c) * 2] = ma;
-    stats[((size_t)blockIdx.x * C + c) * 2 + 1] = qa;
+    const float mean = n > 0.f ? s1 / n : 0.f;
+    stats[((size_t)blockIdx.x * C + c) * 2] = mean;
+    stats[((size_t)blockIdx.x * C + c) * 2 + 1] = fmaxf(s2 - s1 * mean, 0.f);
   }
 }
 
@@ -953,12 +930,8 @@ extern "C" int hvit_c1block_stats(int dt, const hvit_conv_geom_t* g, const void*
     const long P = (long)g->N * g->Hs * g->Ws;
     HVIT_CHECK(P < (1L << 31), "hvit_c1block_stats: too many pixels");
     if (P <= 0) return HVIT_OK;
-    with_ncb(C, [&](auto nc) {
-      constexpr int NCB = decltype(nc)::value;
-      hipLaunchKernelGGL((c1m_stats_kernel<NCB>), dim3(cdiv(P, STATS_TILE)), dim3(THREADS), lds,
-                         (hipStream_t)stream, (const bf16_t*)g->src1, (const bf16_t*)w_packed, bn_partials, g->N,
-                         g->Hs, g->Ws, C);
-    });
+    hipLaunchKernelGGL(c1m_stats_kernel, dim3(cdiv(P, STATS_TILE)), dim3(THREADS), lds, (hipStream_t)stream,
+                       (const bf16_t*)g->src1, (const bf16_t*)w_packed, bn_partials, g->N, g->Hs, g->Ws, C);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
