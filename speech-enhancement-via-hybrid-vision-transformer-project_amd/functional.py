@@ -345,6 +345,44 @@ class CastFn(torch.autograd.Function):
         return cast(g, ctx.src_dt), None
 
 
+SKIPGRAD = os.environ.get("HVIT_SKIPGRAD", "1") != "0"  # A/B knob: 0 = autograd adds the skip gradients
+
+
+class SkipGrad:
+    """The skip gradient of one encoder output, handed from its SkipFn to its
+    other consumer (the next encoder block or the patch embedding) instead of
+    being summed by autograd (hybrid_vit.py:303-305, 376-389: an encoder output
+    feeds both).  SkipFn's backward offers its gradient at decoder resolution,
+    before the bilinear backward; the other consumer's backward then runs that
+    bilinear backward in accumulate mode straight into its own input gradient,
+    so no separate add of two full-resolution tensors is launched.  Backward
+    order makes the offer come first (the decoder's backward completes before
+    the ViT's, which precedes the encoder's); if the consumer drained first,
+    SkipFn returns its gradient to autograd as usual."""
+
+    __slots__ = ("dr", "meta", "closed")
+
+    def __init__(self):
+        self.dr, self.meta, self.closed = None, None, False
+
+    def offer(self, dr, meta) -> bool:
+        if self.closed:
+            return False
+        self.dr, self.meta = dr, meta
+        return True
+
+    def drain(self, de):
+        """Add the offered gradient into ``de`` (the consumer's NHWC input gradient)."""
+        self.closed = True
+        if self.dr is None:
+            return
+        N, Ho, Wo, Ce, He, We, dt = self.meta
+        assert tuple(de.shape) == (N, He, We, Ce) and de.is_contiguous(), (de.shape, self.meta)
+        call("hvit_bilinear_bwd", self.dr.data_ptr(), dt, N, Ho, Wo, Ce, He, We, de.data_ptr(), L.dt_of(de), 1,
+             stream_ptr())
+        self.dr = None
+
+
 class ConvBNActFn(torch.autograd.Function):
     """[nearest up U] -> Conv KSxKS (no bias) over concat(x1, x2) -> BatchNorm2d
     -> ReLU -> Dropout2d -> [MaxPool 2]  (ConvBlock components.py:15-99,
@@ -352,7 +390,8 @@ class ConvBNActFn(torch.autograd.Function):
     hybrid_vit.py:389).  NHWC in / out."""
 
     @staticmethod
-    def forward(ctx, x1, x2, w, gamma, beta, rmean, rvar, nbt, U, pool, training, drop: Drop, momentum, eps, dt):
+    def forward(ctx, x1, x2, w, gamma, beta, rmean, rvar, nbt, U, pool, training, drop: Drop, momentum, eps, dt,
+                sg: Optional[SkipGrad] = None):
         N, Hs, Ws, C1 = x1.shape
         C2 = x2.shape[3] if x2 is not None else 0
         Cout, Cin, KS, _ = w.shape
@@ -389,6 +428,7 @@ class ConvBNActFn(torch.autograd.Function):
         ctx.save_for_backward(x1, x2, w, gamma, beta)
         ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
         ctx.meta = (U, pool, training, dr, dt)
+        ctx.sg = sg
         ctx.zs = _zs(ctx, L.lib().hvit_bn_act_bwd_sums_elems(Cout))
         return y
 
@@ -421,12 +461,14 @@ class ConvBNActFn(torch.autograd.Function):
                 call("hvit_conv_dgrad", dt, g, dz.data_ptr(), wd.data_ptr(), du.data_ptr(), dt, s)
             if U == 1 and C2 == 0:
                 dx1 = du
+                if ctx.sg is not None:
+                    ctx.sg.drain(dx1)
             else:
                 dx1 = _empty((N, Hs, Ws, C1), dt, dev)
                 dx2 = _empty((N, Hs, Ws, C2), dt, dev) if C2 else None
                 call("hvit_upsample_split_bwd", du.data_ptr(), dt, N, Hs, Ws, U, C1, C2, dx1.data_ptr(), dt,
                      ptr(dx2), dt, s)
-        return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 10
+        return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 11
 
 
 C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path
@@ -519,7 +561,7 @@ class PatchEmbedFn(torch.autograd.Function):
     NHWC feature map -> f32 tokens [B, N, D]."""
 
     @staticmethod
-    def forward(ctx, feat, w, b, pos, Pp, drop: Drop, training, dt):
+    def forward(ctx, feat, w, b, pos, Pp, drop: Drop, training, dt, sg: Optional[SkipGrad] = None):
         N, H, W, C = feat.shape
         D = w.shape[0]
         Hp, Wp = H // Pp, W // Pp
@@ -537,6 +579,7 @@ class PatchEmbedFn(torch.autograd.Function):
         ctx.save_for_backward(feat, w)
         ctx.wp = wp
         ctx.meta = (Pp, dr, dt, Nt, None if pos is None else pos.shape)
+        ctx.sg = sg
         ctx.zs = _zs(ctx, D)
         return x0
 
@@ -563,7 +606,9 @@ class PatchEmbedFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dfeat = _empty(feat.shape, dt, dev)
             call("hvit_conv_dgrad", dt, g, gd.data_ptr(), ctx.wp.data_ptr(), dfeat.data_ptr(), dt, s)
-        return dfeat, dw, db, dpos, None, None, None, None
+            if ctx.sg is not None:
+                ctx.sg.drain(dfeat)
+        return dfeat, dw, db, dpos, None, None, None, None, None
 
 
 class PosDropFn(torch.autograd.Function):
@@ -804,7 +849,7 @@ class SkipFn(torch.autograd.Function):
     the GEMM runs on the (up to 16x) smaller grid.  NHWC in / out."""
 
     @staticmethod
-    def forward(ctx, e, w, b, Ho, Wo, dt):
+    def forward(ctx, e, w, b, Ho, Wo, dt, sg: Optional[SkipGrad] = None):
         N, He, We, Ce = e.shape
         Cd = w.shape[0]
         dev = e.device
@@ -820,6 +865,7 @@ class SkipFn(torch.autograd.Function):
         call("hvit_linear_fwd", dt, r.data_ptr(), W.data_ptr(), b.data_ptr(), M, Cd, Ce, y.data_ptr(), dt, None, s)
         ctx.t = (r, W)
         ctx.meta = (N, He, We, Ce, Ho, Wo, Cd, dt, tuple(w.shape))
+        ctx.sg = sg
         return y
 
     @staticmethod
@@ -836,12 +882,14 @@ class SkipFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dr = _empty((N, Ho, Wo, Ce), dt, dev)
             call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, Cd, Ce, dr.data_ptr(), dt, None, s)
+            if ctx.sg is not None and ctx.sg.offer(dr, (N, Ho, Wo, Ce, He, We, dt)):
+                return None, dw, db, None, None, None, None  # the encoder output's other consumer adds it
             if (He, We) != (Ho, Wo):
                 de = _empty((N, He, We, Ce), dt, dev)
                 call("hvit_bilinear_bwd", dr.data_ptr(), dt, N, Ho, Wo, Ce, He, We, de.data_ptr(), dt, 0, s)
             else:
                 de = dr
-        return de, dw, db, None, None, None
+        return de, dw, db, None, None, None, None
 
 
 class FinalFn(torch.autograd.Function):

@@ -408,11 +408,16 @@ class HybridViT(nn.Module):
         return t.permute(0, 3, 1, 2)
 
     # ---------------------------------------------------------- stage runners --
-    def _encoder(self, xh, dt, seed):
+    def _encoder(self, xh, dt, seed, sgs=None):
+        """Encoder blocks; each output is a skip.  sgs (full forward only): one
+        HF.SkipGrad per encoder output, through which the output's SkipFn hands
+        its gradient to the output's other consumer (next block / patch embed)
+        instead of an autograd add."""
         skips = []
         h = xh
         for i, blk in enumerate(self.encoder):
             bn = blk.bn
+            sg = sgs[i - 1] if sgs is not None and i > 0 else None  # this block consumes output i - 1
             if HF.c1block_ok(h, None, blk.conv.weight, 1, blk.pool):
                 h = HF.C1BlockFn.apply(h, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                        bn.num_batches_tracked, blk.pool, self.training,
@@ -420,20 +425,20 @@ class HybridViT(nn.Module):
             else:
                 h = HF.ConvBNActFn.apply(h, None, blk.conv.weight, bn.weight, bn.bias, bn.running_mean,
                                          bn.running_var, bn.num_batches_tracked, 1, blk.pool, self.training,
-                                         HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt)
+                                         HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt, sg)
             skips.append(h)
         return h, skips
 
-    def _tokens(self, feat, dt, seed):
+    def _tokens(self, feat, dt, seed, sg=None):
         P = self.patch_size
         pe = self.patch_embed.projection
         hw = (feat.shape[1] // P, feat.shape[2] // P)
         if self.cls_token is None:  # hot path: pos-embed add and dropout fused into the GEMM epilogue
             t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, self.pos_encoding.pos_embed, P,
-                                      HF.Drop(self.dropout_p, 0, 200, seed), self.training, dt)
+                                      HF.Drop(self.dropout_p, 0, 200, seed), self.training, dt, sg)
             self.last_num_tokens = t.shape[1]
             return t, hw
-        t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, None, P, HF.Drop(), False, dt)
+        t = HF.PatchEmbedFn.apply(feat, pe.weight, pe.bias, None, P, HF.Drop(), False, dt, sg)
         return self._pos_tokens(t, seed), hw
 
     def _pos_tokens(self, t, seed):
@@ -471,8 +476,9 @@ class HybridViT(nn.Module):
         n = self.transformer.norm
         return HF.HeadFn.apply(t, n.weight, n.bias, self.to_feature_map.weight, self.to_feature_map.bias, hw, dt)
 
-    def _decoder(self, x, skips, out_hw, dt, seed):
+    def _decoder(self, x, skips, out_hw, dt, seed, sgs=None):
         skips = skips[::-1]
+        sgs = sgs[::-1] if sgs is not None else [None] * len(skips)
         nd = len(self.decoder)
         for i, blk in enumerate(self.decoder):
             if blk.final:
@@ -480,7 +486,7 @@ class HybridViT(nn.Module):
             s = None
             if self.use_skip_connections and i < nd - 1 and i < len(skips):
                 sp = self.skip_projections[i]
-                s = HF.SkipFn.apply(skips[i], sp.weight, sp.bias, x.shape[1], x.shape[2], dt)
+                s = HF.SkipFn.apply(skips[i], sp.weight, sp.bias, x.shape[1], x.shape[2], dt, sgs[i])
             bn = blk.bn
             x = HF.ConvBNActFn.apply(x, s, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                      bn.num_batches_tracked, blk.up, 1, self.training,
@@ -541,11 +547,13 @@ class HybridViT(nn.Module):
         F, T = x.shape[2], x.shape[3]
         self._prep_weights(dt, x.device)
         xh = HF.CastFn.apply(self._nhwc(x.float() if x.dtype != torch.float32 else x), dt)
-        feat, skips = self._encoder(xh, dt, seed)
-        t, hw = self._tokens(feat, dt, seed)
+        # skip gradients handed between an encoder output's two consumers (HF.SkipGrad)
+        sgs = [HF.SkipGrad() for _ in self.encoder] if self.use_skip_connections and HF.SKIPGRAD else None
+        feat, skips = self._encoder(xh, dt, seed, sgs)
+        t, hw = self._tokens(feat, dt, seed, sgs[-1] if sgs else None)
         t, attns = self._vit(t, dt, seed, return_attentions)
         f = self._head(t, hw, dt)
-        out = self._decoder(f, skips, (F, T), dt, seed)
+        out = self._decoder(f, skips, (F, T), dt, seed, sgs)
         HF.zflush(x.device)
         out = self._nchw(out)
         if return_attentions:
