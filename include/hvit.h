@@ -35,7 +35,8 @@ enum {
   HVIT_ACT_TANH = 2,
   HVIT_ACT_GELU_BWD = 3,
   HVIT_ACT_GELU_DUAL_D = 4, /* GELU_DUAL that stores gelu'(v) instead of v (for MUL_AUX) */
-  HVIT_ACT_MUL_AUX = 5      /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
+  HVIT_ACT_MUL_AUX = 5,     /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
+  HVIT_ACT_RELU = 6         /* conv forward only: v = max(v + bias, 0) (eval-mode BatchNorm folded) */
 };
 /* flags of the backward calls that accumulate atomically: HVIT_ACC_ZEROED says
  * the caller already zeroed the accumulator outputs (one fill for a whole
@@ -144,6 +145,13 @@ int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy, float* dw
 int hvit_conv_weight_pack(const float* w, int Cout, int Cin, int KS, int mode, void* out, int out_dt,
                           void* stream);
 int hvit_conv_weight_unpack(const float* dw_packed, int Cout, int Cin, int KS, float* dw, void* stream);
+/* Eval-mode BatchNorm folded into the conv (components.py:55-85 in eval):
+ * w_packed (mode 0, w_dt) = w * gamma * invstd per output channel, bias =
+ * beta - mean * gamma * invstd, so relu(bn(conv(x, w))) = conv(x, w_packed) +
+ * bias through hvit_conv_fwd with act HVIT_ACT_RELU (mean / invstd from
+ * hvit_bn_eval_prep). */
+int hvit_bn_fold(const float* w, int Cout, int Cin, int KS, const float* mean, const float* invstd,
+                 const float* gamma, const float* beta, void* w_packed, int w_dt, float* bias, void* stream);
 
 /* ---- Multi-head self-attention core (attention.py:82-107): softmax(q k^T *
  * scale) -> dropout -> @ v with qkv [B, N, 3, H, hd] (the qkv Linear output)

@@ -14,7 +14,7 @@ import threading
 import torch
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD, ACT_GELU_DUAL_D, ACT_MUL_AUX = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD, ACT_GELU_DUAL_D, ACT_MUL_AUX, ACT_RELU = 0, 1, 2, 3, 4, 5, 6
 ACC_ZEROED = 1
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -86,6 +86,7 @@ _SIGS = {
     "hvit_conv_wgrad": ([i32, P(ConvGeom), vp, vp, vp, i64, vp], i32),
     "hvit_conv_weight_pack": ([vp, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_conv_weight_unpack": ([vp, i32, i32, i32, vp, vp], i32),
+    "hvit_bn_fold": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),
     "hvit_mhsa_fwd": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_fwd_fp8": ([vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),

@@ -41,6 +41,25 @@ __global__ void conv_pack_kernel(const float* w, int Cout, int Cin, int KS, int 
   }
 }
 
+// Eval-mode BatchNorm folded into the conv (components.py:55-85 in eval):
+// relu(bn(conv(x, w))) = relu(conv(x, w * sc) + sh), sc = gamma * invstd,
+// sh = beta - mean * sc; packed mode-0 weights and the f32 bias
+__global__ void bn_fold_kernel(const float* w, int Cout, int Cin, int KS, const float* mean, const float* invstd,
+                               const float* gamma, const float* beta, void* out, int odt, float* bias) {
+  const long total = (long)Cout * Cin * KS * KS;
+  GRID_STRIDE(i, total) {
+    const int kx = i % KS;
+    long t = i / KS;
+    const int ky = t % KS;
+    t /= KS;
+    const int ci = t % Cin;
+    const int co = t / Cin;
+    const float sc = gamma[co] * invstd[co];
+    st_dt(out, (((long)co * KS + ky) * KS + kx) * Cin + ci, w[i] * sc, odt);
+    if (i < Cout) bias[i] = beta[i] - mean[i] * (gamma[i] * invstd[i]);
+  }
+}
+
 // dw[co][ci][ky][kx] = dwp[co][ky][kx][ci]
 __global__ void conv_unpack_kernel(const float* dwp, int Cout, int Cin, int KS, float* dw) {
   long total = (long)Cout * Cin * KS * KS;
@@ -341,6 +360,18 @@ extern "C" int hvit_conv_weight_pack(const float* w, int Cout, int Cin, int KS, 
   long n = (long)Cout * Cin * KS * KS;
   hipLaunchKernelGGL(conv_pack_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS,
                      mode, out, out_dt);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
+extern "C" int hvit_bn_fold(const float* w, int Cout, int Cin, int KS, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, void* w_packed, int w_dt, float* bias,
+                            void* stream) {
+  HVIT_CHECK(w && mean && invstd && gamma && beta && w_packed && bias, "hvit_bn_fold: null pointer");
+  const long n = (long)Cout * Cin * KS * KS;
+  HVIT_CHECK(n >= Cout && Cout > 0, "hvit_bn_fold: bad shape");
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS, mean,
+                     invstd, gamma, beta, w_packed, w_dt, bias);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

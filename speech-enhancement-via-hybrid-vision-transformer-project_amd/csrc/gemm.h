@@ -355,6 +355,7 @@ struct Epi {
   int act = ACT_NONE;
   const void* aux = nullptr;  // GELU_BWD: pre-activation h[m][n] (gd: gelu'(h) itself)
   int gd = 0;  // GELU_DUAL: out receives gelu'(h) instead of h; GELU_BWD: aux already is gelu'(h)
+  int relu = 0;  // v = max(v, 0) after bias (the eval-mode folded BatchNorm + ReLU of the conv blocks)
   int aux_dt = HVIT_F32;
   long ldaux = 0;
   uint32_t drop_thr = 0;  // dropout keep test (0 = off)
@@ -525,6 +526,10 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
   if (ep.act == ACT_TANH) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+  }
+  if (ep.relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] *= keep[e];
@@ -1451,7 +1456,11 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const int row = r0 + i * RSTEP;
           const int m = mbase + row;
           if (PRED && (m >= M || !nok)) continue;
-          const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
+          f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
+          if (ep.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
           if (ep.out_dt == HVIT_F32) {
             *(f32x4*)((float*)ep.out + (long)m * ep.ldo + n) = v;
           } else {

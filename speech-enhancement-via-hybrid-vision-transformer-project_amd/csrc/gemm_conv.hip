@@ -11,8 +11,9 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
   if (int rc = check_geom(g)) return rc;
   HVIT_CHECK(w_packed && y, "hvit_conv_fwd: null pointer");
   if (int rc = check_epi(epi)) return rc;
-  HVIT_CHECK(!epi || epi->act == HVIT_ACT_NONE || epi->act == HVIT_ACT_TANH,
-             "hvit_conv_fwd: act must be NONE or TANH");
+  HVIT_CHECK(!epi || epi->act == HVIT_ACT_NONE || epi->act == HVIT_ACT_TANH || epi->act == HVIT_ACT_RELU,
+             "hvit_conv_fwd: act must be NONE, TANH or RELU");
+  HVIT_CHECK(!epi || epi->act != HVIT_ACT_RELU || !bn_partials, "hvit_conv_fwd: RELU with BatchNorm partials");
   HVIT_CHECK(!epi || !epi->resid, "hvit_conv_fwd: residual epilogue unsupported");
   HVIT_CHECK(aligned16(w_packed), "hvit_conv_fwd: weight alignment");
   const bool plain_epi = !epi || (epi->dropout.p == 0.f && !epi->rowadd && !epi->colsum);
@@ -21,7 +22,7 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
   // BN partial tiles follow hvit_conv_bn_tile_rows(g): the thin path must have been taken
   HVIT_CHECK(!bn_partials || !thin_c1(g), "hvit_conv_fwd: Cin=1 BatchNorm partials need the thin path "
                                            "(no bias / epilogue, 16-byte aligned output)");
-  if (thin_o1(g) && plain_epi && !bias && !bn_partials)
+  if (thin_o1(g) && plain_epi && !bias && !bn_partials && (!epi || epi->act != HVIT_ACT_RELU))
     return hvit_thin_o1_fwd(dt, g, w_packed, y, y_dt, epi && epi->act == HVIT_ACT_TANH, (hipStream_t)stream);
   Epi ep = to_epi(epi, y, y_dt, g->Cout);
   ep.bias = bias;

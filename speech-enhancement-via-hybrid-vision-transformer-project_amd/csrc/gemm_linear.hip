@@ -8,6 +8,7 @@ extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float
   HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_fwd: bad shape M=%d N=%d K=%d", M, N, K);
   HVIT_CHECK(aligned16(x) && aligned16(w), "hvit_linear_fwd: x/w must be 16-byte aligned");
   if (int rc = check_epi(epi)) return rc;
+  HVIT_CHECK(!epi || epi->act != HVIT_ACT_RELU, "hvit_linear_fwd: RELU is a conv-forward epilogue");
   Epi ep = to_epi(epi, y, y_dt, N);
   ep.bias = bias;
   if (dt == HVIT_BF16) {
@@ -29,6 +30,7 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
   HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_dgrad: bad shape");
   HVIT_CHECK(aligned16(dy) && aligned16(w), "hvit_linear_dgrad: alignment");
   if (int rc = check_epi(epi)) return rc;
+  HVIT_CHECK(!epi || epi->act != HVIT_ACT_RELU, "hvit_linear_dgrad: RELU is a conv-forward epilogue");
   Epi ep = to_epi(epi, dx, dx_dt, K);
   if (dt == HVIT_BF16 && N % 8 == 0) {
     int rc = 0;

@@ -438,7 +438,8 @@ bool ring_ok(int cfg, const LdDense<bf16_t, KCA>& la, const LdDense<bf16_t, KCB>
   if (M % rc.bm || N % rc.bn || kps % 64 || K % kps) return false;
   if (!la.vok || !lb.vok || !ep.vec_ok) return false;
   if ((ep.ldo & 7) || (ep.out2 && (ep.ldo2 & 7)) || (ep.aux && (ep.ldaux & 7))) return false;
-  if (ep.rowadd || ep.stats || ep.rs_ptr || ep.act == ACT_TANH || ep.mode == EPI_SPLIT2 || ep.mode == EPI_PATCH)
+  if (ep.rowadd || ep.stats || ep.rs_ptr || ep.act == ACT_TANH || ep.relu || ep.mode == EPI_SPLIT2 ||
+      ep.mode == EPI_PATCH)
     return false;
   auto al = [](const void* p) { return !p || (((uintptr_t)p) & 15) == 0; };
   if (!al(ep.out) || !al(ep.out2) || !al(ep.aux) || !al(ep.resid) || !al(ep.bias)) return false;

@@ -399,14 +399,29 @@ class ConvBNActFn(torch.autograd.Function):
         H, W = Hs * U, Ws * U
         dev = x1.device
         s = stream_ptr()
-        wp = pack_conv(w, 0, dt)
-        z = _empty((N, H, W, Cout), dt, dev)
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
         mean = torch.empty(Cout, dtype=torch.float32, device=dev)
         invstd = torch.empty_like(mean)
         P = N * H * W
         es = 4 if dt == F32 else 2
         cflops = 2.0 * P * Cout * Cin * KS * KS
+        if not training and pool == 1 and EVALFOLD and not any(ctx.needs_input_grad):
+            # eval, no backward: BatchNorm folded into the conv weights and bias, ReLU
+            # in the conv epilogue (Dropout2d is the identity): z is never stored
+            call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
+                 invstd.data_ptr(), s)
+            wf = _empty((w.numel(),), dt, dev)
+            bias = torch.empty(Cout, dtype=torch.float32, device=dev)
+            call("hvit_bn_fold", w.detach().contiguous().data_ptr(), Cout, Cin, KS, mean.data_ptr(),
+                 invstd.data_ptr(), gamma.detach().contiguous().data_ptr(), beta.detach().contiguous().data_ptr(),
+                 wf.data_ptr(), dt, bias.data_ptr(), s)
+            y = _empty((N, H, W, Cout), dt, dev)
+            with timed("conv_fwd", cflops):
+                call("hvit_conv_fwd", dt, g, wf.data_ptr(), bias.data_ptr(), y.data_ptr(), dt, None,
+                     epilogue(act=L.ACT_RELU), s)
+            return y
+        wp = pack_conv(w, 0, dt)
+        z = _empty((N, H, W, Cout), dt, dev)
         if training:
             tr = L.lib().hvit_conv_bn_tile_rows(C.byref(g))  # rows per BN partial tile
             nt = (P + tr - 1) // tr
@@ -472,6 +487,7 @@ class ConvBNActFn(torch.autograd.Function):
 
 
 C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path
+EVALFOLD = os.environ.get("HVIT_EVALFOLD", "1") != "0"  # A/B knob: 0 = eval convs keep z + bn_act
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
