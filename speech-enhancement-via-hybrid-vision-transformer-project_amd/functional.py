@@ -391,7 +391,7 @@ class ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x1, x2, w, gamma, beta, rmean, rvar, nbt, U, pool, training, drop: Drop, momentum, eps, dt,
-                sg: Optional[SkipGrad] = None):
+                sg: Optional[SkipGrad] = None, nograd: bool = False):
         N, Hs, Ws, C1 = x1.shape
         C2 = x2.shape[3] if x2 is not None else 0
         Cout, Cin, KS, _ = w.shape
@@ -405,8 +405,8 @@ class ConvBNActFn(torch.autograd.Function):
         P = N * H * W
         es = 4 if dt == F32 else 2
         cflops = 2.0 * P * Cout * Cin * KS * KS
-        if not training and pool == 1 and EVALFOLD and not any(ctx.needs_input_grad):
-            # eval, no backward: BatchNorm folded into the conv weights and bias, ReLU
+        if nograd and not training and pool == 1 and EVALFOLD:
+            # eval, no backward (the caller ran outside grad mode): BatchNorm folded into the conv weights and bias, ReLU
             # in the conv epilogue (Dropout2d is the identity): z is never stored
             call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
                  invstd.data_ptr(), s)
@@ -483,7 +483,7 @@ class ConvBNActFn(torch.autograd.Function):
                 dx2 = _empty((N, Hs, Ws, C2), dt, dev) if C2 else None
                 call("hvit_upsample_split_bwd", du.data_ptr(), dt, N, Hs, Ws, U, C1, C2, dx1.data_ptr(), dt,
                      ptr(dx2), dt, s)
-        return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 11
+        return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 12
 
 
 C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path

@@ -490,7 +490,8 @@ class HybridViT(nn.Module):
             bn = blk.bn
             x = HF.ConvBNActFn.apply(x, s, blk.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                      bn.num_batches_tracked, blk.up, 1, self.training,
-                                     HF.Drop(blk.p, 0, 500 + i, seed), bn.momentum, bn.eps, dt)
+                                     HF.Drop(blk.p, 0, 500 + i, seed), bn.momentum, bn.eps, dt, None,
+                                     not torch.is_grad_enabled())
         raise RuntimeError("hvit: decoder has no final layer")
 
     # -------------------------------------------------------- reference API --

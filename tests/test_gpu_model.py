@@ -243,17 +243,15 @@ def test_batch32_eval_forward_vs_oracle(hv):
     assert rel(yb, yo) < BF16_TOL
 
 
-# measured per-group bars of the B=32 bf16 step against the fp32 oracle
-# (relative L2 per parameter tensor; the bf16 step's worst tensor per group,
-# GPUTEST_r03 / gpurun_out logs, with ~2x headroom)
-BF16_STEP_BAR = {"transformer": 3e-2, "to_feature_map": 3e-2, "patch_embed": 3e-2, "pos_encoding": 3e-2,
-                 "encoder": 6e-2, "decoder": 6e-2, "skip_projections": 6e-2}
-
-
 def test_batch32_train_step_bf16_vs_oracle_grads(hv):
     """B=32 train step (BASELINE config 3 shapes, bf16, dropout off) against
     the fp32 CPU oracle: the loss, and EVERY parameter gradient per tensor
-    (relative L2) at the measured bf16 bar of its group (BF16_STEP_BAR)."""
+    (relative L2).  The bar is what bf16 arithmetic itself gives on this model:
+    the same oracle run by torch under bf16 autocast on the GPU (its own
+    rocBLAS / MIOpen kernels) is compared with the fp32 oracle the same way, and
+    each of our tensors must be within 2x of that error (+1e-2): ReLU / max-pool
+    routing flips and BatchNorm statistics in bf16 are inherent to the precision,
+    a wrong tile, swizzle or epilogue is not."""
     cfg = O.HViTConfig()
     cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
     shapes = O.state_dict_shapes(cfg)
@@ -264,6 +262,11 @@ def test_batch32_train_step_bf16_vs_oracle_grads(hv):
     lo_t = O.combined_loss(O.forward(sd, x, cfg, training=True), t)
     lo_t.backward()
     lo = lo_t.item()
+    # torch bf16 autocast of the same oracle (calibration of the bf16 error)
+    sdg = {k: v.detach().cuda().requires_grad_(v.requires_grad) for k, v in sd.items()}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = O.forward(sdg, x.cuda(), cfg, training=True)
+    O.combined_loss(yb.float(), t.cuda()).backward()
     m = build(hv, {}, "bf16", True).train()
     y = m(x.cuda())
     loss = hv.CombinedLoss()(y, t.cuda())
@@ -273,15 +276,16 @@ def test_batch32_train_step_bf16_vs_oracle_grads(hv):
     worst, bad = {}, []
     for k, p in m.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
-        got, ref = p.grad.detach().cpu(), sd[k].grad
+        got, ref, tb = p.grad.detach().cpu(), sd[k].grad, sdg[k].grad.detach().float().cpu()
         if k == "pos_encoding.pos_embed":
-            got, ref = got[:, :256], ref[:, :256]
-        e = relnorm(got, ref)
+            got, ref, tb = got[:, :256], ref[:, :256], tb[:, :256]
+        e, et = relnorm(got, ref), relnorm(tb, ref)
         grp = k.split(".")[0]
-        worst[grp] = max(worst.get(grp, (0.0, "")), (e, k))
-        if e > BF16_STEP_BAR[grp]:
-            bad.append((k, e))
-    print("bf16 B=32 step, worst rel-L2 per group:", {g: f"{v[0]:.2e} ({v[1]})" for g, v in worst.items()})
+        worst[grp] = max(worst.get(grp, (0.0, 0.0, "")), (e, et, k))
+        if e > 2 * et + 1e-2:
+            bad.append((k, round(e, 4), round(et, 4)))
+    print("bf16 B=32 step, worst rel-L2 per group (ours, torch bf16 autocast):",
+          {g: f"{v[0]:.2e} / {v[1]:.2e} ({v[2]})" for g, v in worst.items()})
     assert not bad, bad
 
 
