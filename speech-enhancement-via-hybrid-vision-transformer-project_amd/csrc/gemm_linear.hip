@@ -45,12 +45,19 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
   });
 }
 
+bool hvit_wgrad_small_ok(int dt, int M, int N, int K);  // wgrad_small.hip
+long long hvit_wgrad_small_ws(int M, int N, int K);
+int hvit_wgrad_small(const void* dy, const void* x, int M, int N, int K, float* dw, float* db, float* ws,
+                     long long ws_elems, void* stream);
+
 extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
   // dw is [N_out x K_in] reduced over M rows; slabs only when splitting, each
   // slab followed by N_out bias partials (enough for every tile configuration
-  // the entry point may pick: gemm.h's 128x128, the ring's 128x128 / 128x64)
+  // the entry point may pick: gemm.h's 128x128, the ring's 128x128 / 128x64,
+  // the tall-skinny kernel of wgrad_small.hip)
   int s = std::max(wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN), wgrad_splits(N, K, M, 128, 64));
-  return s > 1 ? (long long)s * ((long long)N * K + N) : 0;
+  const long long g = s > 1 ? (long long)s * ((long long)N * K + N) : 0;
+  return std::max(g, hvit_wgrad_small_ok(HVIT_BF16, M, N, K) ? hvit_wgrad_small_ws(M, N, K) : 0LL);
 }
 
 // per-tile arrival counters of the in-kernel split-K reduction (ring kernels;
@@ -93,6 +100,12 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
     if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return HVIT_OK;
   }
+  // tall-skinny shapes (head, skip projections): one 64x64 tile per workgroup
+  // over a chunk of rows; HVIT_WGRAD_SMALL=0 disables (A/B only)
+  static const bool small_on = !getenv("HVIT_WGRAD_SMALL") || atoi(getenv("HVIT_WGRAD_SMALL"));
+  if (small_on && !tickets && hvit_wgrad_small_ok(dt, M, N, K) && (!db || db == dw + NK) &&
+      ws_elems >= hvit_wgrad_small_ws(M, N, K))
+    return hvit_wgrad_small(dy, x, M, N, K, dw, db, ws, ws_elems, stream);
   // HVIT_NO_RS=1: bias grad by a separate column reduction (A/B measurements only)
   static const bool no_rs = getenv("HVIT_NO_RS") && atoi(getenv("HVIT_NO_RS"));
   const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK && !no_rs;

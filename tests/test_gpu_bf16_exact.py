@@ -170,6 +170,21 @@ def test_linear_wgrad_exact(env, cfg, N, K):
     assert int(tk.count_nonzero()) == 0
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 256, 512), (8192, 256, 256), (32768, 128, 128), (131072, 64, 64),
+                                   (1000, 64, 128)])
+def test_linear_wgrad_small_with_bias_exact(env, M, N, K):
+    """The tall-skinny weight gradients of the step (head, skip projections:
+    csrc/wgrad_small.hip) with the bias gradient, element-wise."""
+    L, HF = env
+    torch.manual_seed(5)
+    dy, x = rb(M, N), rb(M, K)
+    dw, db = HF.linear_wgrad(L.BF16, dy, x, M, N, K, bias=True)
+    check_f32(dw, dy.float().t() @ x.float(), what=f"small wgrad {M}x{N}x{K}")
+    check_f32(db, dy.float().sum(0), what=f"small wgrad bias {M}x{N}x{K}")
+    dw2 = HF.linear_wgrad(L.BF16, dy, x, M, N, K)
+    check_f32(dw2, dy.float().t() @ x.float(), what=f"small wgrad (no bias) {M}x{N}x{K}")
+
+
 CONV_PROD = [
     # N, Hs, Ws, C1, C2, U, Cout: the model's LDS-DMA implicit-im2col shape classes
     (4, 128, 128, 64, 0, 1, 128),   # enc1

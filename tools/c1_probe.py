@@ -59,9 +59,10 @@ for name, fn in (("stats", stats), ("fwd", fwd), ("bwd", bwd)):
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        fn()
+        for _ in range(10):  # back-to-back: host launch latency off the measured span
+            fn()
         e1.record()
         torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.append(e0.elapsed_time(e1) * 1e3 / 10)
     ts.sort()
     print(f"{name:6s} median {ts[len(ts) // 2]:8.1f} us  min {ts[0]:8.1f} us", flush=True)

@@ -29,10 +29,11 @@ for name, M, N, K in SHAPES:
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        HF.linear_wgrad(L.BF16, dy, x, M, N, K, bias=True)
+        for _ in range(10):  # back-to-back: host launch latency off the measured span
+            HF.linear_wgrad(L.BF16, dy, x, M, N, K, bias=True)
         e1.record()
         torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.append(e0.elapsed_time(e1) * 1e3 / 10)
     ts.sort()
     print(f"{name:6s} M={M:6d} N={N:3d} K={K:3d}  median {ts[reps // 2]:6.1f} us  min {ts[0]:6.1f} us  "
           f"err dw {err:.1e} db {errb:.1e}", flush=True)
