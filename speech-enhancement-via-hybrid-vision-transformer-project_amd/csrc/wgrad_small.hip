@@ -6,11 +6,11 @@
 // loaded byte at N = K = 64) that the tiled GEMM covered with one or four
 // output tiles and hundreds of short split-K slices.
 //
-// Here a workgroup owns one 64x64 output tile and a contiguous chunk of rows
-// (about two workgroups per CU over the whole grid): it streams 64-row stages
-// of both operands (16-byte loads of whole 128-byte row segments, next stage
-// prefetched into registers during the current one's MFMAs) through LDS, each
-// wave accumulating a 32x32 sub-tile with v_mfma_f32_16x16x32_bf16.  Operand
+// Here a workgroup owns one 64x64 output tile and 256 rows: it requests all
+// four 64-row stages of both operands at once (16-byte loads of whole 128-byte
+// row segments into registers: one memory latency per workgroup), then passes
+// them through LDS stage by stage, each wave accumulating a 32x32 sub-tile
+// with v_mfma_f32_16x16x32_bf16.  Operand
 // fragments are gathered from the [m][n] / [m][k] LDS images column-wise
 // (k of the MFMA = m).  The k = 0 tile column also sums its dy fragments for
 // the bias gradient.  Each workgroup writes an f32 slab [dW | db]; one
@@ -22,6 +22,7 @@
 namespace hvit_ws {
 
 constexpr int TM = 64;      // rows (m) per stage
+constexpr int NS = 4;       // stages per workgroup, all loaded up front
 constexpr int TILE = 64;    // output tile edge
 constexpr int PITCH = 72;   // LDS row pitch (bf16): 144 B rows spread the column gathers over banks
 
@@ -48,29 +49,24 @@ __global__ __launch_bounds__(256, 2) void wgrad_small_kernel(const bf16_t* __res
   const int n0 = (blockIdx.x / tiles_k) * TILE, k0 = (blockIdx.x % tiles_k) * TILE;
   const int m_begin = blockIdx.y * rows_per_wg, m_end = min(M, m_begin + rows_per_wg);
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
-  // loader: thread -> (row, 8-column group) of a 64x64 stage, two passes of 32 rows
+  // loader: thread -> (row, 8-column group) of a 64x64 stage, two passes of 32
+  // rows; all NS stages of the workgroup's rows are requested before the first
+  // is used (one memory latency per workgroup, not one per stage)
   const int lr = tid >> 3, lc = (tid & 7) * 8;
-  u32x4 ra[2], rb[2];
-  auto load = [&](int m0) {
+  u32x4 ra[NS][2], rb[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      const int m = m0 + lr + 32 * p;
+      const int m = m_begin + s * TM + lr + 32 * p;
       const bool ok = m < m_end;
       const long mm = ok ? m : m_begin;
       const u32x4 va = *(const u32x4*)(dy + mm * N + n0 + lc);
       const u32x4 vb = *(const u32x4*)(x + mm * K + k0 + lc);
       const u32x4 z = {0u, 0u, 0u, 0u};
-      ra[p] = ok ? va : z;
-      rb[p] = ok ? vb : z;
+      ra[s][p] = ok ? va : z;
+      rb[s][p] = ok ? vb : z;
     }
-  };
-  auto stash = [&]() {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      *(u32x4*)(sa + (lr + 32 * p) * PITCH + lc) = ra[p];
-      *(u32x4*)(sb + (lr + 32 * p) * PITCH + lc) = rb[p];
-    }
-  };
   // wave sub-tile: n rows [nb, nb + 32), k columns [kb, kb + 32)
   const int nb = 32 * (wv >> 1), kb = 32 * (wv & 1);
   const bool do_db = with_db && k0 == 0 && (wv & 1) == 0;
@@ -80,12 +76,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_small_kernel(const bf16_t* __res
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs[2] = {0.f, 0.f};
-  load(m_begin);
-  for (int m0 = m_begin; m0 < m_end; m0 += TM) {
-    __syncthreads();  // the previous stage's fragments are read
-    stash();
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (m_begin + s * TM >= m_end) break;  // uniform
+    if (s > 0) __syncthreads();  // the previous stage's fragments are read
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      *(u32x4*)(sa + (lr + 32 * p) * PITCH + lc) = ra[s][p];
+      *(u32x4*)(sb + (lr + 32 * p) * PITCH + lc) = rb[s][p];
+    }
     __syncthreads();
-    if (m0 + TM < m_end) load(m0 + TM);  // next stage in flight during this one's MFMAs
 #pragma unroll
     for (int ks = 0; ks < TM / 32; ++ks) {
       const int r0 = ks * 32 + 8 * (l >> 4);
@@ -129,15 +129,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_small_kernel(const bf16_t* __res
   }
 }
 
-// rows per workgroup (a multiple of the stage) and the split count: about 512
-// workgroups over the output tiles, at least 4 stages each
+// NS stages of rows per workgroup; the split count follows
 inline void plan(int M, int N, int K, int& rows, int& splits) {
-  const int tiles = (N / TILE) * (K / TILE);
-  long want = (512 + tiles - 1) / tiles;
-  long r = (M + want - 1) / want;
-  r = std::max<long>(4 * TM, (r + TM - 1) / TM * TM);
-  rows = (int)r;
-  splits = (int)((M + r - 1) / r);
+  (void)N;
+  (void)K;
+  rows = NS * TM;
+  splits = (M + rows - 1) / rows;
 }
 
 }  // namespace hvit_ws
@@ -146,7 +143,8 @@ using namespace hvit_ws;
 
 // applicable shapes: bf16, N and K multiples of 64, small output, tall M
 bool hvit_wgrad_small_ok(int dt, int M, int N, int K) {
-  return dt == HVIT_BF16 && N % TILE == 0 && K % TILE == 0 && (long)N * K <= 256L * 512 && M >= 8 * TM;
+  return dt == HVIT_BF16 && N % TILE == 0 && K % TILE == 0 && (long)N * K <= 256L * 512 && M >= 8 * TM &&
+         M <= 4096L * NS * TM;
 }
 
 long long hvit_wgrad_small_ws(int M, int N, int K) {
