@@ -156,7 +156,18 @@ def lib():
     return _lib
 
 
+# Measurement hook (functional.py installs it): times a C-ABI call that no
+# explicit op class covers, under the class "abi:<entry point>"
+TIMER = None
+
+
 def call(name, *args):
+    if TIMER is not None:
+        return TIMER(name, lambda: _call(name, *args))
+    return _call(name, *args)
+
+
+def _call(name, *args):
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().hvit_last_error().decode(errors="replace")

@@ -183,7 +183,11 @@ class FusedAdamW(torch.optim.Optimizer):
                                            p.numel(), st["step"].data_ptr() if step is None else None)
                 bc1, bc2 = (1.0, 1.0) if step is None else (1.0 - b1 ** step, 1.0 - b2 ** step)
                 hp = L.AdamWHyper(float(group["lr"]), b1, b2, group["eps"], group["weight_decay"], bc1, bc2)
-                L.call("hvit_adamw", len(ps), items, hp, coef.data_ptr() if coef is not None else None, stream)
+                # read p, g, m, v f32, write p, m, v f32 (+ the bf16 shadow)
+                nbytes = (float(sum(p.numel() * (28 + (2 if HF.shadow_of(p) is not None else 0)) for p in ps))
+                          if HF.OP_TIMES is not None else 0.0)
+                with HF.timed("adamw", nbytes):
+                    L.call("hvit_adamw", len(ps), items, hp, coef.data_ptr() if coef is not None else None, stream)
                 for p in ps:
                     if _bump is not None:
                         _bump(p)  # the kernel wrote p in place: keep version counters honest
