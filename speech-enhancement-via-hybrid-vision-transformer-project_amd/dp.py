@@ -9,11 +9,15 @@ over xGMI; gloo works for CPU tests and for ranks that share one GPU.
   is roughly the order backward produces them.  A bucket's all-reduce is
   launched from a post-accumulate-grad hook as soon as its last gradient lands,
   so communication overlaps the rest of the backward.
-* Every bucket owns two persistent flat buffers used on alternate steps.
-  Gradients are copied into the step's buffer once (the launch), and after the
-  reduction each parameter's ``.grad`` becomes a view of the averaged buffer:
-  no per-step concatenation buffer and no copy-back.  Alternating keeps a
-  launch from ever reducing in place under a ``.grad`` view that a later
+* Every bucket owns two persistent flat buffers used on alternate steps.  The
+  next step's buffer is published before its backward (functional.GRAD_DEST):
+  the ViT linear and conv weight-gradient launches write their result straight
+  into the parameter's slot, autograd adopts that view as ``.grad`` and the
+  bucket launch finds it in place (no copy).  Other gradients (biases, norms,
+  and any gradient accumulated onto an existing ``.grad``) are copied into the
+  buffer at the launch.  After the reduction each ``.grad`` is a view of the
+  averaged buffer: no concatenation buffer and no copy-back.  Alternating keeps
+  a launch from ever reducing in place under a ``.grad`` view that a later
   accumulating backward still writes (``zero_grad(set_to_none=False)``).
 * Gradient accumulation (trainer.py:72, :164-183: several backward passes
   before one optimizer step) is exact: a bucket whose gradients change after
@@ -37,8 +41,12 @@ from __future__ import annotations
 import contextlib
 from typing import Dict, List, Optional
 
+import weakref
+
 import torch
 import torch.distributed as dist
+
+from . import functional as HF
 
 
 class GradAllReducer:
@@ -83,6 +91,19 @@ class GradAllReducer:
         self.broadcast_buffers = broadcast_buffers
         self._max_tokens = 0
         self.reset()
+        self._publish()
+
+    def _publish(self):
+        """Allocate this generation's flat buffers and announce each unsliced
+        parameter's slot in them to the weight-gradient launches."""
+        for b, ps in enumerate(self.buckets):
+            offs, total = self.offsets[b]
+            flat = self.flats[b][self._gen]
+            if flat is None or flat.device != ps[0].device:
+                flat = self.flats[b][self._gen] = torch.empty(total, dtype=torch.float32, device=ps[0].device)
+            for p, o in zip(ps, offs):
+                if self._rows(p) is None:
+                    HF.GRAD_DEST[id(p)] = (weakref.ref(p), flat, o)
 
     # ------------------------------------------------------------ helpers --
     def _rows(self, p):
@@ -204,11 +225,16 @@ class GradAllReducer:
         self._max_tokens = 0
         self._gen ^= 1
         self.reset()
+        self._publish()
 
     def remove(self):
         for h in self._hooks:
             h.remove()
         self._fwd_hook.remove()
+        for p in self.params:
+            e = HF.GRAD_DEST.get(id(p))
+            if e is not None and e[0]() is p:
+                del HF.GRAD_DEST[id(p)]
 
 
 def broadcast_module(model: torch.nn.Module, src: int = 0, group=None):

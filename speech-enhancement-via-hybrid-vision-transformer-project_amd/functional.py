@@ -243,9 +243,31 @@ def pack_conv(w: torch.Tensor, mode: int, dt: int) -> torch.Tensor:
     return out
 
 
-def unpack_conv(dwp: torch.Tensor, shape) -> torch.Tensor:
+# Data-parallel gradient slots (dp.GradAllReducer): id(param) -> (weakref(param),
+# flat bucket buffer, offset).  A weight-gradient launch whose parameter has a
+# slot (and no .grad yet) writes straight into it; autograd then adopts that
+# view as .grad and the bucket's all-reduce copies nothing.
+GRAD_DEST = {}
+
+
+def grad_dest(pid, shape):
+    """The bucket view for parameter ``pid``'s gradient, or None (no slot, or
+    the parameter already holds a gradient that a second backward accumulates
+    into)."""
+    e = GRAD_DEST.get(pid)
+    if e is None:
+        return None
+    ref, flat, o = e
+    p = ref()
+    n = math.prod(shape)
+    if p is None or p.grad is not None or tuple(p.shape) != tuple(shape) or flat.numel() < o + n:
+        return None
+    return flat[o:o + n].view(shape)  # a fresh view each time: autograd can adopt it without a copy
+
+
+def unpack_conv(dwp: torch.Tensor, shape, out=None) -> torch.Tensor:
     co, ci, ks, _ = shape
-    dw = torch.empty(shape, dtype=torch.float32, device=dwp.device)
+    dw = out if out is not None else torch.empty(shape, dtype=torch.float32, device=dwp.device)
     call("hvit_conv_weight_unpack", dwp.data_ptr(), co, ci, ks, dw.data_ptr(), stream_ptr())
     return dw
 
@@ -261,15 +283,18 @@ def wgrad_tickets(M, N, K) -> int:
     return int(L.lib().hvit_wgrad_tickets(M, N, K))
 
 
-def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=None):
+def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=None, dest=None):
     """dw [N, K] = dy^T x (f32); with ``bias`` also db [N] = colsum(dy), which
     the bf16 path fuses into the GEMM (db stored right after dw).  ``tickets``
     (a zeroed f32 tensor of at least wgrad_tickets(M, N, K) elements, e.g. a
     slice of the forward's zero pool): the split-K partials are reduced inside
     the GEMM launch (no second launch, no slab re-read pass)."""
-    buf = torch.empty(N * K + (N if bias else 0), dtype=torch.float32, device=dy.device)
-    dw = buf[:N * K].view(N, K)
-    db = buf[N * K:] if bias else None
+    if dest is not None and not bias:  # the parameter's data-parallel bucket slot (grad_dest)
+        dw, db = dest.view(N, K), None
+    else:
+        buf = torch.empty(N * K + (N if bias else 0), dtype=torch.float32, device=dy.device)
+        dw = buf[:N * K].view(N, K)
+        db = buf[N * K:] if bias else None
     ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
 
@@ -321,7 +346,7 @@ def geom(src1, C1, src2, C2, N, Hs, Ws, U, KS, stride, pad, Cout) -> L.ConvGeom:
     return L.ConvGeom(ptr(src1), C1, ptr(src2), C2, N, Hs, Ws, U, KS, stride, pad, Cout)
 
 
-def conv_wgrad(dt, g: L.ConvGeom, dz, wshape) -> torch.Tensor:
+def conv_wgrad(dt, g: L.ConvGeom, dz, wshape, dest=None) -> torch.Tensor:
     co, ci, ks, _ = wshape
     dwp = torch.empty(co * ci * ks * ks, dtype=torch.float32, device=dz.device)
     ws_n = L.lib().hvit_conv_wgrad_workspace(g)
@@ -334,7 +359,7 @@ def conv_wgrad(dt, g: L.ConvGeom, dz, wshape) -> torch.Tensor:
     with timed("conv_wgrad", 2.0 * P * co * ci * ks * ks):
         launch()
     _record("conv_wgrad", (launch, 2.0 * P * co * ci * ks * ks))
-    return unpack_conv(dwp, wshape)
+    return unpack_conv(dwp, wshape, dest)
 
 
 @dataclass
@@ -462,6 +487,7 @@ class ConvBNActFn(torch.autograd.Function):
             call("hvit_bn_act_fwd", dt, z.data_ptr(), N, H, W, Cout, mean.data_ptr(), invstd.data_ptr(),
                  gamma.data_ptr(), beta.data_ptr(), dr, pool, y.data_ptr(), dt, s)
         ctx.save_for_backward(x1, x2, w, gamma, beta)
+        ctx.wid = (id(w), tuple(w.shape))
         ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
         ctx.meta = (U, pool, training, dr, dt)
         ctx.sg = sg
@@ -488,7 +514,7 @@ class ConvBNActFn(torch.autograd.Function):
                  dz.data_ptr(), dt, sums.data_ptr(), L.ACC_ZEROED, s)
         dbeta, dgamma = sums[:Cout], sums[Cout:2 * Cout]
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
-        dw = conv_wgrad(dt, g, dz, w.shape)
+        dw = conv_wgrad(dt, g, dz, w.shape, grad_dest(*ctx.wid))
         dx1 = dx2 = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             wd = pack_conv(w, 1, dt)
@@ -614,6 +640,7 @@ class PatchEmbedFn(torch.autograd.Function):
         e = epilogue(drop=dr, rowadd=pos, rowadd_rows=Nt)
         call("hvit_conv_fwd", dt, g, wp.data_ptr(), b.data_ptr(), x0.data_ptr(), F32, None, e, s)
         ctx.save_for_backward(feat, w)
+        ctx.wid = (id(w), tuple(w.shape))
         ctx.wp = wp
         ctx.meta = (Pp, dr, dt, Nt, None if pos is None else pos.shape)
         ctx.sg = sg
@@ -638,7 +665,7 @@ class PatchEmbedFn(torch.autograd.Function):
             dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
             call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
         g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
-        dw = conv_wgrad(dt, g, gd, w.shape)
+        dw = conv_wgrad(dt, g, gd, w.shape, grad_dest(*ctx.wid))
         dfeat = None
         if ctx.needs_input_grad[0]:
             dfeat = _empty(feat.shape, dt, dev)
@@ -782,6 +809,7 @@ class ViTBlockFn(torch.autograd.Function):
             call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid, x2.data_ptr(), F32,
                  epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
         ctx.save_for_backward(n1w, n2w)
+        ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, gh, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
         # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
@@ -807,13 +835,14 @@ class ViTBlockFn(torch.autograd.Function):
         g2 = _empty((M, D), dt, dev)
         df2b = zf2b.take(dev)
         dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
-        df2w = linear_wgrad(dt, g2, a, M, D, hid, tag="vit_linear_wgrad")
+        dq_id, dp_id, d1_id, d2_id = ctx.wid
+        df2w = linear_wgrad(dt, g2, a, M, D, hid, tag="vit_linear_wgrad", dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
         df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
         with timed("vit_linear_dgrad", 2.0 * M * D * hid):
             call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
                  epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b), s)
-        df1w = linear_wgrad(dt, dh, xn2, M, hid, D, tag="vit_linear_wgrad")
+        df1w = linear_wgrad(dt, dh, xn2, M, hid, D, tag="vit_linear_wgrad", dest=grad_dest(*d1_id))
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_dgrad", 2.0 * M * hid * D):
             call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
@@ -822,7 +851,7 @@ class ViTBlockFn(torch.autograd.Function):
         g1 = _empty((M, D), dt, dev)
         dpb = zpb.take(dev)
         dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
-        dpw = linear_wgrad(dt, g1, o, M, D, D, tag="vit_linear_wgrad")
+        dpw = linear_wgrad(dt, g1, o, M, D, D, tag="vit_linear_wgrad", dest=grad_dest(*dp_id))
         do = _empty((M, D), dt, dev)
         with timed("vit_linear_dgrad", 2.0 * M * D * D):
             call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
@@ -833,7 +862,7 @@ class ViTBlockFn(torch.autograd.Function):
                  scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
         # qkv bias grad by a column reduction: the wgrad GEMM variant with fused
         # A-row sums spills at 128x128 (rocprof: 42 -> 28 us class without it)
-        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, tag="vit_linear_wgrad")
+        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, tag="vit_linear_wgrad", dest=grad_dest(*dq_id))
         dqkvb = zqb.take(dev)
         call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)

@@ -58,6 +58,14 @@ def _worker(rank, world, port, q):
         red = dp.GradAllReducer(model, bucket_mb=0.05, sliced={"pos_encoding.pos_embed": 320})
         sl = slice(rank * SHAPE[0], (rank + 1) * SHAPE[0])
         crit(model(x[sl].cuda()), t[sl].cuda()).backward()
+        # the ViT and conv weight gradients were written into their bucket slots
+        # (functional.GRAD_DEST): .grad already lives in the flat buffer
+        def in_bucket(p):
+            flat = red.flats[red.where[id(p)]][red._gen]
+            return p.grad.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
+        adopted = all(in_bucket(p) for p in (model.transformer.blocks[0].attn.qkv.weight,
+                                             model.transformer.blocks[-1].mlp.net[3].weight,
+                                             model.encoder[1].block[0].weight))
         red.finish()
         ntok = model.last_num_tokens
         # single-process reference: mean of the per-shard gradients (local BN per shard)
@@ -85,7 +93,7 @@ def _worker(rank, world, port, q):
             opt.step()
             opt.zero_grad(set_to_none=True)
         csum = torch.stack([p.detach().double().sum() for p in model.parameters()]).cpu()
-        q.put((rank, err, pos_tail, beyond, ntok, torch.equal(bn, bn0), csum))
+        q.put((rank, err, pos_tail, beyond, ntok, torch.equal(bn, bn0), csum, adopted))
     finally:
         dist.destroy_process_group()
 
@@ -102,7 +110,8 @@ def test_dp_hybridvit_two_ranks_on_one_gpu():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, err, pos_tail, beyond, ntok, bn_same, _ in out:
+    for rank, err, pos_tail, beyond, ntok, bn_same, _, adopted in out:
+        assert adopted             # weight gradients written in place in the bucket (no launch copy)
         assert ntok == 260
         assert err < 1e-5, (rank, err)
         assert pos_tail > 0.0      # rows 256..259 carry gradient and were reduced
