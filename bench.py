@@ -171,8 +171,11 @@ def cpu_baseline(batch, budget_s):
     from oracle import closed_form as CF
     from oracle import hvit_oracle as O
 
-    # every core this process may run on; OMP_NUM_THREADS caps it if set
+    # every core this process may run on, capped by OMP_NUM_THREADS when the
+    # host sets it (the GPU box's CPU share: its affinity mask can name the whole machine)
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit() and int(os.environ["OMP_NUM_THREADS"]) > 0:
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     if os.environ.get("HVIT_CPU_THREADS"):
         cores = int(os.environ["HVIT_CPU_THREADS"])
     torch.set_num_threads(cores)
@@ -191,13 +194,16 @@ def cpu_baseline(batch, budget_s):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
+    t1 = time.perf_counter()
     step()  # warmup
+    print(f"cpu baseline: warmup step {time.perf_counter() - t1:.1f} s on {cores} threads", file=sys.stderr, flush=True)
     times = []
     t0 = time.perf_counter()
     while len(times) < 3 and (time.perf_counter() - t0) < budget_s:
         t1 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t1)
+        print(f"cpu baseline: step {len(times)} {times[-1]:.1f} s", file=sys.stderr, flush=True)
     times.sort()
     dt = times[len(times) // 2]
     return {"value": round(batch * FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": torch.get_num_threads(),

@@ -92,7 +92,9 @@ def _worker(rank, world, port, q):
             red.finish()
             opt.step()
             opt.zero_grad(set_to_none=True)
-        csum = torch.stack([p.detach().double().sum() for p in model.parameters()]).cpu()
+        # plain floats: a tensor in the queue is shared by file descriptor, which
+        # the parent can only open while this process is still alive
+        csum = torch.stack([p.detach().double().sum() for p in model.parameters()]).cpu().tolist()
         q.put((rank, err, pos_tail, beyond, ntok, torch.equal(bn, bn0), csum, adopted))
     finally:
         dist.destroy_process_group()
@@ -117,7 +119,7 @@ def test_dp_hybridvit_two_ranks_on_one_gpu():
         assert pos_tail > 0.0      # rows 256..259 carry gradient and were reduced
         assert beyond == 0.0
         assert bn_same             # rank 0's running statistics on every rank
-    assert torch.equal(out[0][6], out[1][6])  # bit-identical replicas after 3 optimizer steps
+    assert out[0][6] == out[1][6]  # bit-identical replicas after 3 optimizer steps
 
 
 def test_rccl_world1_bench_dp_branch():
