@@ -163,6 +163,17 @@ int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int hd, float sc
                   const hvit_dropout_t* dropout, void* o, float* lse, float* probs, void* stream);
 int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
                   int hd, float scale, const hvit_dropout_t* dropout, void* dqkv, float* delta_ws, void* stream);
+/* The same with the attention-dropout decisions kept: the forward writes one
+ * bit per (query, key) to keep_bits (hvit_mhsa_keep_bits_elems(B, N, H) 32-bit
+ * words, 16-byte aligned) and the backward reads them instead of regenerating
+ * the mask (bf16, head_dim 64, N <= 256, N % 4 == 0; other shapes and p = 0
+ * ignore keep_bits).  Results equal hvit_mhsa_fwd / hvit_mhsa_bwd. */
+long long hvit_mhsa_keep_bits_elems(int B, int N, int H);
+int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
+                     void* o, float* lse, unsigned* keep_bits, void* stream);
+int hvit_mhsa_bwd_kb(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
+                     int hd, float scale, const hvit_dropout_t* dropout, const unsigned* keep_bits, void* dqkv,
+                     float* delta_ws, void* stream);
 /* fp8 (OCP e4m3) forward of the same core for BASELINE config 5: bf16 qkv / o,
  * per-(b, h) power-of-two scales for K and V and per-query scales for Q
  * (e4m3 range from the absolute maxima), QK^T on v_mfma_f32_16x16x32_fp8_fp8,

@@ -586,7 +586,7 @@ template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int N, int H, float scale,
                                                          uint32_t thr, float dscale, DSeed seed_,
-                                                         uint32_t site) {
+                                                         uint32_t site, uint32_t* __restrict__ kbits) {
   const unsigned long long seed = seed_;
   __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
   char* Ks = smem;
@@ -653,14 +653,27 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   f32x4 ot[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // keep bits for the backward (kbits non-null): bit 8*jp + 4*e + r of this
+  // lane's word pair = keep(q, key 32*jp + 16*e + 4*fq + r)
+  uint32_t kb[2] = {0u, 0u};
 #pragma unroll
   for (int jp = 0; jp < V2_KMAX / 32; ++jp) {
     if (2 * jp < nkt) {
       f32x4 p0 = st[2 * jp] * inv;
       f32x4 p1 = (2 * jp + 1 < nkt) ? st[2 * jp + 1] * inv : (f32x4){0.f, 0.f, 0.f, 0.f};
       if (thr) {
-        p0 *= v2_keep(bh, N, q < N ? q : 0, 32 * jp + 4 * fq, thr, dscale, seed, site);
-        if (2 * jp + 1 < nkt) p1 *= v2_keep(bh, N, q < N ? q : 0, 32 * jp + 16 + 4 * fq, thr, dscale, seed, site);
+        const f32x4 k0 = v2_keep(bh, N, q < N ? q : 0, 32 * jp + 4 * fq, thr, dscale, seed, site);
+        p0 *= k0;
+        uint32_t b8 = 0u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b8 |= (k0[r] != 0.f ? 1u : 0u) << r;
+        if (2 * jp + 1 < nkt) {
+          const f32x4 k1 = v2_keep(bh, N, q < N ? q : 0, 32 * jp + 16 + 4 * fq, thr, dscale, seed, site);
+          p1 *= k1;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) b8 |= (k1[r] != 0.f ? 1u : 0u) << (4 + r);
+        }
+        kb[jp >> 2] |= b8 << (8 * (jp & 3));
       }
       const u32x4 pb = v2_cat(v2_pack(p0), v2_pack(p1));
 #pragma unroll
@@ -677,6 +690,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
       *(uint2*)(op + 16 * t + 4 * fq) = u;
     }
     if (fq == 0) lse[bh * N + q] = (mx + log2f(sum)) * 0.6931471805599453f;
+    if (kbits && thr) *(uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2) = make_uint2(kb[0], kb[1]);
   }
 }
 
@@ -688,7 +702,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
                                                         const float* __restrict__ lse, float* __restrict__ delta,
                                                         bf16_t* __restrict__ dqkv, int N, int H, float scale,
                                                         uint32_t thr, float dscale, DSeed seed_,
-                                                        uint32_t site) {
+                                                        uint32_t site, const uint32_t* __restrict__ kbits) {
   const unsigned long long seed = seed_;
   __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
   char* Ks = smem;
@@ -724,6 +738,12 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
   dl += __shfl_xor(dl, 32, 64);
   if (qv && fq == 0) delta[bh * N + q] = dl;
   const float lse2 = qv ? lse[bh * N + q] * 1.4426950408889634f : 0.f;
+  // the forward's keep bits of this lane's (query, key quad) positions (mhsa_fwd_v2)
+  unsigned long long kb64 = 0ull;
+  if (kbits && thr && qv) {
+    const uint2 w2 = *(const uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2);
+    kb64 = (unsigned long long)w2.x | ((unsigned long long)w2.y << 32);
+  }
   const int NK32 = (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite, P = 0)
   v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK32);
   v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK32);
@@ -744,9 +764,14 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
       s = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], s);
       dp = v2_mma32(v2_fragj(Vs, LN, j, 0), df[0], dp);
       dp = v2_mma32(v2_fragj(Vs, LN, j, 1), df[1], dp);
-      const f32x4 keep = thr ? v2_keep(bh, N, qv ? q : 0, (16 * j + 4 * fq) < N ? 16 * j + 4 * fq : 0, thr,
-                                       dscale, seed, site)
-                             : (f32x4){1.f, 1.f, 1.f, 1.f};
+      f32x4 keep = {1.f, 1.f, 1.f, 1.f};
+      if (thr && kbits) {
+        const uint32_t b4 = (uint32_t)(kb64 >> (8 * (j >> 1) + 4 * (j & 1))) & 0xFu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) keep[r] = (b4 >> r) & 1u ? dscale : 0.f;
+      } else if (thr) {
+        keep = v2_keep(bh, N, qv ? q : 0, (16 * j + 4 * fq) < N ? 16 * j + 4 * fq : 0, thr, dscale, seed, site);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool valid = qv && (16 * j + 4 * fq + r < N);
@@ -778,13 +803,15 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
                                                          const float* __restrict__ lse,
                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                          int N, int H, float scale, uint32_t thr, float dscale,
-                                                         DSeed seed_, uint32_t site) {
+                                                         DSeed seed_, uint32_t site,
+                                                         const uint32_t* __restrict__ kbits) {
   const unsigned long long seed = seed_;
-  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4 + V2_KMAX * 32];
   char* Qs = smem;
   char* Ds = smem + V2_KMAX * V2_ROWB;
   float* Ls = (float*)(smem + 2 * V2_KMAX * V2_ROWB);
   float* Dl = Ls + V2_KMAX;
+  uint32_t* Kb = (uint32_t*)(Dl + V2_KMAX);  // the forward's keep bits of this (b, h): [query][fq][2]
   const int D = H * 64;
   const long pitch = 3L * D;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -810,6 +837,13 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
     Ls[i] = i < N ? lse[bh * N + i] * 1.4426950408889634f : 0.f;
     Dl[i] = i < N ? delta[bh * N + i] : 0.f;
   }
+  const bool use_kb = kbits && thr;
+  if (use_kb)
+    for (int i = threadIdx.x; i < N * 2; i += WAVES * 64)
+      ((u32x4*)Kb)[i] = ((const u32x4*)(kbits + bh * N * 8))[i];
+  // this lane's key inside a query's bit pair: word fq' * 2 + half, bit position
+  const int kbit = 8 * (key >> 5) + 4 * ((key >> 4) & 1) + (key & 3);
+  const int kword = ((key >> 2) & 3) * 2 + (kbit >> 5), kshift = kbit & 31;
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
   // accumulators: rows = d (16t + 4fq + r), column = this lane's key
@@ -832,7 +866,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
       // its key group (two pair hashes); the quad exchanges the 16-bit slices
       // (4 queries x 4 keys)
       uint32_t hlo = 0u, hhi = 0u;
-      if (thr) {
+      if (thr && !use_kb) {
         const int qc = 16 * j + 4 * fq + (frow & 3);
         const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
         const uint32_t rk = rng_key(seed, site);
@@ -845,7 +879,9 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
         const bool valid = kv && qi < N;
         const float p = valid ? __builtin_amdgcn_exp2f(s[r] * c2 - Ls[qi]) : 0.f;
         float kp = 1.f;
-        if (thr) {
+        if (use_kb) {
+          kp = (valid && ((Kb[(qi < N ? qi : 0) * 8 + kword] >> kshift) & 1u)) ? dscale : 0.f;
+        } else if (thr) {
           const int src = (lane & ~3) | r;
           const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
           const uint32_t word = (key & 2) ? hi : lo;
@@ -949,9 +985,9 @@ static int mhsa_bwd_t(const void* qkv, const void* o, const void* dout, const fl
 
 using namespace hvit;
 
-extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
-                             const hvit_dropout_t* dropout, void* o, float* lse, float* probs,
-                             void* stream) {
+static int mhsa_fwd_impl(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
+                         const hvit_dropout_t* dropout, void* o, float* lse, float* probs, uint32_t* keep_bits,
+                         void* stream) {
   HVIT_CHECK(qkv && o && lse, "hvit_mhsa_fwd: null pointer");
   HVIT_CHECK(B > 0 && N > 0 && H > 0, "hvit_mhsa_fwd: bad shape B=%d N=%d H=%d", B, N, H);
   HVIT_CHECK(aligned16(qkv) && aligned16(o), "hvit_mhsa_fwd: qkv/o must be 16-byte aligned");
@@ -964,7 +1000,7 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
     const int wv = v2_waves(B * H);
     auto go = [&](auto kern, int waves) {
       hipLaunchKernelGGL(kern, dim3(cdiv(N, 16 * waves), H, B), dim3(64 * waves), 0, st, (const bf16_t*)qkv,
-                         (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dr), dr ? dr->site : 0u);
+                         (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dr), dr ? dr->site : 0u, keep_bits);
     };
     if (wv == 16) go(mhsa_fwd_v2<16>, 16);
     else if (wv == 8) go(mhsa_fwd_v2<8>, 8);
@@ -975,10 +1011,9 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
   HVIT_HD_DISPATCH(mhsa_fwd_t, qkv, o, lse, probs, B, N, H, scale, dropout, st);
 }
 
-extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout,
-                             const float* lse, int B, int N, int H, int hd, float scale,
-                             const hvit_dropout_t* dropout, void* dqkv, float* delta_ws,
-                             void* stream) {
+static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N,
+                         int H, int hd, float scale, const hvit_dropout_t* dropout, const uint32_t* keep_bits,
+                         void* dqkv, float* delta_ws, void* stream) {
   HVIT_CHECK(qkv && o && dout && lse && dqkv && delta_ws, "hvit_mhsa_bwd: null pointer");
   HVIT_CHECK(B > 0 && N > 0 && H > 0, "hvit_mhsa_bwd: bad shape");
   HVIT_CHECK(aligned16(qkv) && aligned16(o) && aligned16(dout) && aligned16(dqkv),
@@ -994,9 +1029,9 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
     auto go = [&](auto dqk, auto dkvk, int waves) {
       dim3 g(cdiv(N, 16 * waves), H, B);
       hipLaunchKernelGGL(dqk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout,
-                         lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+                         lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits);
       hipLaunchKernelGGL(dkvk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                         (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site);
+                         (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits);
     };
     const int wv = v2_waves(B * H);
     if (wv == 16) go(mhsa_dq_v2<16>, mhsa_dkv_v2<16>, 16);
@@ -1006,4 +1041,37 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
     return HVIT_OK;
   }
   HVIT_HD_DISPATCH(mhsa_bwd_t, qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, dropout, st);
+}
+
+extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
+                             const hvit_dropout_t* dropout, void* o, float* lse, float* probs, void* stream) {
+  return mhsa_fwd_impl(dt, qkv, B, N, H, hd, scale, dropout, o, lse, probs, nullptr, stream);
+}
+
+extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N,
+                             int H, int hd, float scale, const hvit_dropout_t* dropout, void* dqkv, float* delta_ws,
+                             void* stream) {
+  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, nullptr, dqkv, delta_ws, stream);
+}
+
+// keep-bit variants: the forward stores its attention-dropout decisions (one
+// bit per (query, key), B*H*N*8 32-bit words for N <= 256) and the backward
+// reads them instead of re-hashing (bf16, head_dim 64, N <= 256, N % 4 == 0;
+// other shapes ignore keep_bits and regenerate the mask)
+extern "C" long long hvit_mhsa_keep_bits_elems(int B, int N, int H) {
+  return (B > 0 && N > 0 && H > 0) ? (long long)B * H * N * 8 : 0;
+}
+
+extern "C" int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
+                                const hvit_dropout_t* dropout, void* o, float* lse, unsigned* keep_bits,
+                                void* stream) {
+  HVIT_CHECK(!keep_bits || ((uintptr_t)keep_bits & 15) == 0, "hvit_mhsa_fwd_kb: keep_bits alignment");
+  return mhsa_fwd_impl(dt, qkv, B, N, H, hd, scale, dropout, o, lse, nullptr, keep_bits, stream);
+}
+
+extern "C" int hvit_mhsa_bwd_kb(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B,
+                                int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
+                                const unsigned* keep_bits, void* dqkv, float* delta_ws, void* stream) {
+  HVIT_CHECK(!keep_bits || ((uintptr_t)keep_bits & 15) == 0, "hvit_mhsa_bwd_kb: keep_bits alignment");
+  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, keep_bits, dqkv, delta_ws, stream);
 }

@@ -535,6 +535,7 @@ class ConvBNActFn(torch.autograd.Function):
 
 C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path
 EVALFOLD = os.environ.get("HVIT_EVALFOLD", "1") != "0"  # A/B knob: 0 = eval convs keep z + bn_act
+KEEPBITS = os.environ.get("HVIT_KEEPBITS", "1") != "0"  # A/B knob: 0 = the attention backward re-hashes dropout
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
@@ -776,6 +777,7 @@ class ViTBlockFn(torch.autograd.Function):
                  qkv.data_ptr(), dt, None, s)
         o = _empty((M, D), dt, dev)
         lse = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
+        kbits = None
         probs = torch.empty((B, H, Nt, Nt), dtype=torch.float32, device=dev) if want_probs else None
         if attn_fp8 and not want_probs:
             # fp8 (e4m3) QK^T / PV forward (BASELINE config 5); the backward
@@ -785,6 +787,12 @@ class ViTBlockFn(torch.autograd.Function):
             with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
                 call("hvit_mhsa_fwd_fp8", qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
                      lse.data_ptr(), s)
+        elif probs is None and d_attn.p > 0 and KEEPBITS:
+            # the dropout decisions are kept (1 bit per score) so the backward does not re-hash them
+            kbits = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, Nt, H), dtype=torch.int32, device=dev)
+            with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
+                call("hvit_mhsa_fwd_kb", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
+                     lse.data_ptr(), kbits.data_ptr(), s)
         else:
             with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
                 call("hvit_mhsa_fwd", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
@@ -810,6 +818,7 @@ class ViTBlockFn(torch.autograd.Function):
                  epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
         ctx.save_for_backward(n1w, n2w)
         ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
+        ctx.kbits = kbits
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, gh, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
         # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
@@ -858,8 +867,12 @@ class ViTBlockFn(torch.autograd.Function):
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         with timed("attn_bwd", 8.0 * B * H * Nt * Nt * (D // H)):
-            call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H, D // H,
-                 scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
+            if ctx.kbits is not None:
+                call("hvit_mhsa_bwd_kb", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
+                     D // H, scale, dra, ctx.kbits.data_ptr(), dqkv.data_ptr(), delta.data_ptr(), s)
+            else:
+                call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
+                     D // H, scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
         # qkv bias grad by a column reduction: the wgrad GEMM variant with fused
         # A-row sums spills at 128x128 (rocprof: 42 -> 28 us class without it)
         dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, tag="vit_linear_wgrad", dest=grad_dest(*dq_id))

@@ -363,6 +363,48 @@ def test_mhsa_fwd_bwd(hv, dt, B, N, H, hd, p):
         assert rel(g[:, i], r[:, i]) < (1e-4 if dt == "f32" else 4e-2), "qkv"[i]
 
 
+@pytest.mark.parametrize("B,N,H,p", [(2, 256, 8, 0.1), (3, 100, 2, 0.3), (1, 240, 4, 0.1), (2, 64, 8, 0.5)])
+def test_mhsa_keep_bits_equal_rehash(hv, B, N, H, p):
+    """hvit_mhsa_fwd_kb / hvit_mhsa_bwd_kb (forward keeps one dropout bit per
+    score, the backward reads them) give bit-identical o, lse and dqkv to the
+    re-hashing entry points; the bits themselves match the numpy mirror of
+    the counter hash (word pair (b, h, q, fq): bit 8*jp + 4*e + r = key
+    32*jp + 16*e + 4*fq + r)."""
+    l = L(hv)
+    hd, D = 64, H * 64
+    qkv = (torch.randn(B * N, 3 * D, device=DEV) * 0.7).to(torch.bfloat16)
+    dr = l.dropout(p, 99, 31)
+    outs = []
+    kb = torch.zeros(l.lib().hvit_mhsa_keep_bits_elems(B, N, H), dtype=torch.int32, device=DEV)
+    go = (torch.randn(B * N, D, device=DEV)).to(torch.bfloat16)
+    for use_kb in (False, True):
+        o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, N, device=DEV)
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B, H, N, device=DEV)
+        if use_kb:
+            l.call("hvit_mhsa_fwd_kb", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(),
+                   lse.data_ptr(), kb.data_ptr(), s())
+            l.call("hvit_mhsa_bwd_kb", l.BF16, qkv.data_ptr(), o.data_ptr(), go.data_ptr(), lse.data_ptr(), B, N, H,
+                   hd, hd ** -0.5, dr, kb.data_ptr(), dqkv.data_ptr(), delta.data_ptr(), s())
+        else:
+            l.call("hvit_mhsa_fwd", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+                   None, s())
+            l.call("hvit_mhsa_bwd", l.BF16, qkv.data_ptr(), o.data_ptr(), go.data_ptr(), lse.data_ptr(), B, N, H, hd,
+                   hd ** -0.5, dr, dqkv.data_ptr(), delta.data_ptr(), s())
+        outs.append((o, lse, dqkv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # the stored bits against the hash mirror
+    keep = keep_mask(99, 31, B * H * N * N, p).reshape(B * H, N, N)
+    w = kb.cpu().numpy().view(np.uint32).reshape(B * H, N, 4, 2)
+    for key in range(N):
+        jp, e, fq, r = key >> 5, (key >> 4) & 1, (key >> 2) & 3, key & 3
+        bit = 8 * jp + 4 * e + r
+        got = (w[:, :, fq, bit >> 5] >> np.uint32(bit & 31)) & np.uint32(1)
+        assert np.array_equal(got.astype(bool), keep[:, :, key]), key
+
+
 # ------------------------------------------------------------- layernorm ---
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("M,D", [(8192, 512), (37, 64), (16, 768)])
