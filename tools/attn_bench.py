@@ -36,6 +36,17 @@ def main(p=0.1):
                          B, N, H, hd, hd ** -0.5, dr, dqkv.data_ptr(), delta.data_ptr(), st())
     us = timeit(bwd)
     print(f"mhsa bwd p={p}: {us:7.1f} us  {2 * fl / us / 1e6:6.1f} TF/s", flush=True)
+    if p > 0:  # keep-bit variants (the training path)
+        kb = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, N, H), dtype=torch.int32, device="cuda")
+        fwdk = lambda: L.call("hvit_mhsa_fwd_kb", L.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr,  # noqa
+                              o.data_ptr(), lse.data_ptr(), kb.data_ptr(), st())
+        us = timeit(fwdk)
+        print(f"mhsa fwd_kb p={p}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s", flush=True)
+        bwdk = lambda: L.call("hvit_mhsa_bwd_kb", L.BF16, qkv.data_ptr(), o.data_ptr(), do.data_ptr(),  # noqa
+                              lse.data_ptr(), B, N, H, hd, hd ** -0.5, dr, kb.data_ptr(), dqkv.data_ptr(),
+                              delta.data_ptr(), st())
+        us = timeit(bwdk)
+        print(f"mhsa bwd_kb p={p}: {us:7.1f} us  {2 * fl / us / 1e6:6.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
