@@ -189,6 +189,19 @@ int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, float scale,
 int hvit_layernorm_fwd(const float* x, const float* gamma, const float* beta, int M, int D, float eps, void* y,
                        int y_dt, float* mean, float* rstd, void* stream);
 long long hvit_layernorm_bwd_ws_elems(int M, int D);   /* f32 slab for dgamma/dbeta partials */
+/* The backward with the dropout + DropPath scaling of its output fused
+ * (TransformerEncoderBlock, attention.py:206-211: the residual branch's
+ * Dropout and DropPath before the proj / fc2 Linear): besides dx, writes
+ * g_out = dx * keep / (1 - p) * rowscale[m / rows_per_sample] (g_dt) and
+ * accumulates into acc3 = [dgamma | dbeta | colsum(g_out)] (3*D f32; caller-
+ * zeroed with HVIT_ACC_ZEROED, else overwritten); ws =
+ * hvit_layernorm_bwd_drop_ws_elems floats.  Same results as hvit_layernorm_bwd
+ * followed by hvit_dropout_scale with a column sum. */
+long long hvit_layernorm_bwd_drop_ws_elems(int M, int D);
+int hvit_layernorm_bwd_drop(const void* dy, int dy_dt, const float* x, const float* mean, const float* rstd,
+                            const float* gamma, int M, int D, const float* resid, float* dx, float* acc3,
+                            const hvit_dropout_t* dropout, const float* rowscale, int rows_per_sample, void* g_out,
+                            int g_dt, float* ws, long long ws_elems, int flags, void* stream);
 int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean, const float* rstd,
                        const float* gamma, int M, int D, const float* resid, float* dx, float* dgamma,
                        float* dbeta, float* ws, long long ws_elems, int flags, void* stream);  /* ws may be

@@ -95,6 +95,9 @@ _SIGS = {
     "hvit_mhsa_bwd_kb": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_layernorm_fwd": ([vp, vp, vp, i32, i32, f32, vp, i32, vp, vp, vp], i32),
     "hvit_layernorm_bwd_ws_elems": ([i32, i32], i64),
+    "hvit_layernorm_bwd_drop_ws_elems": ([i32, i32], i64),
+    "hvit_layernorm_bwd_drop": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, P(Dropout), vp, i32, vp, i32, vp,
+                                 i64, i32, vp], i32),
     "hvit_layernorm_bwd": ([vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, i64, i32, vp], i32),
     "hvit_bn_finalize": ([vp, i32, i32, i64, i32, vp, vp, vp, vp, vp, f32, f32, vp], i32),
     "hvit_bn_eval_prep": ([vp, vp, i32, f32, vp, vp, vp], i32),

@@ -85,16 +85,42 @@ __device__ __forceinline__ f32x4 load_row4(const TD* p) {
   }
 }
 
+// Dropout (+ DropPath row scale) of the LayerNorm input gradient, fused into
+// the backward (DROP): g = dx * keep(row * D + c) / (1 - p) * rowscale[row /
+// rps] in g's dtype, and the column sums of g (the bias gradient of the GEMM
+// that consumes it) -- hvit_dropout_scale's arithmetic on dx while it is in
+// registers.
+struct LnDrop {
+  uint32_t thr = 0;
+  float ds = 1.f;
+  DSeed seed{0ull, nullptr};
+  uint32_t site = 0;
+  const float* rowscale = nullptr;
+  int rps = 1;
+  void* g = nullptr;
+  int g_bf16 = 1;
+};
+
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) (+ resid);
 // dgamma/dbeta partials per workgroup: written to the slab ws[blk][2][D]
-// (SLAB) and summed by ln_slab_sum_kernel, else added atomically.
-template <typename TD, int MAXV, bool SLAB>
+// (SLAB; [blk][3][D] with DROP's column sums) and summed by a column
+// reduction, else added atomically.
+template <typename TD, int MAXV, bool SLAB, bool DROP = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, const float* __restrict__ x,
                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                                     const float* __restrict__ g, const float* __restrict__ resid,
                                                     float* __restrict__ dx, float* __restrict__ dgamma,
-                                                    float* __restrict__ dbeta, float* __restrict__ ws, int M, int D) {
-  __shared__ float red[4][2][MAXV * 256];
+                                                    float* __restrict__ dbeta, float* __restrict__ ws, int M, int D,
+                                                    LnDrop dr = LnDrop()) {
+  constexpr int NS = DROP ? 3 : 2;
+  __shared__ float red[4][NS][MAXV * 256];
+  f32x4 acs[DROP ? MAXV : 1];
+  uint32_t dkey = 0;
+  if constexpr (DROP) {
+    if (dr.thr) dkey = rng_key((unsigned long long)dr.seed, dr.site);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) acs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   f32x4 ag[MAXV], ab[MAXV], gam[MAXV];
 #pragma unroll
@@ -150,6 +176,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     }
     s1 = wave_sum(s1) / (float)D;
     s2 = wave_sum(s2) / (float)D;
+    const float rsc = (DROP && dr.rowscale) ? dr.rowscale[row / dr.rps] : 1.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int c = lane * 4 + i * 256;
@@ -157,7 +184,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
         f32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = rs[r] * (gy[i][e] - s1 - xh[i][e] * s2);
-        *(f32x4*)(dx + (long)row * D + c) = o + rv[r][i];
+        o += rv[r][i];
+        *(f32x4*)(dx + (long)row * D + c) = o;
+        if constexpr (DROP) {
+          f32x4 k = {dr.ds, dr.ds, dr.ds, dr.ds};
+          if (dr.thr) k = keep4_at(dkey, (uint64_t)row * D + c, dr.thr, dr.ds);
+          const f32x4 gv = o * k * rsc;
+          if (dr.g_bf16) {
+            *(uint2*)((bf16_t*)dr.g + (long)row * D + c) = make_uint2(f2bf2(gv[0], gv[1]), f2bf2(gv[2], gv[3]));
+          } else {
+            *(f32x4*)((float*)dr.g + (long)row * D + c) = gv;
+          }
+          acs[i] += gv;
+        }
       }
     }
   }
@@ -167,18 +206,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     if (c < D) {
       *(f32x4*)&red[w][0][c] = ag[i];
       *(f32x4*)&red[w][1][c] = ab[i];
+      if constexpr (DROP) *(f32x4*)&red[w][2][c] = acs[i];
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += 256) {
-    const float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-    const float bb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    if (SLAB) {
-      ws[(size_t)blockIdx.x * 2 * D + c] = a;
-      ws[(size_t)blockIdx.x * 2 * D + D + c] = bb;
-    } else {
-      atomicAdd(dgamma + c, a);
-      atomicAdd(dbeta + c, bb);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const float a = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+      if (SLAB) ws[(size_t)blockIdx.x * NS * D + k * D + c] = a;
+      else atomicAdd((k == 0 ? dgamma : k == 1 ? dbeta : dgamma + 2 * D) + c, a);
     }
   }
 }
@@ -334,6 +371,48 @@ extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, con
     HVIT_LAUNCH_CHECK();
   }
   return HVIT_OK;
+}
+
+extern "C" long long hvit_layernorm_bwd_drop_ws_elems(int M, int D) {
+  return M > 0 ? (long long)cdiv(M, LNB_ROWS) * 3 * D : 0;
+}
+
+// hvit_layernorm_bwd + the dropout / DropPath scaling of its output (see LnDrop)
+extern "C" int hvit_layernorm_bwd_drop(const void* dy, int dy_dt, const float* x, const float* mean,
+                                       const float* rstd, const float* gamma, int M, int D, const float* resid,
+                                       float* dx, float* acc3, const hvit_dropout_t* dropout, const float* rowscale,
+                                       int rows_per_sample, void* g_out, int g_dt, float* ws, long long ws_elems,
+                                       int flags, void* stream) {
+  HVIT_CHECK(dy && x && mean && rstd && gamma && dx && acc3 && g_out && ws, "hvit_layernorm_bwd_drop: null pointer");
+  HVIT_CHECK(D % 4 == 0 && D <= 1024 && D > 0, "hvit_layernorm_bwd_drop: bad D=%d", D);
+  HVIT_CHECK(aligned16(x) && aligned16(dx) && aligned16(gamma) && aligned16(dy) && aligned16(g_out) &&
+                 (!resid || aligned16(resid)),
+             "hvit_layernorm_bwd_drop: alignment");
+  HVIT_CHECK(ws_elems >= hvit_layernorm_bwd_drop_ws_elems(M, D), "hvit_layernorm_bwd_drop: workspace too small");
+  HVIT_CHECK(!rowscale || rows_per_sample > 0, "hvit_layernorm_bwd_drop: rows_per_sample");
+  HVIT_CHECK(g_dt == HVIT_BF16 || g_dt == HVIT_F32, "hvit_layernorm_bwd_drop: g dtype");
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0) return HVIT_OK;
+  const int nblk = cdiv(M, LNB_ROWS);
+  LnDrop d;
+  d.thr = dropout ? drop_threshold(dropout->p) : 0;
+  d.ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
+  d.seed = dseed(dropout);
+  d.site = dropout ? dropout->site : 0u;
+  d.rowscale = rowscale;
+  d.rps = rows_per_sample > 0 ? rows_per_sample : 1;
+  d.g = g_out;
+  d.g_bf16 = g_dt == HVIT_BF16;
+  dim3 g(nblk);
+#define LNBD(TD, V)                                                                                             \
+  hipLaunchKernelGGL((ln_bwd_kernel<TD, V, true, true>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma, \
+                     resid, dx, acc3, acc3 + D, ws, M, D, d)
+  if (dy_dt == HVIT_F32) { if (D <= 256) LNBD(float, 1); else if (D <= 512) LNBD(float, 2); else LNBD(float, 4); }
+  else { if (D <= 256) LNBD(bf16_t, 1); else if (D <= 512) LNBD(bf16_t, 2); else LNBD(bf16_t, 4); }
+#undef LNBD
+  HVIT_LAUNCH_CHECK();
+  // one column reduction of the [nblk][3D] slab into [dgamma | dbeta | colsum]
+  return hvit_reduce_rows(ws, HVIT_F32, nblk, 3 * D, 3 * D, (flags & HVIT_ACC_ZEROED) ? 1 : 0, acc3, stream);
 }
 
 extern "C" int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C,

@@ -536,6 +536,7 @@ class ConvBNActFn(torch.autograd.Function):
 C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path
 EVALFOLD = os.environ.get("HVIT_EVALFOLD", "1") != "0"  # A/B knob: 0 = eval convs keep z + bn_act
 KEEPBITS = os.environ.get("HVIT_KEEPBITS", "1") != "0"  # A/B knob: 0 = the attention backward re-hashes dropout
+LNDROP = os.environ.get("HVIT_LNDROP", "1") != "0"  # A/B knob: 0 = separate LayerNorm backward and dropout pass
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
@@ -737,6 +738,24 @@ def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):
     return dx, dgw, dgb
 
 
+def _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs: ZSlot, drop, rowscale, rps, g_dt):
+    """_ln_bwd fused with dropout_scale of its output: returns dx (f32), dgamma,
+    dbeta, g = rowscale * dropout(dx) in g_dt and colsum(g).  zs: a zslot(3 * D)
+    (dgamma | dbeta | colsum)."""
+    M, D = x.shape
+    dx = torch.empty((M, D), dtype=torch.float32, device=x.device)
+    g = _empty((M, D), g_dt, x.device)
+    acc = zs.take(x.device)
+    ws_n = L.lib().hvit_layernorm_bwd_drop_ws_elems(M, D)
+    ws = torch.empty(ws_n, dtype=torch.float32, device=x.device)
+    es = g.element_size()
+    with timed("layernorm_bwd", float(M * D * (dy.element_size() + 8 + (4 if resid is not None else 0) + es))):
+        call("hvit_layernorm_bwd_drop", dy.data_ptr(), L.dt_of(dy), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+             gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), acc.data_ptr(), drop, ptr(rowscale), rps, g.data_ptr(),
+             g_dt, ws.data_ptr(), ws_n, L.ACC_ZEROED, stream_ptr())
+    return dx, acc[:D], acc[D:2 * D], g, acc[2 * D:3 * D]
+
+
 def droppath_scales(B, p, seed, dev):
     """DropPath (components.py:407-427) multipliers of a block's two residual
     branches from one launch: keep(seed, site 1, b) for the attention branch,
@@ -823,7 +842,8 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
         # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
         # the GELU-backward epilogue and the two dropout passes)
-        ctx.zs = (_zs(ctx, 2 * D), _zs(ctx, 2 * D), _zs(ctx, hid), _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
+        # (LN2's slot also holds the proj bias grad when its dropout pass is fused, LNDROP)
+        ctx.zs = (_zs(ctx, 2 * D), _zs(ctx, 3 * D), _zs(ctx, hid), _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
         if want_probs:
             ctx.mark_non_differentiable(probs)
         return x2.view(B, Nt, D), probs
@@ -855,11 +875,14 @@ class ViTBlockFn(torch.autograd.Function):
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_dgrad", 2.0 * M * hid * D):
             call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
-        dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2, zln2)
+        if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass
+            dx1, dn2w, dn2b, g1, dpb = _ln_bwd_drop(dxn2, x1, m2, r2, n2w, dx2, zln2, drp, rs1, Nt, dt)
+        else:
+            dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2, zln2)
+            g1 = _empty((M, D), dt, dev)
+            dpb = zpb.take(dev)
+            dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
         # attention branch
-        g1 = _empty((M, D), dt, dev)
-        dpb = zpb.take(dev)
-        dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
         dpw = linear_wgrad(dt, g1, o, M, D, D, tag="vit_linear_wgrad", dest=grad_dest(*dp_id))
         do = _empty((M, D), dt, dev)
         with timed("vit_linear_dgrad", 2.0 * M * D * D):

@@ -541,6 +541,54 @@ def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
         assert rel(dxb.float(), 2 * refb) < 2e-2
 
 
+@pytest.mark.parametrize("g_dt", ["bf16", "f32"])
+@pytest.mark.parametrize("M,D,p,rps", [(8192, 512, 0.1, 256), (37, 64, 0.3, 5), (300, 768, 0.0, 100)])
+def test_layernorm_bwd_drop_equals_two_passes(hv, g_dt, M, D, p, rps):
+    """hvit_layernorm_bwd_drop = hvit_layernorm_bwd then hvit_dropout_scale with
+    its column sum: dx and g bit-identical, [dgamma | dbeta | colsum] to f32
+    summation order."""
+    l = L(hv)
+    torch.manual_seed(M + D)
+    x = torch.randn(M, D, device=DEV) * 2 + 0.5
+    gam = torch.rand(D, device=DEV) + 0.5
+    mean = x.mean(1)
+    rstd = (x.var(1, unbiased=False) + 1e-5).rsqrt()
+    dy = torch.randn(M, D, device=DEV).to(torch.bfloat16)
+    resid = torch.randn(M, D, device=DEV)
+    rs = torch.rand(cdiv(M, rps), device=DEV) + 0.5
+    dr = l.dropout(p, 77, 9)
+    gdt, gt = (l.BF16, torch.bfloat16) if g_dt == "bf16" else (l.F32, torch.float32)
+    # two passes
+    dx = torch.empty(M, D, device=DEV)
+    acc = torch.zeros(2 * D, device=DEV)
+    l.call("hvit_layernorm_bwd", dy.data_ptr(), l.BF16, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+           gam.data_ptr(), M, D, resid.data_ptr(), dx.data_ptr(), acc.data_ptr(), acc[D:].data_ptr(), None, 0,
+           l.ACC_ZEROED, s())
+    g = torch.empty(M, D, device=DEV, dtype=gt)
+    cs = torch.zeros(D, device=DEV)
+    ws_n = l.lib().hvit_dropout_colsum_ws_elems(D)
+    ws = torch.empty(max(ws_n, 1), device=DEV)
+    l.call("hvit_dropout_scale", dx.data_ptr(), l.F32, M, D, dr, rs.data_ptr(), rps, g.data_ptr(), gdt,
+           cs.data_ptr(), ws.data_ptr(), ws_n, s())
+    # fused
+    dx2 = torch.empty_like(dx)
+    g2 = torch.empty_like(g)
+    acc3 = torch.zeros(3 * D, device=DEV)
+    ws2_n = l.lib().hvit_layernorm_bwd_drop_ws_elems(M, D)
+    ws2 = torch.empty(ws2_n, device=DEV)
+    l.call("hvit_layernorm_bwd_drop", dy.data_ptr(), l.BF16, x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+           gam.data_ptr(), M, D, resid.data_ptr(), dx2.data_ptr(), acc3.data_ptr(), dr, rs.data_ptr(), rps,
+           g2.data_ptr(), gdt, ws2.data_ptr(), ws2_n, l.ACC_ZEROED, s())
+    assert torch.equal(dx, dx2)
+    assert torch.equal(g, g2)
+    assert rel(acc3[:2 * D], acc) < 1e-5
+    assert rel(acc3[2 * D:], cs) < 1e-5
+
+
+def cdiv(a, b):
+    return (a + b - 1) // b
+
+
 # --------------------------------------------------------------- DropPath ---
 @pytest.mark.parametrize("p", [0.02, 0.1, 0.5])
 def test_droppath_scale_mask_and_rate(hv, p):
