@@ -756,6 +756,29 @@ def _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs: ZSlot, drop, rowscale, rps, g
     return dx, acc[:D], acc[D:2 * D], g, acc[2 * D:3 * D]
 
 
+class GradHandoff:
+    """Block l's MLP-branch dropout (its fc2 input gradient g2 = DropPath *
+    Dropout of the incoming gradient, attention.py:210-211) computed by the
+    NEXT consumer of block l's output -- block l+1's LN1 backward or the head's
+    final-LN backward -- while that gradient is in its registers
+    (_ln_bwd_drop).  Block l's forward fills the dropout config; the consumer's
+    backward fills g and colsum; block l's backward (which runs after it) uses
+    them instead of a dropout_scale pass.  Unfilled: block l falls back."""
+
+    __slots__ = ("drop", "rowscale", "rps", "dt", "g", "colsum")
+
+    def __init__(self):
+        self.drop = self.rowscale = self.rps = self.dt = self.g = self.colsum = None
+
+    def fuse(self, dy, x, mean, rstd, gw, resid, zs):
+        """The consumer's LN backward with this handoff's dropout fused; returns
+        (dx, dgamma, dbeta) like _ln_bwd."""
+        dx, dgw, dgb, g, cs = _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs, self.drop, self.rowscale, self.rps,
+                                           self.dt)
+        self.g, self.colsum = g, cs
+        return dx, dgw, dgb
+
+
 def droppath_scales(B, p, seed, dev):
     """DropPath (components.py:407-427) multipliers of a block's two residual
     branches from one launch: keep(seed, site 1, b) for the attention branch,
@@ -777,7 +800,8 @@ class ViTBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, H, drops, dpr, training,
-                dt, want_probs, attn_fp8=False):
+                dt, want_probs, attn_fp8=False, ho_in: Optional[GradHandoff] = None,
+                ho_out: Optional[GradHandoff] = None):
         B, Nt, D = x.shape
         M = B * Nt
         hd = D // H
@@ -838,12 +862,17 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.save_for_backward(n1w, n2w)
         ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
         ctx.kbits = kbits
+        # the fc2 branch's dropout / DropPath of the incoming gradient, for the
+        # next consumer of x2 to fuse into its LayerNorm backward (GradHandoff)
+        if ho_out is not None and LNDROP:
+            ho_out.drop, ho_out.rowscale, ho_out.rps, ho_out.dt = d_fc2.c(), rs2, Nt, dt
+        ctx.ho = (ho_in if LNDROP else None, ho_out)
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, gh, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
         # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
         # the GELU-backward epilogue and the two dropout passes)
-        # (LN2's slot also holds the proj bias grad when its dropout pass is fused, LNDROP)
-        ctx.zs = (_zs(ctx, 2 * D), _zs(ctx, 3 * D), _zs(ctx, hid), _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
+        # (LN1's / LN2's slots also hold a bias grad when a dropout pass is fused, LNDROP)
+        ctx.zs = (_zs(ctx, 3 * D), _zs(ctx, 3 * D), _zs(ctx, hid), _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
         if want_probs:
             ctx.mark_non_differentiable(probs)
         return x2.view(B, Nt, D), probs
@@ -861,9 +890,14 @@ class ViTBlockFn(torch.autograd.Function):
             dx2 = dx2.float()
         # MLP branch
         zln1, zln2, zf1b, zf2b, zpb, zqb = ctx.zs
-        g2 = _empty((M, D), dt, dev)
-        df2b = zf2b.take(dev)
-        dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
+        ho_in, ho_out = ctx.ho
+        if ho_out is not None and ho_out.g is not None:  # fused into the next consumer's LN backward
+            g2, df2b = ho_out.g, ho_out.colsum
+            ho_out.g = ho_out.colsum = None
+        else:
+            g2 = _empty((M, D), dt, dev)
+            df2b = zf2b.take(dev)
+            dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
         dq_id, dp_id, d1_id, d2_id = ctx.wid
         df2w = linear_wgrad(dt, g2, a, M, D, hid, tag="vit_linear_wgrad", dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
@@ -905,9 +939,12 @@ class ViTBlockFn(torch.autograd.Function):
         with timed("vit_linear_dgrad", 2.0 * M * 3 * D * D):
             call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None,
                  s)
-        dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
+        if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
+            dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1)
+        else:
+            dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 class HeadFn(torch.autograd.Function):
@@ -916,7 +953,7 @@ class HeadFn(torch.autograd.Function):
     identity: f32 tokens [B, N, D] -> NHWC feature map [B, Hp, Wp, C]."""
 
     @staticmethod
-    def forward(ctx, x, nw, nb, w, b, hw, dt):
+    def forward(ctx, x, nw, nb, w, b, hw, dt, ho: Optional[GradHandoff] = None):
         B, Nt, D = x.shape
         M = B * Nt
         C = w.shape[0]
@@ -929,7 +966,8 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(nw)
         ctx.t = (x2d, xn, m, r, W)
         ctx.meta = (B, Nt, D, C, dt)
-        ctx.zs = _zs(ctx, 2 * D)
+        ctx.ho = ho if LNDROP else None
+        ctx.zs = _zs(ctx, 3 * D)
         return y
 
     @staticmethod
@@ -943,8 +981,11 @@ class HeadFn(torch.autograd.Function):
         dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
         call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32, None,
              stream_ptr())
-        dx, dnw, dnb = _ln_bwd(dxn, x2d, m, r, nw, None, ctx.zs)
-        return dx.view(B, Nt, D), dnw, dnb, dw, db, None, None
+        if ctx.ho is not None and ctx.ho.drop is not None:  # the last block's fc2 dropout, fused
+            dx, dnw, dnb = ctx.ho.fuse(dxn, x2d, m, r, nw, None, ctx.zs)
+        else:
+            dx, dnw, dnb = _ln_bwd(dxn, x2d, m, r, nw, None, ctx.zs)
+        return dx.view(B, Nt, D), dnw, dnb, dw, db, None, None, None
 
 
 class SkipFn(torch.autograd.Function):

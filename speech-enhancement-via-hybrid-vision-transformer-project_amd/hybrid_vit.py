@@ -450,7 +450,11 @@ class HybridViT(nn.Module):
         return HF.PosDropFn.apply(t, self.pos_encoding.pos_embed, HF.Drop(self.dropout_p, 0, 200, seed), self.training)
 
     def _vit(self, t, dt, seed, want_attn=False):
+        """Returns (tokens, attention maps, the last block's GradHandoff or None).
+        Each block's fc2-branch dropout backward rides on the next block's LN1
+        backward (HF.GradHandoff)."""
         attns = []
+        ho = None
         if self.attention_precision == "fp8" and dt != L.BF16 and not self._fp8_warned:
             import warnings
             warnings.warn("hvit: attention_precision='fp8' is ignored: this forward runs the fp32 path "
@@ -462,19 +466,22 @@ class HybridViT(nn.Module):
             drops = (HF.Drop(blk.p_attn, 0, base, seed), HF.Drop(blk.p, 0, base + 1, seed),
                      HF.Drop(blk.p, 0, base + 2, seed), HF.Drop(blk.p, 0, base + 3, seed),
                      HF.Drop(0.0, base << 20, 1, seed))
+            ho_in, ho = ho, (HF.GradHandoff() if HF.LNDROP and self.training else None)
             t, probs = HF.ViTBlockFn.apply(t, blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias,
                                            a.proj.weight, a.proj.bias, blk.norm2.weight, blk.norm2.bias,
                                            m[0].weight, m[0].bias, m[3].weight, m[3].bias, a.num_heads, drops,
                                            blk.dpr, self.training, dt, want_attn,
-                                           self.attention_precision == "fp8" and dt == L.BF16)
+                                           self.attention_precision == "fp8" and dt == L.BF16, ho_in, ho)
             attns.append(probs)
-        return t, attns
+        return t, attns, ho
 
-    def _head(self, t, hw, dt):
+    def _head(self, t, hw, dt, ho=None):
         if self.cls_token is not None:
             t = t[:, 1:]  # hybrid_vit.py:337-338 (LayerNorm is per token, so dropping first is equivalent)
+            ho = None  # the handoff's row -> sample map covers the cls row
         n = self.transformer.norm
-        return HF.HeadFn.apply(t, n.weight, n.bias, self.to_feature_map.weight, self.to_feature_map.bias, hw, dt)
+        return HF.HeadFn.apply(t, n.weight, n.bias, self.to_feature_map.weight, self.to_feature_map.bias, hw, dt,
+                               ho)
 
     def _decoder(self, x, skips, out_hw, dt, seed, sgs=None):
         skips = skips[::-1]
@@ -511,8 +518,8 @@ class HybridViT(nn.Module):
         dt = self._dt()
         seed = self._seed()
         t = self._pos_tokens(x, seed)
-        t, _ = self._vit(t, dt, seed)
-        out = self._head(t, spatial_shape, dt)
+        t, _, ho = self._vit(t, dt, seed)
+        out = self._head(t, spatial_shape, dt, ho)
         HF.zflush(x.device)
         return self._nchw(out)
 
@@ -552,8 +559,8 @@ class HybridViT(nn.Module):
         sgs = [HF.SkipGrad() for _ in self.encoder] if self.use_skip_connections and HF.SKIPGRAD else None
         feat, skips = self._encoder(xh, dt, seed, sgs)
         t, hw = self._tokens(feat, dt, seed, sgs[-1] if sgs else None)
-        t, attns = self._vit(t, dt, seed, return_attentions)
-        f = self._head(t, hw, dt)
+        t, attns, ho = self._vit(t, dt, seed, return_attentions)
+        f = self._head(t, hw, dt, ho)
         out = self._decoder(f, skips, (F, T), dt, seed, sgs)
         HF.zflush(x.device)
         out = self._nchw(out)

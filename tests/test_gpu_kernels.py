@@ -582,7 +582,12 @@ def test_layernorm_bwd_drop_equals_two_passes(hv, g_dt, M, D, p, rps):
     assert torch.equal(dx, dx2)
     assert torch.equal(g, g2)
     assert rel(acc3[:2 * D], acc) < 1e-5
-    assert rel(acc3[2 * D:], cs) < 1e-5
+    # the fused colsum adds the f32 values before the store's rounding; the
+    # two-pass path does too when its colsum kernel applies ((D/4) | 256),
+    # otherwise it reduces the stored bf16 g
+    f32_sums = g_dt == "f32" or 256 % (D // 4) == 0
+    assert rel(acc3[2 * D:], cs) < (1e-5 if f32_sums else 1e-2)
+    assert rel(acc3[2 * D:], g2.float().sum(0)) < (1e-5 if g_dt == "f32" else 1e-2)
 
 
 def cdiv(a, b):

@@ -312,6 +312,34 @@ def test_skip_grad_handoff_matches_autograd_add(hv, precision):
         assert relnorm(grads[0][k].cpu(), grads[1][k].cpu()) < tol, k
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("cls", [False, True], ids=["nocls", "cls"])
+def test_ln_dropout_fusion_matches_separate_passes(hv, precision, cls):
+    """HF.LNDROP (the attention branch's dropout fused into LN2's backward, each
+    block's MLP-branch dropout into the next consumer's LN backward through
+    HF.GradHandoff) gives the gradients of the separate dropout_scale passes,
+    with dropout and DropPath on (train mode, reference default rates; same
+    seeds)."""
+    import sys
+    HF = sys.modules["hvit_amd.functional"]
+    g = golden("tiny_64")
+    x, t = torch.as_tensor(g["x"]).cuda(), torch.as_tensor(g["target"]).cuda()
+    kw = dict(O.TINY, drop_path_rate=0.1, use_cls_token=cls)
+    grads = []
+    for on in (True, False):
+        HF.LNDROP = on
+        try:
+            torch.manual_seed(5)
+            m = build(hv, kw, precision, False).train()
+            hv.CombinedLoss()(m(x), t).backward()
+            grads.append({k: p.grad.detach().clone() for k, p in m.named_parameters()})
+        finally:
+            HF.LNDROP = True
+    tol = 1e-5 if precision == "fp32" else 1e-2
+    for k in grads[0]:
+        assert relnorm(grads[0][k].cpu(), grads[1][k].cpu()) < tol, k
+
+
 @pytest.mark.parametrize("kw", [{}, LARGE], ids=["default", "large"])
 def test_vit_backward_isolated(hv, kw):
     """The transformer path alone (pos-embed add, every ViT block, final
