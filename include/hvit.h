@@ -56,6 +56,16 @@ typedef struct {
   const unsigned long long* seed_ptr;
 } hvit_dropout_t;
 
+/* Split-K partial slabs handed from one launch to a later one: dst[i] =
+ * sum over z < splits of src[z * stride + i], i < n (f32). */
+typedef struct {
+  const float* src;
+  float* dst;
+  long long n;
+  long long stride;
+  int splits;
+} hvit_slab_sum_t;
+
 /* Fused GEMM epilogue (applied in this order):
  *   v  = acc (+ bias[n]) (+ rowadd[(m % rowadd_rows) * N + n])
  *   GELU_DUAL: y = v (pre-activation); out2 = dropout(gelu(v))      -> stop
@@ -77,6 +87,11 @@ typedef struct {
   const float* rowadd;
   int rowadd_rows;
   float* colsum;
+  /* side job (n = 0: none; hvit_linear_fwd / hvit_linear_dgrad only): the
+   * slabs of a deferred weight gradient (hvit_linear_wgrad_defer) summed by
+   * this launch's workgroups before their own tiles -- no reduction launch of
+   * its own.  Complete when this call's launch is. */
+  hvit_slab_sum_t side;
 } hvit_epilogue_t;
 
 /* Convolution geometry.  Input image = concat(src1[C1], src2[C2]) (channels)
@@ -117,9 +132,18 @@ int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, in
  * gemm_ring.h); what 1 = the fused first block's matrix-core kernels (1 on, 0:
  * the VALU kernels).  Returns the previous value (-1 for an unknown knob). */
 int hvit_gemm_tune(int what, int value);
+/* dw[N,K] = dy^T x; db[N] = colsum(dy) (nullable; fused when db == dw + N*K) */
 int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
-                      float* ws, long long ws_elems, void* stream);  /* dw[N,K] = dy^T x; db[N] = colsum(dy)
-                                                                        (nullable; fused when db == dw + N*K) */                        /* dw[N,K] = dy^T x */
+                      float* ws, long long ws_elems, void* stream);
+/* The weight gradient with its split-K reduction deferred: when the GEMM
+ * splits K, it leaves the partial slabs in ws and fills *job (job->n > 0) for
+ * the caller to pass as the `side` job of the next hvit_linear_fwd / _dgrad
+ * epilogue on the same stream (or to hvit_sum_slabs_strided); dw is final only
+ * after that.  Otherwise dw is written and job->n = 0.  No bias gradient.
+ * side (nullable): an earlier launch's slabs, summed by this launch. */
+int hvit_linear_wgrad_defer(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* ws,
+                            long long ws_elems, const hvit_slab_sum_t* side, hvit_slab_sum_t* job, void* stream);
+int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream);
 
 /* ---- Convolution as implicit GEMM (ConvBlock conv components.py:55-62,
  * TransposeConvBlock upsample+conv components.py:146-158, PatchEmbedding
@@ -174,6 +198,17 @@ int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float
 int hvit_mhsa_bwd_kb(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
                      int hd, float scale, const hvit_dropout_t* dropout, const unsigned* keep_bits, void* dqkv,
                      float* delta_ws, void* stream);
+/* The backward with keep_bits optional (NULL: regenerate the mask) and the qkv
+ * Linear's bias gradient (attention.py:55, Linear(dim, 3*dim) bias) formed on
+ * the way: dbias_rows (f32 [hvit_mhsa_bias_rows(...)][3 * H * hd], NULL for
+ * none) receives partial column sums of dqkv (overwritten) whose sum over the
+ * rows is the bias gradient -- one row per attention workgroup, written by
+ * the backward kernels themselves (other shapes: column reductions of dqkv).
+ * Sum them with an hvit_slab_sum_t {dbias_rows, db, 3*H*hd, 3*H*hd, rows}. */
+long long hvit_mhsa_bias_rows(int dt, int B, int N, int H, int hd);
+int hvit_mhsa_bwd_db(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
+                     int hd, float scale, const hvit_dropout_t* dropout, const unsigned* keep_bits, void* dqkv,
+                     float* delta_ws, float* dbias_rows, void* stream);
 /* fp8 (OCP e4m3) forward of the same core for BASELINE config 5: bf16 qkv / o,
  * per-(b, h) power-of-two scales for K and V and per-query scales for Q
  * (e4m3 range from the absolute maxima), QK^T on v_mfma_f32_16x16x32_fp8_fp8,

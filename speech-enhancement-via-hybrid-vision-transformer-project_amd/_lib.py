@@ -31,11 +31,16 @@ class Dropout(C.Structure):
     _fields_ = [("p", C.c_float), ("seed", C.c_ulonglong), ("site", C.c_uint), ("seed_ptr", C.c_void_p)]
 
 
+class SlabSum(C.Structure):
+    """hvit_slab_sum_t: split-K slabs of a deferred weight gradient."""
+    _fields_ = [("src", vp), ("dst", vp), ("n", i64), ("stride", i64), ("splits", i32)]
+
+
 class Epilogue(C.Structure):
     _fields_ = [
         ("act", i32), ("out2", vp), ("out2_dt", i32), ("aux", vp), ("aux_dt", i32),
         ("dropout", Dropout), ("resid", vp), ("rowscale", vp), ("rows_per_sample", i32),
-        ("rowadd", vp), ("rowadd_rows", i32), ("colsum", vp),
+        ("rowadd", vp), ("rowadd_rows", i32), ("colsum", vp), ("side", SlabSum),
     ]
 
 
@@ -79,6 +84,9 @@ _SIGS = {
     "hvit_wgrad_workspace": ([i32, i32, i32], i64),
     "hvit_linear_wgrad": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp], i32),
     "hvit_wgrad_tickets": ([i32, i32, i32], i64),
+    "hvit_linear_wgrad_defer": ([i32, vp, vp, i32, i32, i32, vp, vp, i64, P(SlabSum), P(SlabSum), vp], i32),
+    "hvit_mhsa_bias_rows": ([i32, i32, i32, i32, i32], i64),
+    "hvit_sum_slabs_strided": ([vp, i32, i64, i64, vp, vp], i32),
     "hvit_linear_wgrad_tk": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp, i64, i32, vp], i32),
     "hvit_conv_fwd": ([i32, P(ConvGeom), vp, vp, vp, i32, vp, P(Epilogue), vp], i32),
     "hvit_conv_dgrad": ([i32, P(ConvGeom), vp, vp, vp, i32, vp], i32),
@@ -93,6 +101,7 @@ _SIGS = {
     "hvit_mhsa_keep_bits_elems": ([i32, i32, i32], i64),
     "hvit_mhsa_fwd_kb": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_bwd_kb": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
+    "hvit_mhsa_bwd_db": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp, vp], i32),
     "hvit_layernorm_fwd": ([vp, vp, vp, i32, i32, f32, vp, i32, vp, vp, vp], i32),
     "hvit_layernorm_bwd_ws_elems": ([i32, i32], i64),
     "hvit_layernorm_bwd_drop_ws_elems": ([i32, i32], i64),

@@ -16,6 +16,7 @@
 // Backward (FlashAttention-2 style recompute from lse): a dQ kernel over query
 // tiles and a dK/dV kernel over key tiles, both recomputing P; delta =
 // rowsum(dO * O) is produced by a small pre-pass.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -694,6 +695,40 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   }
 }
 
+// Column sums over a workgroup's rows of one head's [rows][64] gradient block
+// held as acc[t][r] (column d = 16t + 4fq + r, row = the lane's query / key):
+// the 16 lanes of a quarter (frow) by xor shuffles, the waves through LDS `red`
+// ([WAVES][64] f32), then one plain store per column into out[0..63] (this
+// workgroup's partial of the qkv bias gradient, attention.py:55; a later pass
+// sums the partials: 32 workgroups adding to one address serialised at L2
+// and cost more than the reduction pass they replaced).
+template <int WAVES>
+__device__ __forceinline__ void v2_colsum64(const f32x4 (&acc)[4], float mul, float* red, float* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // the 16 rows of a quarter are one DPP row: rotate-and-add (row_ror 8,
+      // 4, 2, 1) leaves the row sum in every lane, on the VALU (no LDS
+      // permutes)
+      float v = acc[t][r] * mul;
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+      if (frow == 0) red[w * 64 + 16 * t + 4 * fq + r] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) s += red[i * 64 + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+}
+
 // dQ (+ delta = rowsum(dO * O), written for the dK/dV kernel):
 // workgroup = (b, h, 16*WAVES queries); K, V images in LDS
 template <int WAVES>
@@ -702,9 +737,10 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
                                                         const float* __restrict__ lse, float* __restrict__ delta,
                                                         bf16_t* __restrict__ dqkv, int N, int H, float scale,
                                                         uint32_t thr, float dscale, DSeed seed_,
-                                                        uint32_t site, const uint32_t* __restrict__ kbits) {
+                                                        uint32_t site, const uint32_t* __restrict__ kbits,
+                                                        float* __restrict__ dbias) {
   const unsigned long long seed = seed_;
-  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
+  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + WAVES * 64 * 4];
   char* Ks = smem;
   char* Vs = smem + V2_KMAX * V2_ROWB;
   const int D = H * 64;
@@ -793,6 +829,10 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
       *(uint2*)(dp_out + 16 * t + 4 * fq) = u;
     }
   }
+  // q bias gradient (queries >= N hold dq = 0)
+  if (dbias)
+    v2_colsum64<WAVES>(dq, scale, (float*)(smem + 2 * V2_KMAX * V2_ROWB),
+                       dbias + (long)(b * gridDim.x + blockIdx.x) * 3 * D + h * 64);
 }
 
 // dK, dV: workgroup = (b, h, 16*WAVES keys); wave = 16 keys x all queries;
@@ -804,9 +844,11 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                          int N, int H, float scale, uint32_t thr, float dscale,
                                                          DSeed seed_, uint32_t site,
-                                                         const uint32_t* __restrict__ kbits) {
+                                                         const uint32_t* __restrict__ kbits,
+                                                         float* __restrict__ dbias) {
   const unsigned long long seed = seed_;
-  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4 + V2_KMAX * 32];
+  constexpr int RED = 2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4 + V2_KMAX * 32;  // colsum scratch offset
+  __shared__ __attribute__((aligned(16))) char smem[RED + 2 * WAVES * 64 * 4];
   char* Qs = smem;
   char* Ds = smem + V2_KMAX * V2_ROWB;
   float* Ls = (float*)(smem + 2 * V2_KMAX * V2_ROWB);
@@ -915,6 +957,12 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
       *(uint2*)(row + 2 * D + 16 * t + 4 * fq) = u;
     }
   }
+  // k and v bias gradients (keys >= N hold dk = dv = 0)
+  if (dbias) {
+    float* prow = dbias + (long)(b * gridDim.x + blockIdx.x) * 3 * D;
+    v2_colsum64<WAVES>(dkt, scale, (float*)(smem + RED), prow + D + h * 64);
+    v2_colsum64<WAVES>(dvt, 1.f, (float*)(smem + RED) + WAVES * 64, prow + 2 * D + h * 64);
+  }
 }
 
 static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 && N <= V2_KMAX && N % 4 == 0; }
@@ -1011,9 +1059,15 @@ static int mhsa_fwd_impl(int dt, const void* qkv, int B, int N, int H, int hd, f
   HVIT_HD_DISPATCH(mhsa_fwd_t, qkv, o, lse, probs, B, N, H, scale, dropout, st);
 }
 
+// partial rows of the fused bias gradient per sample: one per v2 workgroup
+// along the token axis; one per sample otherwise
+static long long mhsa_bias_rows_per_sample(int dt, int hd, int N) {
+  return v2_ok(dt, hd, N) ? cdiv(N, 16 * v2_waves(0)) : 1;
+}
+
 static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N,
                          int H, int hd, float scale, const hvit_dropout_t* dropout, const uint32_t* keep_bits,
-                         void* dqkv, float* delta_ws, void* stream) {
+                         void* dqkv, float* delta_ws, float* dbias, void* stream) {
   HVIT_CHECK(qkv && o && dout && lse && dqkv && delta_ws, "hvit_mhsa_bwd: null pointer");
   HVIT_CHECK(B > 0 && N > 0 && H > 0, "hvit_mhsa_bwd: bad shape");
   HVIT_CHECK(aligned16(qkv) && aligned16(o) && aligned16(dout) && aligned16(dqkv),
@@ -1029,15 +1083,28 @@ static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dou
     auto go = [&](auto dqk, auto dkvk, int waves) {
       dim3 g(cdiv(N, 16 * waves), H, B);
       hipLaunchKernelGGL(dqk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout,
-                         lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits);
+                         lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits, dbias);
       hipLaunchKernelGGL(dkvk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
-                         (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits);
+                         (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits, dbias);
     };
     const int wv = v2_waves(B * H);
     if (wv == 16) go(mhsa_dq_v2<16>, mhsa_dkv_v2<16>, 16);
     else if (wv == 8) go(mhsa_dq_v2<8>, mhsa_dkv_v2<8>, 8);
     else go(mhsa_dq_v2<4>, mhsa_dkv_v2<4>, 4);
     HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
+  if (dbias) {  // other shapes: the partial rows by column reductions of dqkv (one per row group)
+    const auto rc = [&]() -> int { HVIT_HD_DISPATCH(mhsa_bwd_t, qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, dropout, st); }();
+    if (rc) return rc;
+    const long long C3 = 3LL * H * hd, R = mhsa_bias_rows_per_sample(dt, hd, N);
+    const long long per = (N + R - 1) / R;
+    for (long long g = 0; g < (long long)B * R; ++g) {
+      const long long r0 = (g / R) * N + (g % R) * per, nr = std::min<long long>(per, (g / R) * N + N - r0);
+      if (int rc2 = hvit_reduce_rows((const char*)dqkv + r0 * C3 * (dt == HVIT_BF16 ? 2 : 4), dt, nr, C3, C3, 0,
+                                     dbias + g * C3, stream))
+        return rc2;
+    }
     return HVIT_OK;
   }
   HVIT_HD_DISPATCH(mhsa_bwd_t, qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, dropout, st);
@@ -1051,7 +1118,7 @@ extern "C" int hvit_mhsa_fwd(int dt, const void* qkv, int B, int N, int H, int h
 extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N,
                              int H, int hd, float scale, const hvit_dropout_t* dropout, void* dqkv, float* delta_ws,
                              void* stream) {
-  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, nullptr, dqkv, delta_ws, stream);
+  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, nullptr, dqkv, delta_ws, nullptr, stream);
 }
 
 // keep-bit variants: the forward stores its attention-dropout decisions (one
@@ -1073,5 +1140,21 @@ extern "C" int hvit_mhsa_bwd_kb(int dt, const void* qkv, const void* o, const vo
                                 int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
                                 const unsigned* keep_bits, void* dqkv, float* delta_ws, void* stream) {
   HVIT_CHECK(!keep_bits || ((uintptr_t)keep_bits & 15) == 0, "hvit_mhsa_bwd_kb: keep_bits alignment");
-  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, keep_bits, dqkv, delta_ws, stream);
+  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, keep_bits, dqkv, delta_ws, nullptr, stream);
+}
+
+// keep_bits and dbias_rows both optional: dbias_rows (f32
+// [hvit_mhsa_bias_rows(B, N, H, hd)][3 * H * hd], overwritten) receives partial
+// column sums of dqkv whose sum over rows is the qkv bias gradient, formed
+// inside the attention backward (v2 shapes) instead of by a pass over dqkv
+extern "C" long long hvit_mhsa_bias_rows(int dt, int B, int N, int H, int hd) {
+  (void)H;
+  return (B > 0 && N > 0) ? (long long)B * mhsa_bias_rows_per_sample(dt, hd, N) : 0;
+}
+
+extern "C" int hvit_mhsa_bwd_db(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B,
+                                int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
+                                const unsigned* keep_bits, void* dqkv, float* delta_ws, float* dbias, void* stream) {
+  HVIT_CHECK(!keep_bits || ((uintptr_t)keep_bits & 15) == 0, "hvit_mhsa_bwd_db: keep_bits alignment");
+  return mhsa_bwd_impl(dt, qkv, o, dout, lse, B, N, H, hd, scale, dropout, keep_bits, dqkv, delta_ws, dbias, stream);
 }

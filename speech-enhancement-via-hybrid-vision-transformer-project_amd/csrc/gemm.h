@@ -380,7 +380,40 @@ struct Epi {
   int dma = 1;              // host: LDS-DMA kernels allowed (GemmCoreDma); 0 = register staging only
   // EPI_PATCH: m = token (b, py, px) of Hp x Wp, n = (ky*P + kx)*C + c
   int pP = 0, pC = 0, pHp = 0, pWp = 0, pH = 0, pW = 0;
+  // side job (hvit_slab_sum_t): a deferred weight gradient's split-K slabs
+  // summed by this launch's workgroups before their own tiles (epi_side)
+  const float* sj_src = nullptr;
+  float* sj_dst = nullptr;
+  long sj_n4 = 0;      // float4 granules
+  long sj_stride4 = 0;
+  int sj_splits = 0;
 };
+
+// dst[i] = sum_z src[z * stride + i] over the side job's granules, spread over
+// every workgroup of the launch; the same pairing as sum_slabs_strided_kernel
+// (even slabs | odd slabs), so the result is bit-identical to that launch.
+// gemm_kernel runs it after its tile's epilogue (two or three workgroups per
+// CU, out of phase: the load latency overlaps a co-resident workgroup's K
+// loop); the ring kernels after issuing their DMA prologue (one workgroup per
+// CU: the latency overlaps the first stages' flight).  Any in-flight stores
+// only make a later counted vmcnt wait stricter.
+__device__ __forceinline__ void epi_side(const Epi& ep) {
+  if (!ep.sj_n4) return;
+  const long nthr = (long)gridDim.x * gridDim.y * gridDim.z * blockDim.x;
+  const long b = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+  const f32x4* src = (const f32x4*)ep.sj_src;
+  f32x4* dst = (f32x4*)ep.sj_dst;
+  for (long i = b * blockDim.x + threadIdx.x; i < ep.sj_n4; i += nthr) {
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+    int k = 0;
+    for (; k + 1 < ep.sj_splits; k += 2) {
+      s0 += src[(long)k * ep.sj_stride4 + i];
+      s1 += src[(long)(k + 1) * ep.sj_stride4 + i];
+    }
+    if (k < ep.sj_splits) s0 += src[(long)k * ep.sj_stride4 + i];
+    dst[i] = s0 + s1;
+  }
+}
 
 // 4 adjacent output columns (n .. n+nv-1) of row m: store helpers and the
 // fused epilogue math.
@@ -1401,6 +1434,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           atomicAdd(ep.colsum + n8 + e, t);
         }
     }
+    epi_side(ep);
     GEMM_STAMP(2);
     return;
   }
@@ -1664,6 +1698,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
         atomicAdd(ep.colsum + n + e, s);
       }
   }
+  epi_side(ep);
   GEMM_STAMP(2);
 }
 

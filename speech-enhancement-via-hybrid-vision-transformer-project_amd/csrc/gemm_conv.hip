@@ -24,6 +24,7 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
                                            "(no bias / epilogue, 16-byte aligned output)");
   if (thin_o1(g) && plain_epi && !bias && !bn_partials && (!epi || epi->act != HVIT_ACT_RELU))
     return hvit_thin_o1_fwd(dt, g, w_packed, y, y_dt, epi && epi->act == HVIT_ACT_TANH, (hipStream_t)stream);
+  HVIT_CHECK(!epi || epi->side.n <= 0, "hvit_conv_fwd: epilogue side jobs are for the linear entry points");
   Epi ep = to_epi(epi, y, y_dt, g->Cout);
   ep.bias = bias;
   ep.stats = bn_partials;

@@ -15,6 +15,9 @@
 
 using namespace hvit;
 
+extern "C" int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out,
+                                      void* stream);
+
 namespace {
 
 Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
@@ -53,6 +56,24 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
   ep.rowadd_mod = e->rowadd_rows > 0 ? e->rowadd_rows : 1;
   ep.colsum = e->colsum;
   return ep;
+}
+
+// the side job of a linear fwd / dgrad epilogue: handed to the GEMM kernels
+// (Epi::sj_*, float4 granules) when vector-aligned and the launch has rows,
+// else run here as its own reduction launch
+int take_side(const hvit_slab_sum_t* jp, Epi& ep, int M, hipStream_t st) {
+  if (!jp || jp->n <= 0) return HVIT_OK;
+  const hvit_slab_sum_t& j = *jp;
+  HVIT_CHECK(j.src && j.dst && j.splits > 0 && j.stride >= j.n, "epilogue side job: bad slabs");
+  if (M > 0 && j.n % 4 == 0 && j.stride % 4 == 0 && aligned16(j.src) && aligned16(j.dst)) {
+    ep.sj_src = j.src;
+    ep.sj_dst = j.dst;
+    ep.sj_n4 = (long)(j.n / 4);
+    ep.sj_stride4 = (long)(j.stride / 4);
+    ep.sj_splits = j.splits;
+    return HVIT_OK;
+  }
+  return hvit_sum_slabs_strided(j.src, j.splits, j.stride, j.n, j.dst, st);
 }
 
 int check_epi(const hvit_epilogue_t* e) {
@@ -216,7 +237,6 @@ bool thin_o1(const hvit_conv_geom_t* g) {
 }  // namespace
 
 int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats, hipStream_t st);
-int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream);
 int hvit_thin_c1_bn_tile_rows();
 long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g);
 int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,

@@ -11,6 +11,8 @@ extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float
   HVIT_CHECK(!epi || epi->act != HVIT_ACT_RELU, "hvit_linear_fwd: RELU is a conv-forward epilogue");
   Epi ep = to_epi(epi, y, y_dt, N);
   ep.bias = bias;
+  if (int rc = take_side(epi ? &epi->side : nullptr, ep, M, (hipStream_t)stream)) return rc;
+  if (M == 0) return HVIT_OK;
   if (dt == HVIT_BF16) {
     int rc = 0;
     if (try_ring(dense<bf16_t, true>(x, K, M, K), dense<bf16_t, true>(w, K, N, K), M, N, K, 1, ep,
@@ -32,6 +34,8 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
   if (int rc = check_epi(epi)) return rc;
   HVIT_CHECK(!epi || epi->act != HVIT_ACT_RELU, "hvit_linear_dgrad: RELU is a conv-forward epilogue");
   Epi ep = to_epi(epi, dx, dx_dt, K);
+  if (int rc = take_side(epi ? &epi->side : nullptr, ep, M, (hipStream_t)stream)) return rc;
+  if (M == 0) return HVIT_OK;
   if (dt == HVIT_BF16 && N % 8 == 0) {
     int rc = 0;
     if (try_ring(dense<bf16_t, true>(dy, N, M, N), dense<bf16_t, false>(w, K, K, N), M, K, N, 1, ep,
@@ -72,7 +76,8 @@ extern "C" long long hvit_wgrad_tickets(int M, int N, int K) {
 // over the token reduction); otherwise a column reduction of dy.
 static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                              float* ws, long long ws_elems, unsigned* tickets, long long tickets_elems, int flags,
-                             void* stream);
+                             void* stream, hvit_slab_sum_t* job = nullptr,
+                             const hvit_slab_sum_t* side = nullptr);
 
 extern "C" int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                                  float* ws, long long ws_elems, void* stream) {
@@ -85,17 +90,53 @@ extern "C" int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M
   return linear_wgrad_impl(dt, dy, x, M, N, K, dw, db, ws, ws_elems, tickets, tickets_elems, flags, stream);
 }
 
+extern "C" int hvit_linear_wgrad_defer(int dt, const void* dy, const void* x, int M, int N, int K, float* dw,
+                                       float* ws, long long ws_elems, const hvit_slab_sum_t* side,
+                                       hvit_slab_sum_t* job, void* stream) {
+  HVIT_CHECK(job, "hvit_linear_wgrad_defer: null job");
+  *job = hvit_slab_sum_t{nullptr, nullptr, 0, 0, 0};
+  return linear_wgrad_impl(dt, dy, x, M, N, K, dw, nullptr, ws, ws_elems, nullptr, 0, 0, stream, job, side);
+}
+
+// the split-K slab sum: deferred into *job when the caller asked, else launched
+static int slab_reduce(const float* ws, int splits, long long stride, long long n, float* out, void* stream,
+                       hvit_slab_sum_t* job) {
+  if (job) {
+    *job = hvit_slab_sum_t{ws, out, n, stride, splits};
+    return HVIT_OK;
+  }
+  return hvit_sum_slabs_strided(ws, splits, stride, n, out, stream);
+}
+
 static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                              float* ws, long long ws_elems, unsigned* tickets, long long tickets_elems, int flags,
-                             void* stream) {
+                             void* stream, hvit_slab_sum_t* job, const hvit_slab_sum_t* side) {
   HVIT_CHECK(dy && x && dw, "hvit_linear_wgrad: null pointer");
   HVIT_CHECK(M >= 0 && N > 0 && K > 0, "hvit_linear_wgrad: bad shape");
   HVIT_CHECK(aligned16(dy) && aligned16(x), "hvit_linear_wgrad: alignment");
   hipStream_t st = (hipStream_t)stream;
+  // a side job carried by this launch's GEMM kernels (epi_side); paths that
+  // launch none of them run it first as its own reduction
+  Epi sj;
+  if (int rc = take_side(side, sj, M, st)) return rc;
   const long long NK = (long long)N * K;
   int splits = wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN);
   if ((long long)splits * (NK + N) > ws_elems || !ws) splits = 1;
+  auto side_alone = [&]() -> int {
+    if (!sj.sj_n4) return HVIT_OK;
+    const int r = hvit_sum_slabs_strided(sj.sj_src, sj.sj_splits, sj.sj_stride4 * 4, sj.sj_n4 * 4, sj.sj_dst, stream);
+    sj.sj_n4 = 0;
+    return r;
+  };
+  auto carry = [&](Epi& e) {
+    e.sj_src = sj.sj_src;
+    e.sj_dst = sj.sj_dst;
+    e.sj_n4 = sj.sj_n4;
+    e.sj_stride4 = sj.sj_stride4;
+    e.sj_splits = sj.sj_splits;
+  };
   if (M == 0) {
+    if (int rc = side_alone()) return rc;
     (void)hipMemsetAsync(dw, 0, sizeof(float) * NK, st);
     if (db) (void)hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return HVIT_OK;
@@ -104,8 +145,10 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
   // over a chunk of rows; HVIT_WGRAD_SMALL=0 disables (A/B only)
   static const bool small_on = !getenv("HVIT_WGRAD_SMALL") || atoi(getenv("HVIT_WGRAD_SMALL"));
   if (small_on && !tickets && hvit_wgrad_small_ok(dt, M, N, K) && (!db || db == dw + NK) &&
-      ws_elems >= hvit_wgrad_small_ws(M, N, K))
+      ws_elems >= hvit_wgrad_small_ws(M, N, K)) {
+    if (int rc = side_alone()) return rc;
     return hvit_wgrad_small(dy, x, M, N, K, dw, db, ws, ws_elems, stream);
+  }
   // HVIT_NO_RS=1: bias grad by a separate column reduction (A/B measurements only)
   static const bool no_rs = getenv("HVIT_NO_RS") && atoi(getenv("HVIT_NO_RS"));
   const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK && !no_rs;
@@ -122,6 +165,7 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
     e.mode = s > 1 ? EPI_SLAB : EPI_STORE;
     e.out = s > 1 ? (void*)ws : (void*)dw;
     e.slab_stride = NK + N;
+    carry(e);
     // in-kernel reduction when the caller provides the ticket counters
     const bool tk = s > 1 && tickets && tickets_elems >= (long long)(N / r.bm) * (K / r.bn);
     if (tk) {
@@ -133,7 +177,7 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
     if (try_ring(dense<bf16_t, false>(dy, N, N, M), dense<bf16_t, false>(x, K, K, M), N, K, M, s, e, st, &rc, rcfg)) {
       if (rc) return rc;
       if (s > 1 && !tk)
-        if (int rc2 = hvit_sum_slabs_strided(ws, s, NK + N, NK, dw, stream)) return rc2;
+        if (int rc2 = slab_reduce(ws, s, NK + N, NK, dw, stream, job)) return rc2;
       if (db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
       return HVIT_OK;
     }
@@ -141,6 +185,7 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
   Epi ep;
   ep.out_dt = HVIT_F32;
   ep.ldo = K;
+  carry(ep);
   DT_DISPATCH(dt, {
     HVIT_CHECK(N % Elem<T>::PER16 == 0 && K % Elem<T>::PER16 == 0, "hvit_linear_wgrad: N, K alignment");
     splits = plan_splits<T>(M, splits);
@@ -157,7 +202,8 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
   });
   if (splits > 1) {
     // sums [dw | db] when fused (db follows dw), else dw alone
-    if (int rc = hvit_sum_slabs_strided(ws, splits, NK + N, fused_db ? NK + N : NK, dw, stream)) return rc;
+    if (int rc = slab_reduce(ws, splits, NK + N, fused_db ? NK + N : NK, dw, stream, fused_db ? nullptr : job))
+      return rc;
   }
   if (db && !fused_db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
   return HVIT_OK;

@@ -60,12 +60,16 @@ struct RingCore {
   }
 
   __device__ __forceinline__ static void run(const LdDense<bf16_t, KCA>& la, const LdDense<bf16_t, KCB>& lb, char* smem,
-                                             int m0, int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN]) {
+                                             int m0, int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN],
+                                             const Epi& ep) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
     const int nk = (kend - kbeg) / BK;
-    if (nk <= 0) return;
+    if (nk <= 0) {
+      epi_side(ep);
+      return;
+    }
     const __amdgpu_buffer_rsrc_t ra = rsrc(la), rb = rsrc(lb);
     const unsigned oa = (unsigned)(KCA ? ((long)m0 * la.ld + kbeg) * 2 : ((long)kbeg * la.ld + m0) * 2);
     const unsigned da = (unsigned)(KCA ? BK * 2 : (long)BK * la.ld * 2);
@@ -112,6 +116,8 @@ struct RingCore {
     // prologue: stages 0 .. NB-2 in flight
 #pragma unroll
     for (int t = 0; t < NB - 1; ++t) issue(t);
+    // a side job (epi_side) while the prologue stages are in flight
+    epi_side(ep);
     for (int t = 0; t < nk; ++t) {
       // stage t landed for this wave (NB-2 younger stages stay in flight) ...
       __builtin_amdgcn_s_waitcnt(vm_imm((NB - 2) * INFL));
@@ -197,7 +203,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  C::run(la, lb, smem, m0, n0, kbeg, kend, acc);
+  C::run(la, lb, smem, m0, n0, kbeg, kend, acc, ep);
 
   // ------------------------------------------------------------ epilogue ---
   const uint32_t dkey = epi_key(ep);

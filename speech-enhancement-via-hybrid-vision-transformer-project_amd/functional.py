@@ -283,6 +283,31 @@ def wgrad_tickets(M, N, K) -> int:
     return int(L.lib().hvit_wgrad_tickets(M, N, K))
 
 
+def linear_wgrad_deferred(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None, side: Optional[Deferred] = None):
+    if not DEFER:  # A/B: the two-launch form (an incoming side job summed first)
+        if side is not None:
+            call("hvit_sum_slabs_strided", side.job.src, side.job.splits, side.job.stride, side.job.n, side.job.dst,
+                 stream_ptr())
+        return linear_wgrad(dt, dy, x, M, N, K, tag=tag, dest=dest), None
+    """dw [N, K] = dy^T x (f32) with the split-K slab sum deferred: returns
+    (dw, Deferred); dw is final once the Deferred has been passed as the side
+    job of the next hvit_linear_fwd / _dgrad epilogue on this stream.
+    ``side``: an earlier launch's slabs for this launch to sum."""
+    dw = dest.view(N, K) if dest is not None else torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
+    job = L.SlabSum()
+
+    def launch():
+        call("hvit_linear_wgrad_defer", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), ws_n,
+             C.byref(side.job) if side is not None else None, C.byref(job), stream_ptr())
+
+    with timed(tag, 2.0 * M * N * K):
+        launch()
+    _record(tag, (launch, 2.0 * M * N * K))
+    return dw, Deferred(job, ws)
+
+
 def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=None, dest=None):
     """dw [N, K] = dy^T x (f32); with ``bias`` also db [N] = colsum(dy), which
     the bf16 path fuses into the GEMM (db stored right after dw).  ``tickets``
@@ -324,9 +349,22 @@ def dropout_scale(g, M, N, drop, rowscale, rps, out, colsum=None):
              L.dt_of(out), ptr(colsum), ptr(ws), ws_n, stream_ptr())
 
 
+class Deferred:
+    """A weight gradient whose split-K slab sum is handed to the next linear
+    launch on the stream (hvit_linear_wgrad_defer): ``job`` goes into that
+    launch's epilogue ``side``; ``ws`` (the slabs) is held until it is enqueued."""
+
+    __slots__ = ("job", "ws")
+
+    def __init__(self, job, ws):
+        self.job, self.ws = job, ws
+
+
 def epilogue(act=L.ACT_NONE, out2=None, aux=None, drop=None, resid=None, rowscale=None, rps=1, rowadd=None,
-             rowadd_rows=1, colsum=None):
+             rowadd_rows=1, colsum=None, side: Optional[Deferred] = None):
     e = L.Epilogue()
+    if side is not None:
+        e.side = side.job
     e.act = act
     e.out2 = ptr(out2)
     e.out2_dt = L.dt_of(out2) if out2 is not None else 0
@@ -537,6 +575,9 @@ C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfuse
 EVALFOLD = os.environ.get("HVIT_EVALFOLD", "1") != "0"  # A/B knob: 0 = eval convs keep z + bn_act
 KEEPBITS = os.environ.get("HVIT_KEEPBITS", "1") != "0"  # A/B knob: 0 = the attention backward re-hashes dropout
 LNDROP = os.environ.get("HVIT_LNDROP", "1") != "0"  # A/B knob: 0 = separate LayerNorm backward and dropout pass
+# A/B knob: 0 = ViT weight gradients reduce their split-K slabs in a launch of
+# their own and the qkv bias gradient is a column reduction of dqkv
+DEFER = os.environ.get("HVIT_DEFER", "1") != "0"
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
@@ -899,16 +940,19 @@ class ViTBlockFn(torch.autograd.Function):
             df2b = zf2b.take(dev)
             dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
         dq_id, dp_id, d1_id, d2_id = ctx.wid
-        df2w = linear_wgrad(dt, g2, a, M, D, hid, tag="vit_linear_wgrad", dest=grad_dest(*d2_id))
+        # each weight gradient's split-K slab sum rides on the data-gradient launch
+        # that follows it (epilogue side job): no reduction launch of its own
+        df2w, j2 = linear_wgrad_deferred(dt, g2, a, M, D, hid, dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
         df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
         with timed("vit_linear_dgrad", 2.0 * M * D * hid):
             call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
-                 epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b), s)
-        df1w = linear_wgrad(dt, dh, xn2, M, hid, D, tag="vit_linear_wgrad", dest=grad_dest(*d1_id))
+                 epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b, side=j2), s)
+        df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id))
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_dgrad", 2.0 * M * hid * D):
-            call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32, None, s)
+            call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
+                 epilogue(side=j1), s)
         if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass
             dx1, dn2w, dn2b, g1, dpb = _ln_bwd_drop(dxn2, x1, m2, r2, n2w, dx2, zln2, drp, rs1, Nt, dt)
         else:
@@ -917,28 +961,26 @@ class ViTBlockFn(torch.autograd.Function):
             dpb = zpb.take(dev)
             dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
         # attention branch
-        dpw = linear_wgrad(dt, g1, o, M, D, D, tag="vit_linear_wgrad", dest=grad_dest(*dp_id))
+        dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id))
         do = _empty((M, D), dt, dev)
         with timed("vit_linear_dgrad", 2.0 * M * D * D):
-            call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, None, s)
+            call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, epilogue(side=jp), s)
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
+        # the qkv bias grad: per-workgroup partial column sums of dqkv written by
+        # the attention backward, summed as the qkv weight-gradient launch's side job
+        nbr = L.lib().hvit_mhsa_bias_rows(dt, B, Nt, H, D // H)
+        bparts = torch.empty((nbr, 3 * D), dtype=torch.float32, device=dev)
+        dqkvb = torch.empty(3 * D, dtype=torch.float32, device=dev)
         with timed("attn_bwd", 8.0 * B * H * Nt * Nt * (D // H)):
-            if ctx.kbits is not None:
-                call("hvit_mhsa_bwd_kb", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
-                     D // H, scale, dra, ctx.kbits.data_ptr(), dqkv.data_ptr(), delta.data_ptr(), s)
-            else:
-                call("hvit_mhsa_bwd", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
-                     D // H, scale, dra, dqkv.data_ptr(), delta.data_ptr(), s)
-        # qkv bias grad by a column reduction: the wgrad GEMM variant with fused
-        # A-row sums spills at 128x128 (rocprof: 42 -> 28 us class without it)
-        dqkvw = linear_wgrad(dt, dqkv, xn1, M, 3 * D, D, tag="vit_linear_wgrad", dest=grad_dest(*dq_id))
-        dqkvb = zqb.take(dev)
-        call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
+            call("hvit_mhsa_bwd_db", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
+                 D // H, scale, dra, ptr(ctx.kbits), dqkv.data_ptr(), delta.data_ptr(), bparts.data_ptr(), s)
+        jb = Deferred(L.SlabSum(bparts.data_ptr(), dqkvb.data_ptr(), 3 * D, 3 * D, nbr), bparts)
+        dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_dgrad", 2.0 * M * 3 * D * D):
-            call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32, None,
-                 s)
+            call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32,
+                 epilogue(side=jq), s)
         if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
             dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         else:

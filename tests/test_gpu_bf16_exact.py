@@ -170,6 +170,48 @@ def test_linear_wgrad_exact(env, cfg, N, K):
     assert int(tk.count_nonzero()) == 0
 
 
+@pytest.mark.parametrize("cfg", [-1, 0])
+@pytest.mark.parametrize("N,K", [(D, HID), (HID, D), (D, D), (3 * D, D)])
+def test_linear_wgrad_deferred_side_job(env, cfg, N, K):
+    """hvit_linear_wgrad_defer leaves the split-K slabs; the next linear
+    launch's epilogue side job sums them: dw bit-identical to the two-launch
+    hvit_linear_wgrad, and the carrying dgrad's own output unchanged (fwd and
+    dgrad carriers; also the M = 0 carrier, which runs the sum as its own
+    launch)."""
+    L, HF = env
+    L.lib().hvit_gemm_tune(0, cfg)
+    torch.manual_seed(4)
+    dy, x = rb(M, N), rb(M, K)
+    want = HF.linear_wgrad(L.BF16, dy, x, M, N, K)
+    g, w = rb(M, D), rb(D, D, scale=D ** -0.5)
+    out_ref = torch.empty(M, D, device=DEV, dtype=torch.float32)
+    L.call("hvit_linear_dgrad", L.BF16, g.data_ptr(), w.data_ptr(), M, D, D, out_ref.data_ptr(), L.F32, None, s())
+    for carrier in ("dgrad", "fwd", "empty"):
+        dw, job = HF.linear_wgrad_deferred(L.BF16, dy, x, M, N, K)
+        out = torch.empty_like(out_ref)
+        if carrier == "dgrad":
+            L.call("hvit_linear_dgrad", L.BF16, g.data_ptr(), w.data_ptr(), M, D, D, out.data_ptr(), L.F32,
+                   HF.epilogue(side=job), s())
+            assert torch.equal(out, out_ref)
+        elif carrier == "fwd":
+            L.call("hvit_linear_fwd", L.BF16, g.data_ptr(), w.data_ptr(), None, M, D, D, out.data_ptr(), L.F32,
+                   HF.epilogue(side=job), s())
+        else:
+            L.call("hvit_linear_fwd", L.BF16, g.data_ptr(), w.data_ptr(), None, 0, D, D, out.data_ptr(), L.F32,
+                   HF.epilogue(side=job), s())
+        torch.cuda.synchronize()
+        assert job.job.n in (0, N * K)
+        assert torch.equal(dw, want), f"{carrier}: {(dw - want).abs().max().item()}"
+    # a deferred weight gradient carrying another one's slabs (the model's
+    # attention bias partials ride on the qkv weight gradient this way)
+    dw1, j1 = HF.linear_wgrad_deferred(L.BF16, dy, x, M, N, K)
+    dw2, j2 = HF.linear_wgrad_deferred(L.BF16, dy, x, M, N, K, side=j1)
+    L.call("hvit_linear_dgrad", L.BF16, g.data_ptr(), w.data_ptr(), M, D, D, out.data_ptr(), L.F32,
+           HF.epilogue(side=j2), s())
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, want) and torch.equal(dw2, want)
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 256, 512), (8192, 256, 256), (32768, 128, 128), (131072, 64, 64),
                                    (1000, 64, 128)])
 def test_linear_wgrad_small_with_bias_exact(env, M, N, K):

@@ -405,6 +405,45 @@ def test_mhsa_keep_bits_equal_rehash(hv, B, N, H, p):
         assert np.array_equal(got.astype(bool), keep[:, :, key]), key
 
 
+@pytest.mark.parametrize("B,N,H,p,kb", [(4, 256, 8, 0.1, True), (3, 100, 2, 0.0, False), (2, 300, 2, 0.1, False)])
+def test_mhsa_bwd_fused_qkv_bias(hv, B, N, H, p, kb):
+    """hvit_mhsa_bwd_db: dqkv bit-identical to hvit_mhsa_bwd(_kb), and the sum of
+    its partial bias rows equal to the f32 column sums of dqkv over the B*N
+    tokens (the qkv bias gradient).  The kernel sums the unrounded f32 gradients, the
+    check sums the bf16-rounded dqkv: bar = bf16 half-ulp of the column's
+    absolute sum (N=300 takes the flash-style kernels + column reduction)."""
+    l = L(hv)
+    hd, D = 64, H * 64
+    qkv = (torch.randn(B * N, 3 * D, device=DEV) * 0.7).to(torch.bfloat16)
+    go = torch.randn(B * N, D, device=DEV).to(torch.bfloat16)
+    dr = l.dropout(p, 5, 41) if p > 0 else None
+    o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    bits = torch.zeros(l.lib().hvit_mhsa_keep_bits_elems(B, N, H), dtype=torch.int32, device=DEV) if kb else None
+    if kb:
+        l.call("hvit_mhsa_fwd_kb", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+               bits.data_ptr(), s())
+    else:
+        l.call("hvit_mhsa_fwd", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+               None, s())
+    ref = torch.empty_like(qkv)
+    delta = torch.empty(B, H, N, device=DEV)
+    l.call("hvit_mhsa_bwd", l.BF16, qkv.data_ptr(), o.data_ptr(), go.data_ptr(), lse.data_ptr(), B, N, H, hd,
+           hd ** -0.5, dr, ref.data_ptr(), delta.data_ptr(), s())
+    got = torch.empty_like(qkv)
+    rows = l.lib().hvit_mhsa_bias_rows(l.BF16, B, N, H, hd)
+    parts = torch.full((rows, 3 * D), float("nan"), device=DEV)  # every row is written
+    l.call("hvit_mhsa_bwd_db", l.BF16, qkv.data_ptr(), o.data_ptr(), go.data_ptr(), lse.data_ptr(), B, N, H, hd,
+           hd ** -0.5, dr, bits.data_ptr() if kb else None, got.data_ptr(), delta.data_ptr(), parts.data_ptr(), s())
+    db = torch.empty(3 * D, device=DEV)
+    l.call("hvit_sum_slabs_strided", parts.data_ptr(), rows, 3 * D, 3 * D, db.data_ptr(), s())
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    want = ref.float().sum(0)
+    bar = ref.float().abs().sum(0) * 2.0 ** -8 + 1e-5
+    assert ((db - want).abs() <= bar).all(), float(((db - want).abs() / bar).max())
+
+
 # ------------------------------------------------------------- layernorm ---
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("M,D", [(8192, 512), (37, 64), (16, 768)])

@@ -47,6 +47,13 @@ def main(p=0.1):
                               delta.data_ptr(), st())
         us = timeit(bwdk)
         print(f"mhsa bwd_kb p={p}: {us:7.1f} us  {2 * fl / us / 1e6:6.1f} TF/s", flush=True)
+        rows = L.lib().hvit_mhsa_bias_rows(L.BF16, B, N, H, hd)
+        parts = torch.empty(rows, 3 * D, device="cuda")
+        bwdb = lambda: L.call("hvit_mhsa_bwd_db", L.BF16, qkv.data_ptr(), o.data_ptr(), do.data_ptr(),  # noqa
+                              lse.data_ptr(), B, N, H, hd, hd ** -0.5, dr, kb.data_ptr(), dqkv.data_ptr(),
+                              delta.data_ptr(), parts.data_ptr(), st())
+        us = timeit(bwdb)
+        print(f"mhsa bwd_kb+bias p={p}: {us:7.1f} us  {2 * fl / us / 1e6:6.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
