@@ -611,7 +611,10 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK32);
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
-  // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q), log2 units
+  // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q) in log2 units
+  // (keys >= N of the last, partial tile masked to -inf).  VALU diet: the 1/sum
+  // and the dropout 1/(1-p) on the 16 outputs instead of the 64
+  // probabilities, the dropout mask a select, masking only in a partial tile.
   f32x4 st[V2_KMAX / 16];
   float mx = -INFINITY;
 #pragma unroll
@@ -620,24 +623,32 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       a = v2_mma32(v2_fragj(Ks, LN, j, 0), qf[0], a);
       a = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], a);
+      if (16 * j + 16 > N) {  // wave-uniform: only a partial last tile
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = (16 * j + 4 * fq + r < N) ? a[r] * c2 : -INFINITY;
-        a[r] = v;
-        mx = fmaxf(mx, v);
+        a[r] *= c2;
+        mx = fmaxf(mx, a[r]);
       }
       st[j] = a;
     }
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  // (exp2(fma(s, c2, -mx c2)) on the raw scores measured run-to-run
+  // nondeterministic at the bf16-ulp level in this kernel -- tools/det_check.py
+  // -- so the scores are scaled first, as before)
+  const float mxc = mx;  // the max in log2 units
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < V2_KMAX / 16; ++j) {
     if (j < nkt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = __builtin_amdgcn_exp2f(st[j][r] - mx);
+        const float p = __builtin_amdgcn_exp2f(st[j][r] - mxc);
         st[j][r] = p;
         sum += p;
       }
@@ -657,22 +668,29 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   // keep bits for the backward (kbits non-null): bit 8*jp + 4*e + r of this
   // lane's word pair = keep(q, key 32*jp + 16*e + 4*fq + r)
   uint32_t kb[2] = {0u, 0u};
+  const uint32_t rk = rng_key(seed, site);
+  const uint64_t qrow = (bh * N + (q < N ? q : 0)) * (uint64_t)N;
 #pragma unroll
   for (int jp = 0; jp < V2_KMAX / 32; ++jp) {
     if (2 * jp < nkt) {
-      f32x4 p0 = st[2 * jp] * inv;
-      f32x4 p1 = (2 * jp + 1 < nkt) ? st[2 * jp + 1] * inv : (f32x4){0.f, 0.f, 0.f, 0.f};
+      f32x4 p0 = st[2 * jp];
+      f32x4 p1 = (2 * jp + 1 < nkt) ? st[2 * jp + 1] : (f32x4){0.f, 0.f, 0.f, 0.f};
       if (thr) {
-        const f32x4 k0 = v2_keep(bh, N, q < N ? q : 0, 32 * jp + 4 * fq, thr, dscale, seed, site);
-        p0 *= k0;
         uint32_t b8 = 0u;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) b8 |= (k0[r] != 0.f ? 1u : 0u) << r;
-        if (2 * jp + 1 < nkt) {
-          const f32x4 k1 = v2_keep(bh, N, q < N ? q : 0, 32 * jp + 16 + 4 * fq, thr, dscale, seed, site);
-          p1 *= k1;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) b8 |= (k1[r] != 0.f ? 1u : 0u) << (4 + r);
+        for (int e = 0; e < 2; ++e) {
+          if (2 * jp + e < nkt) {
+            const uint64_t i0 = qrow + 32 * jp + 16 * e + 4 * fq;
+            const uint32_t h0 = rng_pair(rk, i0), h1 = rng_pair(rk, i0 + 2);
+            const bool k0 = (h0 & 0xffffu) >= thr, k1 = (h0 >> 16) >= thr;
+            const bool k2 = (h1 & 0xffffu) >= thr, k3 = (h1 >> 16) >= thr;
+            f32x4& pp = e ? p1 : p0;
+            pp[0] = k0 ? pp[0] : 0.f;
+            pp[1] = k1 ? pp[1] : 0.f;
+            pp[2] = k2 ? pp[2] : 0.f;
+            pp[3] = k3 ? pp[3] : 0.f;
+            b8 |= ((uint32_t)k0 | ((uint32_t)k1 << 1) | ((uint32_t)k2 << 2) | ((uint32_t)k3 << 3)) << (4 * e);
+          }
         }
         kb[jp >> 2] |= b8 << (8 * (jp & 3));
       }
@@ -682,15 +700,16 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
     }
   }
   if (q < N) {
+    const float os = thr ? inv * dscale : inv;
     bf16_t* op = o + ((long)b * N + q) * D + h * 64;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       uint2 u;
-      u.x = f2bf2(ot[t][0], ot[t][1]);
-      u.y = f2bf2(ot[t][2], ot[t][3]);
+      u.x = f2bf2(ot[t][0] * os, ot[t][1] * os);
+      u.y = f2bf2(ot[t][2] * os, ot[t][3] * os);
       *(uint2*)(op + 16 * t + 4 * fq) = u;
     }
-    if (fq == 0) lse[bh * N + q] = (mx + log2f(sum)) * 0.6931471805599453f;
+    if (fq == 0) lse[bh * N + q] = (mxc + log2f(sum)) * 0.6931471805599453f;
     if (kbits && thr) *(uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2) = make_uint2(kb[0], kb[1]);
   }
 }
@@ -808,12 +827,18 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
       } else if (thr) {
         keep = v2_keep(bh, N, qv ? q : 0, (16 * j + 4 * fq) < N ? 16 * j + 4 * fq : 0, thr, dscale, seed, site);
       }
+      // queries >= N need no mask (q = dO = 0 there: dS = 1 * (0 - 0)); keys
+      // >= N only in a partial last tile (wave-uniform branch)
+      f32x4 p;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool valid = qv && (16 * j + 4 * fq + r < N);
-        const float p = valid ? __builtin_amdgcn_exp2f(s[r] * c2 - lse2) : 0.f;
-        ds2[u][r] = p * (dp[r] * keep[r] - dl);
+      for (int r = 0; r < 4; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2));
+      if (16 * j + 16 > N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * j + 4 * fq + r >= N) p[r] = 0.f;
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds2[u][r] = p[r] * fmaf(dp[r], keep[r], -dl);
     }
     const u32x4 db = v2_cat(v2_pack(ds2[0]), v2_pack(ds2[1]));
 #pragma unroll
@@ -915,23 +940,34 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
         hlo = rng_pair(rk, idx);      // keys (key & ~3) + 0, 1
         hhi = rng_pair(rk, idx + 2);  // keys (key & ~3) + 2, 3
       }
+      // keys >= N (lanes of a partial last key block: k = v = 0 there, S = 0):
+      // masked once per lane (kv); queries >= N only in a partial last tile
+      // (wave-uniform branch; their Ls / Dl rows are 0)
+      const f32x4 l4 = *(const f32x4*)(Ls + 16 * j + 4 * fq);
+      const f32x4 d4 = *(const f32x4*)(Dl + 16 * j + 4 * fq);
+      f32x4 p;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = kv ? __builtin_amdgcn_exp2f(fmaf(s[r], c2, -l4[r])) : 0.f;
+      if (16 * j + 16 > N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * j + 4 * fq + r >= N) p[r] = 0.f;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qi = 16 * j + 4 * fq + r;
-        const bool valid = kv && qi < N;
-        const float p = valid ? __builtin_amdgcn_exp2f(s[r] * c2 - Ls[qi]) : 0.f;
         float kp = 1.f;
         if (use_kb) {
-          kp = (valid && ((Kb[(qi < N ? qi : 0) * 8 + kword] >> kshift) & 1u)) ? dscale : 0.f;
+          kp = ((Kb[(qi < N ? qi : 0) * 8 + kword] >> kshift) & 1u) ? dscale : 0.f;
         } else if (thr) {
           const int src = (lane & ~3) | r;
           const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
           const uint32_t word = (key & 2) ? hi : lo;
           const uint32_t u16 = (key & 1) ? (word >> 16) : (word & 0xffffu);
-          kp = (valid && u16 >= thr) ? dscale : 0.f;
+          kp = u16 >= thr ? dscale : 0.f;
         }
-        pd2[u][r] = p * kp;
-        ds2[u][r] = p * (dp[r] * kp - Dl[qi]);
+        pd2[u][r] = p[r] * kp;
+        ds2[u][r] = p[r] * fmaf(dp[r], kp, -d4[r]);
       }
     }
     // dV^T[d][key] += dO^T[d][q] P~[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
