@@ -497,6 +497,55 @@ __device__ __forceinline__ void load_ncb(const TD* p, float* v) {
     for (int e = 0; e < NCB; ++e) v[e] = p[e];
   }
 }
+// the same NCB channels as raw bits, converted at their use: the load of the
+// next window group is issued before the current one's arithmetic (the dy
+// stream was latency-bound: one dependent HBM round trip per group)
+template <typename TD, int NCB>
+struct RawNcb {
+  float v[NCB];
+  __device__ __forceinline__ void load(const TD* p) {
+#pragma unroll
+    for (int e = 0; e < NCB; ++e) v[e] = p[e];
+  }
+  __device__ __forceinline__ void get(float* o) const {
+#pragma unroll
+    for (int e = 0; e < NCB; ++e) o[e] = v[e];
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int e = 0; e < NCB; ++e) v[e] = 0.f;
+  }
+};
+template <>
+struct RawNcb<bf16_t, 4> {
+  uint2 q;
+  __device__ __forceinline__ void load(const bf16_t* p) { q = *(const uint2*)p; }
+  __device__ __forceinline__ void get(float* o) const {
+    o[0] = __uint_as_float(q.x << 16);
+    o[1] = __uint_as_float(q.x & 0xffff0000u);
+    o[2] = __uint_as_float(q.y << 16);
+    o[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+  __device__ __forceinline__ void zero() { q = make_uint2(0u, 0u); }
+};
+template <>
+struct RawNcb<bf16_t, 2> {
+  uint32_t q;
+  __device__ __forceinline__ void load(const bf16_t* p) { q = *(const uint32_t*)p; }
+  __device__ __forceinline__ void get(float* o) const {
+    o[0] = __uint_as_float(q << 16);
+    o[1] = __uint_as_float(q & 0xffff0000u);
+  }
+  __device__ __forceinline__ void zero() { q = 0u; }
+};
+template <>
+struct RawNcb<bf16_t, 1> {
+  bf16_t q;
+  __device__ __forceinline__ void load(const bf16_t* p) { q = *p; }
+  __device__ __forceinline__ void get(float* o) const { o[0] = bf2f(q); }
+  __device__ __forceinline__ void zero() { q = 0; }
+};
+
 template <typename TO, int NCB>
 __device__ __forceinline__ void store_ncb(TO* p, const float* v) {
   if constexpr (sizeof(TO) == 2) {
@@ -602,14 +651,27 @@ __global__ __launch_bounds__(THREADS) void c1m_sums_kernel(Args a_, const TD* __
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) s1[cb] = s2[cb] = 0.f;
   const int nwin = min(a.RB, Ho - oy0) * Wo;
+  // dy of group g for this lane (window 4g + (l >> 4)), one group ahead
+  auto issue = [&](int g, RawNcb<TD, NCB>& raw) {
+    const int it = 4 * g + (l >> 4);
+    if (4 * g < nwin && it < nwin) {
+      const int r = it / Wo, ox = it - r * Wo;
+      raw.load(dy + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c0);
+    } else {
+      raw.zero();
+    }
+  };
+  RawNcb<TD, NCB> nxt;
+  issue(wv, nxt);
   for (int g = wv; 4 * g < nwin; g += THREADS / 64) {
+    const RawNcb<TD, NCB> cur = nxt;
+    issue(g + THREADS / 64, nxt);
     f32x4 z[NCB];
     group_z<NCB>(xs, pitch, g, nwin, Wo, l, bw, z);
     const int it = 4 * g + (l >> 4);
     if (it < nwin) {
-      const int r = it / Wo, ox = it - r * Wo;
       float d[NCB];
-      load_ncb<TD, NCB>(dy + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c0, d);
+      cur.get(d);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
         int arg;
@@ -677,9 +739,25 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
   const int m = l & 15;
   const int mo = m < 9 ? (m / 3) * pitch + m % 3 : 0;
   const int nwin = min(a.RB, Hw - oy0) * Ww;
+  // dy of group g for this lane (zero outside the full windows), issued one
+  // iteration (two groups) ahead
+  auto issue = [&](int g, RawNcb<TD, NCB>& raw) {
+    const int it = 4 * g + (l >> 4);
+    const int itc = min(it, nwin - 1);
+    const int r = itc / Ww, ox = itc - r * Ww;
+    const int oy = oy0 + r;
+    if (it < nwin && oy < Ho && ox < Wo) raw.load(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c0);
+    else raw.zero();
+  };
+  RawNcb<TD, NCB> nxt[2];
+  issue(2 * wv, nxt[0]);
+  issue(2 * wv + 1, nxt[1]);
   for (int g0 = 2 * wv; 4 * g0 < nwin; g0 += 2 * (THREADS / 64)) {
     u32x4 bhi[NCB], blo[NCB];
     float xa[8];
+    const RawNcb<TD, NCB> cur[2] = {nxt[0], nxt[1]};
+    issue(g0 + 2 * (THREADS / 64), nxt[0]);
+    issue(g0 + 2 * (THREADS / 64) + 1, nxt[1]);
 #pragma unroll
     for (int gs = 0; gs < 2; ++gs) {
       const int g = g0 + gs;
@@ -690,11 +768,8 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
       const int itc = min(it, nwin - 1);
       const int r = itc / Ww, ox = itc - r * Ww;
       const int oy = oy0 + r;
-      const bool full = valid && oy < Ho && ox < Wo;
       float d[NCB];
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) d[cb] = 0.f;
-      if (full) load_ncb<TD, NCB>(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c0, d);
+      cur[gs].get(d);
       // the lane's 4 pixels: inside the image and inside the block's windows?
       float inb[4];
 #pragma unroll

@@ -578,6 +578,9 @@ LNDROP = os.environ.get("HVIT_LNDROP", "1") != "0"  # A/B knob: 0 = separate Lay
 # A/B knob: 0 = ViT weight gradients reduce their split-K slabs in a launch of
 # their own and the qkv bias gradient is a column reduction of dqkv
 DEFER = os.environ.get("HVIT_DEFER", "1") != "0"
+# A/B knob: 0 = the qkv bias gradient by a column reduction of dqkv after the
+# attention backward (instead of the backward's per-workgroup partial sums)
+ATTN_DB = os.environ.get("HVIT_ATTN_DB", "1") != "0"
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
@@ -969,13 +972,23 @@ class ViTBlockFn(torch.autograd.Function):
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         # the qkv bias grad: per-workgroup partial column sums of dqkv written by
         # the attention backward, summed as the qkv weight-gradient launch's side job
-        nbr = L.lib().hvit_mhsa_bias_rows(dt, B, Nt, H, D // H)
-        bparts = torch.empty((nbr, 3 * D), dtype=torch.float32, device=dev)
-        dqkvb = torch.empty(3 * D, dtype=torch.float32, device=dev)
-        with timed("attn_bwd", 8.0 * B * H * Nt * Nt * (D // H)):
-            call("hvit_mhsa_bwd_db", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
-                 D // H, scale, dra, ptr(ctx.kbits), dqkv.data_ptr(), delta.data_ptr(), bparts.data_ptr(), s)
-        jb = Deferred(L.SlabSum(bparts.data_ptr(), dqkvb.data_ptr(), 3 * D, 3 * D, nbr), bparts)
+        jb = None
+        # (the register-resident bf16 kernels: hd 64, N <= 256, N % 4 == 0; other
+        # shapes keep the column reduction)
+        if ATTN_DB and dt == BF16 and D // H == 64 and Nt <= 256 and Nt % 4 == 0:
+            nbr = L.lib().hvit_mhsa_bias_rows(dt, B, Nt, H, D // H)
+            bparts = torch.empty((nbr, 3 * D), dtype=torch.float32, device=dev)
+            dqkvb = torch.empty(3 * D, dtype=torch.float32, device=dev)
+            with timed("attn_bwd", 8.0 * B * H * Nt * Nt * (D // H)):
+                call("hvit_mhsa_bwd_db", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
+                     D // H, scale, dra, ptr(ctx.kbits), dqkv.data_ptr(), delta.data_ptr(), bparts.data_ptr(), s)
+            jb = Deferred(L.SlabSum(bparts.data_ptr(), dqkvb.data_ptr(), 3 * D, 3 * D, nbr), bparts)
+        else:
+            with timed("attn_bwd", 8.0 * B * H * Nt * Nt * (D // H)):
+                call("hvit_mhsa_bwd_db", dt, qkv.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(), B, Nt, H,
+                     D // H, scale, dra, ptr(ctx.kbits), dqkv.data_ptr(), delta.data_ptr(), None, s)
+            dqkvb = zqb.take(dev)
+            call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
         dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_dgrad", 2.0 * M * 3 * D * D):

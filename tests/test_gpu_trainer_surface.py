@@ -187,14 +187,15 @@ def test_train_step_cuda_graph_capture(hv):
     assert any(not torch.equal(p.detach(), q) for p, q in zip(ma.parameters(), p0))
 
 
-def test_train_step_graph_with_dropout_and_device_counters(hv):
+@pytest.mark.parametrize("kw", [KW, dict(KW, embed_dim=128, num_heads=2)], ids=["hd16", "hd64"])
+def test_train_step_graph_with_dropout_and_device_counters(hv, kw):
     """The bench's graph mode: a whole bf16 train step WITH dropout (p = 0.1
     everywhere, DropPath 0.1) and FusedAdamW(capturable=True) captured once and
     replayed.  The dropout seed stream and the AdamW step counters live on the
     device, so every replay draws new masks and applies its own bias
     corrections: the parameters after each replay match an eager copy driven
     through the same number of steps from the same seed state."""
-    kw = dict(KW, precision="bf16")
+    kw = dict(kw, precision="bf16")
     torch.manual_seed(0)
     ma = hv.HybridViT(**kw).to(DEV).train()
     mb = copy.deepcopy(ma)
