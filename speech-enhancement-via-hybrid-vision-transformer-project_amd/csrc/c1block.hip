@@ -54,6 +54,14 @@ __device__ __forceinline__ float ldv(const void* p, long i) {
   return Elem<T>::to_f(((const T*)p)[i]);
 }
 
+// row and column of window `it` among rows of `w` windows, for it < 4 * w (a
+// workgroup owns RB <= 4 rows): compares instead of an integer division (a
+// ~25-instruction VALU sequence per use in these VALU-bound loops)
+__device__ __forceinline__ void win_rc(int it, int w, int& r, int& ox) {
+  r = (it >= w ? 1 : 0) + (it >= 2 * w ? 1 : 0) + (it >= 3 * w ? 1 : 0);
+  ox = it - r * w;
+}
+
 // rows [y_lo, y_lo + nrows) of sample n, `pitch` floats each: column c holds
 // x = c - 1 (zero outside [0, W)); rows outside the image are zeros.  Loads go
 // out in batches of UB per thread (one load -> store chain per element would
@@ -206,7 +214,8 @@ __global__ __launch_bounds__(THREADS) void c1_apply_kernel(Args a_, TO* __restri
   drop_cv<CV>(a, n, c, m);
   const int rows = min(a.RB, Ho - oy0);
   for (int it = threadIdx.x / CC; it < rows * Wo; it += lanes) {
-    const int r = it / Wo, ox = it - r * Wo;
+    int r, ox;
+    win_rc(it, Wo, r, ox);
     float pt[P + 2][P + 2];
     load_patch<P>(xs, pitch, r, ox, pt);
     float best[CV];
@@ -273,7 +282,8 @@ __global__ __launch_bounds__(THREADS) void c1_sums_kernel(Args a_, const TD* __r
   for (int e = 0; e < CV; ++e) acc1[e] = acc2[e] = 0.f;
   const int rows = min(a.RB, Ho - oy0);
   for (int it = threadIdx.x / CC; it < rows * Wo; it += lanes) {
-    const int r = it / Wo, ox = it - r * Wo;
+    int r, ox;
+    win_rc(it, Wo, r, ox);
     float d[CV];
     load_cv<TD, CV>(dy + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c, d);
     float pt[P + 2][P + 2];
@@ -361,7 +371,8 @@ __global__ __launch_bounds__(THREADS) void c1_bwd_kernel(Args a_, const TD* __re
     for (int e = 0; e < CV; ++e) acc[t][e] = 0.f;
   const int rows = min(a.RB, Hw - oy0);
   for (int it = threadIdx.x / CC; it < rows * Ww; it += lanes) {
-    const int r = it / Ww, ox = it - r * Ww;
+    int r, ox;
+    win_rc(it, Ww, r, ox);
     const int oy = oy0 + r;
     const bool full = oy < Ho && ox < Wo;
     float d[CV];
@@ -566,7 +577,8 @@ __device__ __forceinline__ void group_z(const float* xs, int pitch, int g, int n
                                         const u32x4 (&bw)[NCB], f32x4 (&z)[NCB]) {
   const int row = l & 15;
   const int it = min(4 * g + (row >> 2), nwin - 1);
-  const int r = it / ww, ox = it - r * ww;
+  int r, ox;
+  win_rc(it, ww, r, ox);
   const float* b = xs + (r * 2 + ((row & 3) >> 1)) * pitch + ox * 2 + (row & 1);
   float t[9];
 #pragma unroll
@@ -614,7 +626,8 @@ __global__ __launch_bounds__(THREADS) void c1m_apply_kernel(Args a_, TO* __restr
     group_z<NCB>(xs, pitch, g, nwin, Wo, l, bw, z);
     const int it = 4 * g + (l >> 4);
     if (it < nwin) {
-      const int r = it / Wo, ox = it - r * Wo;
+      int r, ox;
+    win_rc(it, Wo, r, ox);
       float o[NCB];
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
@@ -655,7 +668,8 @@ __global__ __launch_bounds__(THREADS) void c1m_sums_kernel(Args a_, const TD* __
   auto issue = [&](int g, RawNcb<TD, NCB>& raw) {
     const int it = 4 * g + (l >> 4);
     if (4 * g < nwin && it < nwin) {
-      const int r = it / Wo, ox = it - r * Wo;
+      int r, ox;
+    win_rc(it, Wo, r, ox);
       raw.load(dy + (((long)n * Ho + oy0 + r) * Wo + ox) * a.C + c0);
     } else {
       raw.zero();
@@ -744,7 +758,8 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
   auto issue = [&](int g, RawNcb<TD, NCB>& raw) {
     const int it = 4 * g + (l >> 4);
     const int itc = min(it, nwin - 1);
-    const int r = itc / Ww, ox = itc - r * Ww;
+    int r, ox;
+    win_rc(itc, Ww, r, ox);
     const int oy = oy0 + r;
     if (it < nwin && oy < Ho && ox < Wo) raw.load(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c0);
     else raw.zero();
@@ -766,7 +781,8 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
       const int it = 4 * g + (l >> 4);
       const bool valid = it < nwin;
       const int itc = min(it, nwin - 1);
-      const int r = itc / Ww, ox = itc - r * Ww;
+      int r, ox;
+    win_rc(itc, Ww, r, ox);
       const int oy = oy0 + r;
       float d[NCB];
       cur[gs].get(d);
@@ -784,7 +800,7 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float gq = arg == q ? gv : 0.f;
-          dz[q] = inb[q] * (training ? k.sc[cb] * gq + ca[cb] + cbz[cb] * z[cb][q] : k.sc[cb] * gq);
+          dz[q] = inb[q] * fmaf(cbz[cb], z[cb][q], fmaf(k.sc[cb], gq, ca[cb]));  // ca = cbz = 0 in eval
         }
         float lo[4];
 #pragma unroll
@@ -950,7 +966,7 @@ int make_args(Args& a, int dt, const hvit_conv_geom_t* g, const void* w, const f
   a.W = g->Ws;
   a.C = g->Cout;
   a.RB = rows_per_block(g->Ws, pool);
-  HVIT_CHECK(a.RB >= 1, "c1block: W=%d too wide for the staged rows", g->Ws);
+  HVIT_CHECK(a.RB >= 1 && a.RB <= 4, "c1block: W=%d too wide for the staged rows", g->Ws);  // win_rc: RB <= 4
   a.mean = mean;
   a.invstd = invstd;
   a.gamma = gamma;
