@@ -11,6 +11,8 @@
 //   reduce pass: sums[0][c] = sum g, sums[1][c] = sum g * xhat  (dbeta, dgamma)
 //   apply pass : dz = gamma * invstd * (g - sum g / M - xhat * sum g*xhat / M)
 // Window / pixel indices stay in 32 bits.
+#include <algorithm>
+
 #include "common.h"
 
 namespace hvit {
@@ -46,6 +48,8 @@ struct BnArgs {
   const unsigned long long* seedp;  // device seed word (hvit_dropout_t.seed_ptr)
   unsigned long long seed;
   uint32_t site;
+  // index divisors: channel groups, full windows (Wo, Ho), all windows (Ww, Hw)
+  FastDiv fG, fWo, fHo, fWw, fHw;
   // at kernel entry: fold in the device seed word (one scalar load)
   __device__ __forceinline__ void resolve() {
     if (seedp && thr) key = rng_key(seed ^ *seedp, site);
@@ -105,11 +109,11 @@ __global__ __launch_bounds__(256) void bnact_fwd_kernel(const T* __restrict__ z,
     sh[e] = be_[e] - mu_[e] * sc[e];
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    int t = i / G;
-    const int ox = t % Wo;
-    t /= Wo;
-    const int oy = t % Ho;
-    const int n = t / Ho;
+    const int t = a.fG.div(i);
+    const int t1 = a.fWo.div(t);
+    const int ox = t - t1 * Wo;
+    const int n = a.fHo.div(t1);
+    const int oy = t1 - n * Ho;
     float best[CV];
 #pragma unroll
     for (int e = 0; e < CV; ++e) best[e] = 0.f;  // relu output >= 0
@@ -181,11 +185,11 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
     ca[e] = -sc[e] * s1 - cb[e] * mu[e];
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    int t = i / G;
-    const int wx = t % Ww;
-    t /= Ww;
-    const int wy = t % Hw;
-    const int n = t / Hw;
+    const int t = a.fG.div(i);
+    const int t1 = a.fWw.div(t);
+    const int wx = t - t1 * Ww;
+    const int n = a.fHw.div(t1);
+    const int wy = t1 - n * Hw;
     // window values
     float zv[MAXW][CV];
     bool inb[MAXW];
@@ -328,11 +332,11 @@ __global__ __launch_bounds__(256) void bnact_sums_kernel(const T* __restrict__ z
   };
   auto load = [&](int i, Item& it) {
     if (i >= total) return;
-    int t = i / G;
-    const int wx = t % Wo;
-    t /= Wo;
-    const int wy = t % Ho;
-    it.n = t / Ho;
+    const int t = a.fG.div(i);
+    const int t1 = a.fWo.div(t);
+    const int wx = t - t1 * Wo;
+    it.n = a.fHo.div(t1);
+    const int wy = t1 - it.n * Ho;
 #pragma unroll
     for (int q = 0; q < MAXW; ++q)
       if (q < P * P)
@@ -439,6 +443,11 @@ static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const floa
   a.seedp = dr ? dr->seed_ptr : nullptr;
   a.seed = dr ? dr->seed : 0ull;
   a.site = dr ? dr->site : 0u;
+  a.fG = FastDiv(C / cv);
+  a.fWo = FastDiv(std::max(1, W / pool));
+  a.fHo = FastDiv(std::max(1, H / pool));
+  a.fWw = FastDiv((W + pool - 1) / pool);
+  a.fHw = FastDiv((H + pool - 1) / pool);
   return HVIT_OK;
 }
 

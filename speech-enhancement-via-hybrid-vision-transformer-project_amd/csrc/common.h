@@ -185,3 +185,24 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// n / d for 0 <= n < 2^31 by a multiply-high instead of the ~25-instruction
+// integer division sequence (index math in VALU-bound grid-stride loops):
+// q = floor(n m / 2^(32+s)), m = ceil(2^(32+s) / d), s = ceil(log2 d).  Exact:
+// m = 2^(32+s)/d + e, e < 1, adds n e / 2^(32+s) < 2^-(s+1) < 1/d to n/d.
+struct FastDiv {
+  uint32_t mlo = 0, mhi = 1;
+  int s = 0;
+  FastDiv() = default;
+  explicit FastDiv(int d) {
+    while ((1LL << s) < d) ++s;
+    const unsigned __int128 one = 1;
+    const unsigned long long m = (unsigned long long)(((one << (32 + s)) + (unsigned)d - 1) / (unsigned)d);
+    mlo = (uint32_t)m;
+    mhi = (uint32_t)(m >> 32);
+  }
+  __device__ __forceinline__ int div(int n) const {
+    const uint32_t hi = __umulhi((uint32_t)n, mlo) + (mhi ? (uint32_t)n : 0u);
+    return (int)(hi >> s);
+  }
+};
