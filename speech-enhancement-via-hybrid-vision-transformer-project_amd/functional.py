@@ -97,6 +97,14 @@ def _record(name, fn):
         REPLAY.setdefault(name, []).append(fn)
 
 
+def _launch(name, work, fn):
+    """One timed, recorded launch of op class ``name`` (the ViT data gradients:
+    re-runnable in isolation for the roofline loop)."""
+    with timed(name, work):
+        fn()
+    _record(name, (fn, work))
+
+
 def _empty(shape, dt, dev):
     return torch.empty(shape, dtype=L.torch_dtype(dt), device=dev)
 
@@ -948,14 +956,16 @@ class ViTBlockFn(torch.autograd.Function):
         df2w, j2 = linear_wgrad_deferred(dt, g2, a, M, D, hid, dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
         df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
-        with timed("vit_linear_dgrad", 2.0 * M * D * hid):
-            call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
-                 epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b, side=j2), s)
+        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b, side=j2)
+        _launch("vit_linear_dgrad", 2.0 * M * D * hid,
+                lambda: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
+                             e_fc2, s))
         df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id))
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        with timed("vit_linear_dgrad", 2.0 * M * hid * D):
-            call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
-                 epilogue(side=j1), s)
+        e_fc1 = epilogue(side=j1)
+        _launch("vit_linear_dgrad", 2.0 * M * hid * D,
+                lambda: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
+                             e_fc1, s))
         if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass
             dx1, dn2w, dn2b, g1, dpb = _ln_bwd_drop(dxn2, x1, m2, r2, n2w, dx2, zln2, drp, rs1, Nt, dt)
         else:
@@ -966,8 +976,10 @@ class ViTBlockFn(torch.autograd.Function):
         # attention branch
         dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id))
         do = _empty((M, D), dt, dev)
-        with timed("vit_linear_dgrad", 2.0 * M * D * D):
-            call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, epilogue(side=jp), s)
+        e_pr = epilogue(side=jp)
+        _launch("vit_linear_dgrad", 2.0 * M * D * D,
+                lambda: call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, e_pr,
+                             s))
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         # the qkv bias grad: per-workgroup partial column sums of dqkv written by
@@ -991,9 +1003,10 @@ class ViTBlockFn(torch.autograd.Function):
             call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
         dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        with timed("vit_linear_dgrad", 2.0 * M * 3 * D * D):
-            call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(), F32,
-                 epilogue(side=jq), s)
+        e_qkv = epilogue(side=jq)
+        _launch("vit_linear_dgrad", 2.0 * M * 3 * D * D,
+                lambda: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
+                             F32, e_qkv, s))
         if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
             dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         else:
