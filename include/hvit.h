@@ -165,7 +165,13 @@ int hvit_conv_dgrad(int dt, const hvit_conv_geom_t* g, const void* dy, const voi
                     void* stream);
 long long hvit_conv_wgrad_workspace(const hvit_conv_geom_t* g);
 int hvit_conv_wgrad(int dt, const hvit_conv_geom_t* g, const void* dy, float* dw_packed, float* ws,
-                    long long ws_elems, void* stream);                           /* dw_packed mode-0 layout */
+                    long long ws_elems, void* stream);
+/* The same with dw written in the conv Parameter's layout [Cout][Cin][KS][KS]
+ * (Cin = C1 + C2): the split-K slab reduction stores that order directly, so
+ * no hvit_conv_weight_unpack pass runs; dw_packed (Cout*Cin*KS*KS f32) is
+ * scratch for the unsplit case. */
+int hvit_conv_wgrad_torch(int dt, const hvit_conv_geom_t* g, const void* dy, float* dw, float* dw_packed, float* ws,
+                          long long ws_elems, void* stream);                           /* dw_packed mode-0 layout */
 int hvit_conv_weight_pack(const float* w, int Cout, int Cin, int KS, int mode, void* out, int out_dt,
                           void* stream);
 int hvit_conv_weight_unpack(const float* dw_packed, int Cout, int Cin, int KS, float* dw, void* stream);

@@ -92,6 +92,7 @@ _SIGS = {
     "hvit_conv_dgrad": ([i32, P(ConvGeom), vp, vp, vp, i32, vp], i32),
     "hvit_conv_wgrad_workspace": ([P(ConvGeom)], i64),
     "hvit_conv_wgrad": ([i32, P(ConvGeom), vp, vp, vp, i64, vp], i32),
+    "hvit_conv_wgrad_torch": ([i32, P(ConvGeom), vp, vp, vp, vp, i64, vp], i32),
     "hvit_conv_weight_pack": ([vp, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_conv_weight_unpack": ([vp, i32, i32, i32, vp, vp], i32),
     "hvit_bn_fold": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),

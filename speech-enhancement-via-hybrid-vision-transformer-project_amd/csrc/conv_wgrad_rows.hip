@@ -305,7 +305,7 @@ long long conv_wgrad_rows_ws(const hvit_conv_geom_t* g) {
 }
 
 int conv_wgrad_rows(const hvit_conv_geom_t* g, const void* dy, float* dw_packed, float* ws, long long ws_elems,
-                    hipStream_t st) {
+                    hipStream_t st, ConvSlabs* slabs) {
   RowsArgs a;
   const int Ho = g->Hs * g->U, Wo = g->Ws * g->U;
   a.dy = (const bf16_t*)dy;
@@ -342,6 +342,13 @@ int conv_wgrad_rows(const hvit_conv_geom_t* g, const void* dy, float* dw_packed,
   else
     hvit_rows::conv_wgrad_rows_kernel<64><<<grid, dim3(256), 0, st>>>(a);
   HVIT_LAUNCH_CHECK();
-  if (splits > 1) return hvit_sum_slabs(ws, splits, a.slab, dw_packed, st);
+  if (splits > 1) {
+    if (slabs) {  // the caller reduces them (hvit_conv_wgrad_torch)
+      slabs->splits = splits;
+      slabs->slab = a.slab;
+      return HVIT_OK;
+    }
+    return hvit_sum_slabs(ws, splits, a.slab, dw_packed, st);
+  }
   return HVIT_OK;
 }

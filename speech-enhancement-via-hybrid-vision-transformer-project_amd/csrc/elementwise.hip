@@ -376,6 +376,52 @@ extern "C" int hvit_bn_fold(const float* w, int Cout, int Cin, int KS, const flo
   return HVIT_OK;
 }
 
+// dw[co][ci][ky][kx] = sum_z ws[z * slab + ((co*KS + ky)*KS + kx)*Cin + ci]: a
+// packed conv weight gradient's split-K slabs summed straight into the
+// Parameter's layout (one pass instead of a slab sum and an unpack).  Threads
+// walk the packed order four channels at a time (coalesced 16-byte slab reads,
+// the same four-accumulator order as sum_slabs4_kernel) and scatter the four
+// sums to their [co][ci][ky][kx] places.
+__global__ void sum_slabs_unpack4_kernel(const float* ws, int splits, long slab4, int Cout, int Cin, int KS,
+                                         float* dw) {
+  const int C4 = Cin / 4, T = KS * KS;
+  const long total = (long)Cout * T * C4;
+  GRID_STRIDE(i, total) {
+    const int c4 = i % C4;
+    const long t = i / C4;
+    const int tap = t % T;
+    const int co = t / T;
+    const f32x4* p = (const f32x4*)ws + i;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    int k = 0;
+    for (; k + 4 <= splits; k += 4) {
+      s0 += p[(long)k * slab4];
+      s1 += p[(long)(k + 1) * slab4];
+      s2 += p[(long)(k + 2) * slab4];
+      s3 += p[(long)(k + 3) * slab4];
+    }
+    for (; k < splits; ++k) s0 += p[(long)k * slab4];
+    const f32x4 v = (s0 + s1) + (s2 + s3);
+    float* o = dw + ((long)co * Cin + 4 * c4) * T + tap;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[(long)e * T] = v[e];
+  }
+}
+
+int hvit_sum_slabs_unpack(const float* ws, int splits, long long slab, int Cout, int Cin, int KS, float* dw,
+                          float* tmp, hipStream_t st) {
+  const long n4 = (long)Cout * KS * KS * (Cin / 4);
+  if (Cin % 4 || slab % 4 || ((uintptr_t)ws & 15) || splits >= 64) {
+    // (many slabs: the column-reduction form of hvit_sum_slabs into tmp, then unpack)
+    if (int rc = hvit_sum_slabs(ws, splits, slab, tmp, st)) return rc;
+    return hvit_conv_weight_unpack(tmp, Cout, Cin, KS, dw, st);
+  }
+  hipLaunchKernelGGL(sum_slabs_unpack4_kernel, dim3(grid_for(n4)), dim3(256), 0, st, ws, splits, (long)(slab / 4),
+                     Cout, Cin, KS, dw);
+  HVIT_LAUNCH_CHECK();
+  return HVIT_OK;
+}
+
 extern "C" int hvit_conv_weight_unpack(const float* dw_packed, int Cout, int Cin, int KS, float* dw,
                                        void* stream) {
   HVIT_CHECK(dw_packed && dw, "hvit_conv_weight_unpack: null pointer");

@@ -237,6 +237,14 @@ bool thin_o1(const hvit_conv_geom_t* g) {
 }  // namespace
 
 int hvit_thin_c1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, int y_dt, float* stats, hipStream_t st);
+// split-K slabs a conv weight gradient left for its caller to reduce
+// (hvit_conv_wgrad_torch): splits > 1 when there are any
+struct ConvSlabs {
+  int splits = 1;
+  long long slab = 0;
+};
+int hvit_sum_slabs_unpack(const float* ws, int splits, long long slab, int Cout, int Cin, int KS, float* dw,
+                          float* tmp, hipStream_t st);
 int hvit_thin_c1_bn_tile_rows();
 long long hvit_thin_c1_wgrad_ws(const hvit_conv_geom_t* g);
 int hvit_thin_c1_wgrad(int dt, const hvit_conv_geom_t* g, const void* dz, float* dw, float* ws, long long ws_elems,

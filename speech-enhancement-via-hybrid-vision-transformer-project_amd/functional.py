@@ -393,19 +393,23 @@ def geom(src1, C1, src2, C2, N, Hs, Ws, U, KS, stride, pad, Cout) -> L.ConvGeom:
 
 
 def conv_wgrad(dt, g: L.ConvGeom, dz, wshape, dest=None) -> torch.Tensor:
+    """Conv weight gradient in the Parameter's layout [Cout][Cin][KS][KS]: the
+    split-K slab sum writes that order directly (hvit_conv_wgrad_torch)."""
     co, ci, ks, _ = wshape
+    dw = dest if dest is not None else torch.empty(wshape, dtype=torch.float32, device=dz.device)
     dwp = torch.empty(co * ci * ks * ks, dtype=torch.float32, device=dz.device)
     ws_n = L.lib().hvit_conv_wgrad_workspace(g)
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dz.device)
     P = dz.numel() // co  # output pixels
 
     def launch():
-        call("hvit_conv_wgrad", dt, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, stream_ptr())
+        call("hvit_conv_wgrad_torch", dt, g, dz.data_ptr(), dw.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n,
+             stream_ptr())
 
     with timed("conv_wgrad", 2.0 * P * co * ci * ks * ks):
         launch()
     _record("conv_wgrad", (launch, 2.0 * P * co * ci * ks * ks))
-    return unpack_conv(dwp, wshape, dest)
+    return dw.view(wshape)
 
 
 @dataclass

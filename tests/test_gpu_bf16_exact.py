@@ -261,6 +261,13 @@ def test_conv3x3_bf16_exact(env, case):
     ref.backward(gz.float())
     dz = gz.permute(0, 2, 3, 1).contiguous()
     dw = HF.conv_wgrad(L.BF16, g, dz, w.shape)
+    # the torch-layout entry (fused slab sum + unpack) against the packed one
+    # followed by hvit_conv_weight_unpack: bit-identical
+    ws_n = L.lib().hvit_conv_wgrad_workspace(g)
+    ws = torch.empty(max(ws_n, 1), device=DEV)
+    dwp = torch.empty(w.numel(), device=DEV)
+    L.call("hvit_conv_wgrad", L.BF16, g, dz.data_ptr(), dwp.data_ptr(), ws.data_ptr(), ws_n, s())
+    assert torch.equal(dw, HF.unpack_conv(dwp, w.shape))
     check_f32(dw, wr.grad, what="conv wgrad")
     wd = HF.pack_conv(w, 1, L.BF16)
     du = torch.empty(N, H, W, C1 + C2, device=DEV)
