@@ -872,13 +872,16 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
                                                          const uint32_t* __restrict__ kbits,
                                                          float* __restrict__ dbias) {
   const unsigned long long seed = seed_;
-  constexpr int RED = 2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4 + V2_KMAX * 32;  // colsum scratch offset
+  // keep bits transposed in LDS: KbT[word][query], pitch KBP words (a lane's 4
+  // query rows of one word are one 16-byte read)
+  constexpr int KBP = V2_KMAX + 16;
+  constexpr int RED = 2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4 + 8 * KBP * 4;  // colsum scratch offset
   __shared__ __attribute__((aligned(16))) char smem[RED + 2 * WAVES * 64 * 4];
   char* Qs = smem;
   char* Ds = smem + V2_KMAX * V2_ROWB;
   float* Ls = (float*)(smem + 2 * V2_KMAX * V2_ROWB);
   float* Dl = Ls + V2_KMAX;
-  uint32_t* Kb = (uint32_t*)(Dl + V2_KMAX);  // the forward's keep bits of this (b, h): [query][fq][2]
+  uint32_t* Kb = (uint32_t*)(Dl + V2_KMAX);  // the forward's keep bits of this (b, h): KbT[fq*2 + half][query]
   const int D = H * 64;
   const long pitch = 3L * D;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -906,8 +909,12 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
   }
   const bool use_kb = kbits && thr;
   if (use_kb)
-    for (int i = threadIdx.x; i < N * 2; i += WAVES * 64)
-      ((u32x4*)Kb)[i] = ((const u32x4*)(kbits + bh * N * 8))[i];
+    for (int i = threadIdx.x; i < N * 2; i += WAVES * 64) {
+      const u32x4 v = ((const u32x4*)(kbits + bh * N * 8))[i];
+      const int q = i >> 1, w0 = 4 * (i & 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Kb[(w0 + e) * KBP + q] = v[e];
+    }
   // this lane's key inside a query's bit pair: word fq' * 2 + half, bit position
   const int kbit = 8 * (key >> 5) + 4 * ((key >> 4) & 1) + (key & 3);
   const int kword = ((key >> 2) & 3) * 2 + (kbit >> 5), kshift = kbit & 31;
@@ -945,6 +952,8 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
       // (wave-uniform branch; their Ls / Dl rows are 0)
       const f32x4 l4 = *(const f32x4*)(Ls + 16 * j + 4 * fq);
       const f32x4 d4 = *(const f32x4*)(Dl + 16 * j + 4 * fq);
+      u32x4 kw4 = {0u, 0u, 0u, 0u};
+      if (use_kb) kw4 = *(const u32x4*)(Kb + kword * KBP + 16 * j + 4 * fq);
       f32x4 p;
 #pragma unroll
       for (int r = 0; r < 4; ++r) p[r] = kv ? __builtin_amdgcn_exp2f(fmaf(s[r], c2, -l4[r])) : 0.f;
@@ -958,7 +967,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
         const int qi = 16 * j + 4 * fq + r;
         float kp = 1.f;
         if (use_kb) {
-          kp = ((Kb[(qi < N ? qi : 0) * 8 + kword] >> kshift) & 1u) ? dscale : 0.f;
+          kp = ((kw4[r] >> kshift) & 1u) ? dscale : 0.f;  // (rows >= N: p is 0 there)
         } else if (thr) {
           const int src = (lane & ~3) | r;
           const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
