@@ -347,8 +347,25 @@ def main():
     # instrumented repeat of the timed steps (eager: HIP events around every
     # launch of each op class, functional.timed) for the per-op roofline table
     isteps = min(args.steps, 10)
+    # each instrumented step is queued behind a GPU spin of ~1.5 eager steps, so
+    # the host enqueues the whole step while the GPU is busy and no host
+    # launch gap falls inside an op's event window (the eager host enqueue is
+    # slower than the GPU step: unqueued, its gaps inflated the classes with the
+    # most host work per launch)
+    spin = None
+    if hasattr(torch.cuda, "_sleep"):
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1 << 20)
+        c0.record()
+        torch.cuda._sleep(1 << 22)
+        c1.record()
+        c1.synchronize()
+        per_ms = (1 << 22) / max(c0.elapsed_time(c1), 1e-3)
+        spin = min(int(per_ms * 1.5 * max(eager_ms or 0.0, ms * 1.5, 5.0)), 1 << 28)
     HF.OP_TIMES = {}
     for _ in range(isteps):
+        if spin:
+            torch.cuda._sleep(spin)
         eager_step()
     torch.cuda.synchronize()
     table = op_table(HF.OP_TIMES, isteps)
