@@ -19,6 +19,21 @@
 namespace hvit {
 
 // ------------------------------------------------------------- LayerNorm ---
+// Full-wave sum on the VALU: rotate-and-add inside each 16-lane DPP row
+// (row_ror 8, 4, 2, 1), then the four row sums read out of lanes 0, 16, 32,
+// 48 (the shuffle-based wave_sum is six dependent LDS permutes)
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 template <typename TY, int MAXV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                     const float* __restrict__ b, TY* __restrict__ y,
@@ -36,7 +51,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
     v[i] = c < D ? *(const f32x4*)(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
     s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   }
-  float mean = wave_sum(s) / (float)D;
+  float mean = wave_sum_dpp(s) / (float)D;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
@@ -45,7 +60,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 #pragma unroll
       for (int e = 0; e < 4; ++e) { float d = v[i][e] - mean; q += d * d; }
   }
-  float var = wave_sum(q) / (float)D;
+  float var = wave_sum_dpp(q) / (float)D;
   float rstd = rsqrtf(var + eps);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
@@ -174,8 +189,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
         }
       }
     }
-    s1 = wave_sum(s1) / (float)D;
-    s2 = wave_sum(s2) / (float)D;
+    s1 = wave_sum_dpp(s1) / (float)D;
+    s2 = wave_sum_dpp(s2) / (float)D;
     const float rsc = (DROP && dr.rowscale) ? dr.rowscale[row / dr.rps] : 1.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
