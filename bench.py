@@ -46,8 +46,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--graph", type=int, default=None, choices=[0, 1],
                     help="1: capture one whole step (fwd + loss + bwd + clip + AdamW, device-side dropout seeds and "
-                         "AdamW step counters) in a hipGraph and replay it; 0: eager launches.  Default 1 at one "
-                         "GPU, 0 under DP")
+                         "AdamW step counters; under DP also the hook-launched bucket all-reduces and the "
+                         "reducer's finish) in a hipGraph and replay it; 0: eager launches.  Default 1")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 32; 16 for --variant large)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -64,7 +64,7 @@ def parse():
                     help="op class for --roofline-only (functional.timed tag with a recorded replay)")
     a = ap.parse_args()
     if a.graph is None:
-        a.graph = 1 if int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("HVIT_FORCE_DIST") != "1" else 0
+        a.graph = 1
     if a.batch is None:
         a.batch = 16 if a.variant == "large" else 32
     return a
@@ -279,9 +279,12 @@ def main():
     graph = None
     if args.graph:
         # warm up eagerly on a side stream (allocator pools, weight shadows,
-        # optimizer state, device step counters), then capture one whole step;
-        # every replay is a full step: new dropout masks (device seed stream),
-        # AdamW bias corrections from the device step counters
+        # optimizer state, device step counters, both generations of the DP
+        # bucket buffers, the token-bound agreement), then capture one whole
+        # step; every replay is a full step: new dropout masks (device seed
+        # stream), AdamW bias corrections from the device step counters, and
+        # under DP the bucket all-reduces over RCCL (captured from the hooks
+        # in backward order, then the reducer's wait + average)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):

@@ -38,9 +38,13 @@ enum {
   HVIT_ACT_MUL_AUX = 5,     /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
   HVIT_ACT_RELU = 6         /* conv forward only: v = max(v + bias, 0) (eval-mode BatchNorm folded) */
 };
-/* flags of the backward calls that accumulate atomically: HVIT_ACC_ZEROED says
- * the caller already zeroed the accumulator outputs (one fill for a whole
- * backward pass), so the call skips its own clear. */
+/* flags of the backward calls that accumulate into caller memory:
+ * HVIT_ACC_ZEROED says the caller already zeroed the accumulator outputs (one
+ * fill for a whole backward pass), so the call skips its own clear.
+ * Determinism: every reduction of the train step is a fixed-order sum of
+ * per-workgroup partial rows (plain stores), so results are bit-identical from
+ * run to run and between eager launches and hipGraph replays.  The one
+ * exception is hvit_layernorm_bwd called WITHOUT a workspace (float atomics). */
 enum { HVIT_ACC_ZEROED = 1 };
 
 /* Counter-based dropout: element i is kept iff a 16-bit hash of (seed, site, i)
@@ -73,7 +77,12 @@ typedef struct {
  *   TANH: v = tanh(v) ; v = dropout(v) ; GELU_BWD: v *= gelu'(aux[m, n])
  *     (MUL_AUX: v *= aux[m, n])
  *   resid: v = resid[m, n] + rowscale[m / rows_per_sample] * v     (f32)
- *   colsum[n] += sum_m v ; y[m, n] = v                                         */
+ *   y[m, n] = v ; colsum (f32 [ceil(M/64)][N], overwritten): row r = sum of v
+ *     over rows 64r .. 64r+63 where the GEMM tile starting there is <= 64 rows
+ *     tall, else the tile's whole column sum in its first 64-row row and zeros
+ *     in the others (deterministic partial rows: the column sum is their
+ *     row-order sum, e.g. an hvit_slab_sum_t {colsum, out, N, N, ceil(M/64)}
+ *     side job of the next launch)                                             */
 typedef struct {
   int act;
   void* out2;
@@ -86,7 +95,7 @@ typedef struct {
   int rows_per_sample;
   const float* rowadd;
   int rowadd_rows;
-  float* colsum;
+  float* colsum; /* partial rows, see above */
   /* side job (n = 0: none; hvit_linear_fwd / hvit_linear_dgrad only): the
    * slabs of a deferred weight gradient (hvit_linear_wgrad_defer) summed by
    * this launch's workgroups before their own tiles -- no reduction launch of
@@ -255,8 +264,8 @@ int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* m
  * momentum and the unbiased variance, and increments num_batches_tracked);
  * eval: hvit_bn_eval_prep.  Backward: dz from dy = grad of the pooled output;
  * sums (hvit_bn_act_bwd_sums_elems(C) floats: [2][C] result followed by
- * per-slot partials) receives (dbeta, dgamma) in its first 2*C entries; with
- * flags & HVIT_ACC_ZEROED the caller has zeroed sums (else the call clears it). */
+ * per-workgroup partial rows, all overwritten -- no zeroing needed, flags is
+ * ignored) receives (dbeta, dgamma) in its first 2*C entries. */
 long long hvit_bn_act_bwd_sums_elems(int C);
 int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C, float* mean,
                      float* invstd, float* running_mean, float* running_var, long long* num_batches_tracked,
@@ -278,8 +287,9 @@ int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const flo
  * hvit_conv_bn_tile_rows) for hvit_bn_finalize; hvit_c1block_fwd recomputes z
  * and writes the pooled output y [N, H/pool, W/pool, Cout]; hvit_c1block_bwd
  * recomputes z, forms dz (hvit_bn_act_bwd's arithmetic) and reduces it straight
- * into the weight gradient dw_packed [Cout][9] f32 (sums as in hvit_bn_act_bwd,
- * ws = hvit_c1block_bwd_ws floats).  g: C1 = 1, C2 = 0, U = 1, KS = 3, stride 1,
+ * into the weight gradient dw_packed [Cout][9] f32 (sums: [dbeta | dgamma], 2*Cout
+ * floats, overwritten; ws = hvit_c1block_bwd_ws floats, which also holds the
+ * sums' per-workgroup partial rows).  g: C1 = 1, C2 = 0, U = 1, KS = 3, stride 1,
  * pad 1, Cout a power of two <= 256.  There is no input gradient (the model
  * input). */
 int hvit_c1block_stats(int dt, const hvit_conv_geom_t* g, const void* w_packed, float* bn_partials, void* stream);
@@ -324,7 +334,7 @@ int hvit_dropout_scale(const void* g, int g_dt, long long M, int N, const hvit_d
                        floats of per-workgroup partials (NULL: a slower two-pass fallback) */
 int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long long n, void* dz, int dz_dt, void* stream);
 int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate, float* out,
-                     void* stream);                                     /* out[n] (+)= sum_m x[m*ld+n] */
+                     void* stream);       /* out[n] (+)= sum_m x[m*ld+n], fixed summation order (no atomics) */
 int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream);
 int hvit_droppath_scale(int B, const hvit_dropout_t* dropout, float* out, void* stream);  /* DropPath
                                                                      components.py:407-427 */

@@ -1015,9 +1015,15 @@ static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 &&
 // workgroup, K/V (Q/dO) staged once.  Measured: two 8-wave workgroups per
 // (b, h) are slower both at B*H = 256 (default, B=32) and at B*H = 192
 // (config 5, B=16: 20.6 -> 21.5 us per layer); HVIT_ATTN_WAVES = 4 / 8 / 16
-// overrides (A/B only)
+// overrides (A/B only).  The one place the wave count is chosen: the launches
+// and the bias-partial row count both use it, so an unsupported value (clamped
+// to 4, the template the launches fall back to) cannot size the rows apart
+// from the grid.
 static int v2_waves(int) {
-  static const int w = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
+  static const int w = [] {
+    const int e = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
+    return (e == 16 || e == 8) ? e : 4;
+  }();
   return w;
 }
 
@@ -1139,18 +1145,11 @@ static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dou
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
-  if (dbias) {  // other shapes: the partial rows by column reductions of dqkv (one per row group)
+  if (dbias) {  // other shapes: one partial row per sample, a segmented column sum of dqkv (one launch, fixed order)
     const auto rc = [&]() -> int { HVIT_HD_DISPATCH(mhsa_bwd_t, qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, dropout, st); }();
     if (rc) return rc;
-    const long long C3 = 3LL * H * hd, R = mhsa_bias_rows_per_sample(dt, hd, N);
-    const long long per = (N + R - 1) / R;
-    for (long long g = 0; g < (long long)B * R; ++g) {
-      const long long r0 = (g / R) * N + (g % R) * per, nr = std::min<long long>(per, (g / R) * N + N - r0);
-      if (int rc2 = hvit_reduce_rows((const char*)dqkv + r0 * C3 * (dt == HVIT_BF16 ? 2 : 4), dt, nr, C3, C3, 0,
-                                     dbias + g * C3, stream))
-        return rc2;
-    }
-    return HVIT_OK;
+    const long long C3 = 3LL * H * hd;
+    return hvit_reduce_rows_seg(dqkv, dt, B, N, C3, C3, 0, dbias, stream);
   }
   HVIT_HD_DISPATCH(mhsa_bwd_t, qkv, o, dout, lse, delta_ws, dqkv, B, N, H, scale, dropout, st);
 }

@@ -17,7 +17,10 @@
 
 namespace hvit {
 
-constexpr int BN_SLOTS = 32;  // atomic spreading slots for the backward sums
+// partial rows of the backward sums: one per workgroup of the sums kernel
+// (plain stores, summed in row order by a deterministic column reduction), so
+// the sums grid is capped at BN_PART_ROWS
+constexpr int BN_PART_ROWS = 1024;
 
 template <typename T>
 struct V16 {  // 16 bytes of T as floats
@@ -278,14 +281,13 @@ __global__ __launch_bounds__(256) void bnact_bwd_kernel(const T* __restrict__ z,
           t1[e] += red[0][k][e];
           t2[e] += red[1][k][e];
         }
-      // spread the per-block partials over BN_SLOTS copies so that few blocks
-      // add to the same address (same-address atomics serialise)
-      float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+      // this workgroup's partial row (deterministic: no atomics)
+      float* slot = sums + 2 * a.C * (1 + blockIdx.x);
       const int cc = threadIdx.x * CV;
 #pragma unroll
       for (int e = 0; e < CV; ++e) {
-        atomicAdd(slot + cc + e, t1[e]);
-        atomicAdd(slot + a.C + cc + e, t2[e]);
+        slot[cc + e] = t1[e];
+        slot[a.C + cc + e] = t2[e];
       }
     }
   }
@@ -397,24 +399,16 @@ __global__ __launch_bounds__(256) void bnact_sums_kernel(const T* __restrict__ z
         t1[e] += red[0][k][e];
         t2[e] += red[1][k][e];
       }
-    float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+    float* slot = sums + 2 * a.C * (1 + blockIdx.x);  // this workgroup's partial row (no atomics)
     const int cc = threadIdx.x * CV;
 #pragma unroll
     for (int e = 0; e < CV; ++e) {
-      atomicAdd(slot + cc + e, t1[e]);
-      atomicAdd(slot + a.C + cc + e, t2[e]);
+      slot[cc + e] = t1[e];
+      slot[a.C + cc + e] = t2[e];
     }
   }
 }
 
-// sums[0 .. 2C) = sum over the BN_SLOTS slot copies that follow it
-__global__ void bn_slots_reduce_kernel(float* sums, int n2) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n2) return;
-  float s = 0.f;
-  for (int k = 1; k <= BN_SLOTS; ++k) s += sums[(size_t)k * n2 + i];
-  sums[i] = s;
-}
 
 // grid-stride launches; per-kernel caps measured on the B=32 encoder shapes
 // (fewer, longer-lived workgroups stream better here than one item per thread)
@@ -424,7 +418,7 @@ static int grid_for(long n, long cap) {
   if (g < 1) g = 1;
   return (int)g;
 }
-constexpr long BN_GRID_FWD = 2048, BN_GRID_SUMS = 2048, BN_GRID_APPLY = 1024;
+constexpr long BN_GRID_FWD = 2048, BN_GRID_SUMS = BN_PART_ROWS, BN_GRID_APPLY = 1024;
 
 static int make_args(BnArgs& a, int N, int H, int W, int C, int pool, const float* mean, const float* invstd,
                      const float* gamma, const float* beta, const hvit_dropout_t* dr, int cv) {
@@ -489,12 +483,13 @@ static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* su
   dim3 g(grid_for(total, BN_GRID_SUMS)), ga(grid_for(total, BN_GRID_APPLY));
   {  // the sums are dbeta / dgamma in both modes; only training-mode dz uses them
     const long tsum = (long)a.N * (a.H / P) * (a.W / P) * (a.C / cv);
-    if (tsum > 0)
-      hipLaunchKernelGGL((bnact_sums_kernel<T, TD>), dim3(grid_for(tsum, BN_GRID_SUMS)), dim3(256), 0, st,
-                         (const T*)z, (const TD*)dy, a, sums);
-    HVIT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(bn_slots_reduce_kernel, dim3(cdiv(2 * a.C, 256)), dim3(256), 0, st, sums, 2 * a.C);
-    HVIT_LAUNCH_CHECK();
+    const int gs = tsum > 0 ? grid_for(tsum, BN_GRID_SUMS) : 0;
+    if (gs > 0) {
+      hipLaunchKernelGGL((bnact_sums_kernel<T, TD>), dim3(gs), dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums);
+      HVIT_LAUNCH_CHECK();
+    }
+    // sums[0 .. 2C) = the partial rows summed in row order (0 rows: zeros)
+    if (int rc = hvit_reduce_rows(sums + 2 * a.C, HVIT_F32, gs, 2 * a.C, 2 * a.C, 0, sums, st)) return rc;
   }
   hipLaunchKernelGGL((bnact_bwd_kernel<T, TD, true>), ga, dim3(256), 0, st, (const T*)z, (const TD*)dy, a, sums,
                      training, (T*)dz);
@@ -502,7 +497,7 @@ static int bnact_bwd_t(const void* z, const void* dy, const BnArgs& a, float* su
   return HVIT_OK;
 }
 
-extern "C" long long hvit_bn_act_bwd_sums_elems(int C) { return 2LL * C * (1 + BN_SLOTS); }
+extern "C" long long hvit_bn_act_bwd_sums_elems(int C) { return 2LL * C * (1 + BN_PART_ROWS); }
 
 extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C, const float* mean,
                                const float* invstd, const float* gamma, const float* beta,
@@ -515,7 +510,7 @@ extern "C" int hvit_bn_act_bwd(int dt, const void* z, int N, int H, int W, int C
   const int cv = dt == HVIT_BF16 ? 8 : 4;
   if (int rc = make_args(a, N, H, W, C, pool, mean, invstd, gamma, beta, dropout2d, cv)) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (!(flags & HVIT_ACC_ZEROED)) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * (1 + BN_SLOTS), st);
+  (void)flags;  // (the partial rows are plain stores: no zeroed accumulator needed)
   if (dt == HVIT_BF16)
     return dy_dt == HVIT_BF16 ? bnact_bwd_t<bf16_t, bf16_t>(z, dy, a, sums, training, dz, st)
                               : bnact_bwd_t<bf16_t, float>(z, dy, a, sums, training, dz, st);

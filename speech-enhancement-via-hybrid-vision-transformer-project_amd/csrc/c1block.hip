@@ -26,7 +26,9 @@
 
 namespace hvit_c1 {
 
-constexpr int BN_SLOTS = 32;  // the hvit_bn_act_bwd_sums_elems layout (bnact.hip)
+// the backward sums' partial rows: one [2C] row per sums workgroup, written
+// into the weight-gradient workspace (which the backward kernel overwrites only
+// after the rows are reduced) and summed in row order: no atomics
 constexpr int THREADS = 256;
 
 struct Args {
@@ -260,9 +262,9 @@ __device__ __forceinline__ void route(const float (&zq)[P * P][CV], const float*
 }
 
 // backward reduce pass: per-channel sum g (dbeta), sum g * xhat (dgamma) over the
-// full windows; workgroup partials spread over the BN_SLOTS slot copies of sums
+// full windows; one partial row [2C] per workgroup in part (no atomics)
 template <typename T, typename TD, int P, int CV>
-__global__ __launch_bounds__(THREADS) void c1_sums_kernel(Args a_, const TD* __restrict__ dy, float* __restrict__ sums) {
+__global__ __launch_bounds__(THREADS) void c1_sums_kernel(Args a_, const TD* __restrict__ dy, float* __restrict__ part) {
   Args a = a_;
   a.resolve();
   extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -314,17 +316,9 @@ __global__ __launch_bounds__(THREADS) void c1_sums_kernel(Args a_, const TD* __r
     }
   }
   __syncthreads();
-  float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+  float* row = part + (size_t)2 * a.C * blockIdx.x;
   for (int i = threadIdx.x; i < 2 * a.C; i += THREADS)
-    atomicAdd(slot + i, red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i]);
-}
-
-__global__ void slots_reduce_kernel(float* sums, int n2) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n2) return;
-  float s = 0.f;
-  for (int k = 1; k <= BN_SLOTS; ++k) s += sums[(size_t)k * n2 + i];
-  sums[i] = s;
+    row[i] = red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i];
 }
 
 // backward apply + weight gradient: dz of every pixel (all windows, the
@@ -643,7 +637,7 @@ __global__ __launch_bounds__(THREADS) void c1m_apply_kernel(Args a_, TO* __restr
 
 template <typename TD, int NCB>
 __global__ __launch_bounds__(THREADS) void c1m_sums_kernel(Args a_, const TD* __restrict__ dy,
-                                                           float* __restrict__ sums) {
+                                                           float* __restrict__ part) {
   Args a = a_;
   a.resolve();
   extern __shared__ __attribute__((aligned(16))) float xs[];
@@ -710,9 +704,9 @@ __global__ __launch_bounds__(THREADS) void c1m_sums_kernel(Args a_, const TD* __
     }
   }
   __syncthreads();
-  float* slot = sums + 2 * a.C * (1 + (blockIdx.x % BN_SLOTS));
+  float* row = part + (size_t)2 * a.C * blockIdx.x;
   for (int i = threadIdx.x; i < 2 * a.C; i += THREADS)
-    atomicAdd(slot + i, red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i]);
+    row[i] = red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i];
 }
 
 template <typename TD, int NCB>
@@ -1093,8 +1087,9 @@ extern "C" int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w
   HVIT_CHECK(ws_elems >= hvit_c1block_bwd_ws(g, pool), "hvit_c1block_bwd: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const int C = a.C;
-  if (!(flags & HVIT_ACC_ZEROED)) (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * (1 + BN_SLOTS), st);
+  (void)flags;  // (partial rows, plain stores: no zeroed accumulator needed)
   if (a.N <= 0 || a.H <= 0 || a.W <= 0) {
+    (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st);
     (void)hipMemsetAsync(dw_packed, 0, sizeof(float) * C * 9, st);
     return HVIT_OK;
   }
@@ -1110,31 +1105,33 @@ extern "C" int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w
         constexpr int NCB = decltype(nc)::value;
         if (dy_dt == HVIT_BF16)
           hipLaunchKernelGGL((c1m_sums_kernel<bf16_t, NCB>), dim3(blocks), dim3(THREADS), lds, st, a,
-                             (const bf16_t*)dy, sums);
+                             (const bf16_t*)dy, ws);
         else
           hipLaunchKernelGGL((c1m_sums_kernel<float, NCB>), dim3(blocks), dim3(THREADS), lds, st, a,
-                             (const float*)dy, sums);
+                             (const float*)dy, ws);
       });
     } else {
       with_pool(pool, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         if (dt == HVIT_BF16 && dy_dt == HVIT_BF16)
           hipLaunchKernelGGL((c1_sums_kernel<bf16_t, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                             (const bf16_t*)dy, sums);
+                             (const bf16_t*)dy, ws);
         else if (dt == HVIT_BF16)
           hipLaunchKernelGGL((c1_sums_kernel<bf16_t, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                             (const float*)dy, sums);
+                             (const float*)dy, ws);
         else if (dy_dt == HVIT_BF16)
           hipLaunchKernelGGL((c1_sums_kernel<float, bf16_t, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                             (const bf16_t*)dy, sums);
+                             (const bf16_t*)dy, ws);
         else
           hipLaunchKernelGGL((c1_sums_kernel<float, float, P, CV>), dim3(blocks), dim3(THREADS), lds, st, a,
-                             (const float*)dy, sums);
+                             (const float*)dy, ws);
       });
     }
     HVIT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(slots_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, sums, 2 * C);
-    HVIT_LAUNCH_CHECK();
+    HVIT_CHECK((long long)blocks * 2 * C <= ws_elems, "hvit_c1block_bwd: workspace too small for the sums rows");
+    if (int rc = hvit_reduce_rows(ws, HVIT_F32, blocks, 2 * C, 2 * C, 0, sums, st)) return rc;
+  } else {
+    (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st);
   }
   const int Hw = (a.H + pool - 1) / pool;
   const int blocks = a.N * ((Hw + a.RB - 1) / a.RB);

@@ -19,6 +19,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ errors --
 void hvit_set_error(const char* fmt, ...);
+// deterministic column sums (elementwise.hip): S segments of M rows -> out [S][N];
+// and a tall matrix's column sums in two levels through f32 scratch ws (>= 64 * N)
+int hvit_reduce_rows_seg(const void* x, int dt, long long S, long long M, long long N, long long ld, int accumulate,
+                         float* out, void* stream);
+int hvit_reduce_rows_ws(const void* x, int dt, long long M, long long N, long long ld, int accumulate, float* out,
+                        float* ws, long long ws_elems, void* stream);
 #define HVIT_CHECK(cond, ...)                 \
   do {                                        \
     if (!(cond)) {                            \

@@ -193,63 +193,74 @@ __global__ void tanh_bwd_kernel(const void* dy, int dydt, const float* y, void* 
   }
 }
 
-// out[n] += sum_m x[m*ld + n]; block = 256 columns x row-chunk (generic path)
-__global__ void reduce_rows_kernel(const void* x, int dt, long M, long N, long ld, int rows_per_block,
-                                   float* out) {
-  long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  long m0 = (long)blockIdx.y * rows_per_block;
-  long m1 = m0 + rows_per_block < M ? m0 + rows_per_block : M;
-  float s = 0.f;
-  for (long m = m0; m < m1; ++m) s += ld_dt(x, m * ld + n, dt);
-  atomicAdd(out + n, s);
-}
-
-// Vectorised column sums: each thread owns one 16-byte column chunk (VEC
-// elements) and walks rows ty, ty+RY, ... of the block's R-row slice; the RY
-// partial rows are folded through LDS and one atomic per column and block is
-// issued.  Needs N % VEC == 0, ld % VEC == 0, 16-byte aligned base.
-constexpr int RC_TX = 32, RC_RY = 8;
-template <typename T>
-__global__ __launch_bounds__(256) void reduce_cols_vec_kernel(const T* x, int M, int N, int ld, int R, float* out) {
+// Deterministic column sums (no atomics: the result is bit-identical from run
+// to run and between eager launches and graph replays).  out[s*N + n] (+)=
+// sum of x[m*ld + n] over the rows m of segment s = blockIdx.y, [s*Ms,
+// min((s+1)*Ms, Mt)).  A
+// block owns TX column chunks of VEC elements (16-byte loads, or scalar loads
+// for unaligned widths) and splits the rows over RY = 256 / TX row groups:
+// thread (tx, ty) sums rows ty, ty + RY, ... into four accumulators (four rows
+// in flight), folded in a fixed order; the RY partials of a column are then
+// added in row-group order through LDS.  The summation order depends only on
+// (M, N, TX), which the host derives from the shape.
+template <typename T, bool VECLD>
+__global__ __launch_bounds__(256) void colsum_det_kernel(const T* __restrict__ x, int Ms, int Mt, int N, long ld,
+                                                          int TX, int accumulate, float* __restrict__ out) {
   constexpr int VEC = 16 / sizeof(T);
-  __shared__ float red[RC_RY][RC_TX * VEC + 4];
-  const int tx = threadIdx.x % RC_TX, ty = threadIdx.x / RC_TX;
-  const int n = (blockIdx.x * RC_TX + tx) * VEC;
-  const int m0 = blockIdx.y * R;
-  const int m1 = min(M, m0 + R);
-  float acc[VEC];
+  __shared__ float red[256 * VEC];
+  const int RY = 256 / TX;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const int n = (blockIdx.x * TX + tx) * VEC;
+  const long seg_off = (long)blockIdx.y * Ms;
+  const int M = min(Ms, Mt - (int)seg_off);  // rows of this segment
+  float a0[VEC], a1[VEC], a2[VEC], a3[VEC];
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
-  if (n < N) {
-    const T* p = x + (long)(m0 + ty) * ld + n;
-    int m = m0 + ty;
-    // two rows in flight per iteration
-    for (; m + RC_RY < m1; m += 2 * RC_RY, p += 2L * RC_RY * ld) {
-      const u32x4 a = *(const u32x4*)p;
-      const u32x4 b = *(const u32x4*)(p + (long)RC_RY * ld);
-      const T* ea = (const T*)&a;
-      const T* eb = (const T*)&b;
+  for (int e = 0; e < VEC; ++e) a0[e] = a1[e] = a2[e] = a3[e] = 0.f;
+  auto ld_row = [&](long m, float* v) {
+    const T* p = x + (seg_off + m) * ld + n;
+    if constexpr (VECLD) {
+      const u32x4 u = *(const u32x4*)p;
+      const T* eu = (const T*)&u;
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) acc[e] += Elem<T>::to_f(ea[e]) + Elem<T>::to_f(eb[e]);
+      for (int e = 0; e < VEC; ++e) v[e] = Elem<T>::to_f(eu[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[e] = n + e < N ? Elem<T>::to_f(p[e]) : 0.f;
     }
-    if (m < m1) {
-      const u32x4 a = *(const u32x4*)p;
-      const T* ea = (const T*)&a;
+  };
+  if (n < N) {
+    int m = ty;
+    for (; m + 3 * RY < M; m += 4 * RY) {
+      float v0[VEC], v1[VEC], v2[VEC], v3[VEC];
+      ld_row(m, v0);
+      ld_row(m + RY, v1);
+      ld_row(m + 2 * RY, v2);
+      ld_row(m + 3 * RY, v3);
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) acc[e] += Elem<T>::to_f(ea[e]);
+      for (int e = 0; e < VEC; ++e) {
+        a0[e] += v0[e];
+        a1[e] += v1[e];
+        a2[e] += v2[e];
+        a3[e] += v3[e];
+      }
+    }
+    for (; m < M; m += RY) {
+      float v0[VEC];
+      ld_row(m, v0);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) a0[e] += v0[e];
     }
   }
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) red[ty][tx * VEC + e] = acc[e];
+  for (int e = 0; e < VEC; ++e) red[ty * (TX * VEC) + tx * VEC + e] = (a0[e] + a1[e]) + (a2[e] + a3[e]);
   __syncthreads();
-  for (int c = threadIdx.x; c < RC_TX * VEC; c += blockDim.x) {
-    const int col = blockIdx.x * RC_TX * VEC + c;
+  for (int c = threadIdx.x; c < TX * VEC; c += blockDim.x) {
+    const int col = blockIdx.x * TX * VEC + c;
     if (col >= N) continue;
     float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < RC_RY; ++k) s += red[k][c];
-    atomicAdd(out + col, s);
+    for (int k = 0; k < RY; ++k) s += red[k * (TX * VEC) + c];
+    float* o = out + (long)blockIdx.y * N + col;
+    *o = accumulate ? *o + s : s;
   }
 }
 
@@ -483,38 +494,66 @@ extern "C" int hvit_tanh_bwd(const void* dy, int dy_dt, const float* y, long lon
   return HVIT_OK;
 }
 
-extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate,
-                                float* out, void* stream) {
+// Deterministic column sums (colsum_det_kernel) over segments of Ms rows
+// (the last one clipped at Mt): out [S = cdiv(Mt, Ms)][N].  The column-chunk
+// width TX is the largest of 32 / 16 / 8 / 4 that still gives >= 128
+// workgroups, so short-and-wide and tall-and-narrow matrices both spread over
+// the chip; the choice depends on the shape only (fixed summation order).
+static int colsum_launch(const void* x, int dt, long long Ms, long long Mt, long long N, long long ld, int accumulate,
+                         float* out, hipStream_t st) {
   HVIT_CHECK(x && out, "hvit_reduce_rows: null pointer");
   HVIT_CHECK(dt == HVIT_F32 || dt == HVIT_BF16, "hvit_reduce_rows: dtype");
-  hipStream_t st = (hipStream_t)stream;
-  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
-  if (M <= 0 || N <= 0) return HVIT_OK;
-  const int vec = dt == HVIT_F32 ? 4 : 8;
-  if (N % vec == 0 && ld % vec == 0 && ((uintptr_t)x & 15) == 0 && M * ld < (1LL << 31)) {
-    const int gx = (int)((N / vec + RC_TX - 1) / RC_TX);
-    // about 1024 workgroups, row slices a multiple of 2*RC_RY
-    long R = (M * gx + 1023) / 1024;
-    R = ((R + 2 * RC_RY - 1) / (2 * RC_RY)) * (2 * RC_RY);
-    if (R < 2 * RC_RY) R = 2 * RC_RY;
-    const int gy = (int)((M + R - 1) / R);
-    if (dt == HVIT_F32)
-      hipLaunchKernelGGL(reduce_cols_vec_kernel<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, (int)M,
-                         (int)N, (int)ld, (int)R, out);
-    else
-      hipLaunchKernelGGL(reduce_cols_vec_kernel<bf16_t>, dim3(gx, gy), dim3(256), 0, st, (const bf16_t*)x, (int)M,
-                         (int)N, (int)ld, (int)R, out);
-    HVIT_LAUNCH_CHECK();
-    return HVIT_OK;
+  HVIT_CHECK(Ms > 0 && Mt >= 0 && N >= 0 && ld >= N && Mt < (1LL << 31) && N < (1LL << 31),
+             "hvit_reduce_rows: bad shape");
+  const long long S = Mt > 0 ? (Mt + Ms - 1) / Ms : 1;  // (no rows: one segment of zeros)
+  HVIT_CHECK(S < 65536, "hvit_reduce_rows: too many segments");
+  if (S == 0 || N == 0) return HVIT_OK;
+  const int es = dt == HVIT_F32 ? 4 : 2, vec = 16 / es;
+  const bool vecld = N % vec == 0 && ld % vec == 0 && ((uintptr_t)x & 15) == 0;
+  const long nvec = (N + vec - 1) / vec;
+  int tx = 32;
+  while (tx > 4 && cdiv(nvec, tx) * S < 128) tx /= 2;
+  dim3 g((unsigned)cdiv(nvec, tx), (unsigned)S);
+#define HVIT_COLSUM(T, V)                                                                                       \
+  hipLaunchKernelGGL((colsum_det_kernel<T, V>), g, dim3(256), 0, st, (const T*)x, (int)Ms, (int)Mt, (int)N, (long)ld, \
+                     tx, accumulate, out)
+  if (dt == HVIT_F32) {
+    if (vecld) HVIT_COLSUM(float, true);
+    else HVIT_COLSUM(float, false);
+  } else {
+    if (vecld) HVIT_COLSUM(bf16_t, true);
+    else HVIT_COLSUM(bf16_t, false);
   }
-  int rpb = 64;
-  long gy = (M + rpb - 1) / rpb;
-  long gx = (N + 255) / 256;
-  while (gx * gy > 65536 && rpb < (1 << 20)) { rpb *= 2; gy = (M + rpb - 1) / rpb; }
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, x, dt, (long)M,
-                     (long)N, (long)ld, rpb, out);
+#undef HVIT_COLSUM
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
+}
+
+// S segments of M rows each (x rows [s*M, (s+1)*M)) -> out [S][N]
+int hvit_reduce_rows_seg(const void* x, int dt, long long S, long long M, long long N, long long ld, int accumulate,
+                         float* out, void* stream) {
+  if (S <= 0 || M <= 0) return HVIT_OK;
+  return colsum_launch(x, dt, M, S * M, N, ld, accumulate, out, (hipStream_t)stream);
+}
+
+// Column sums of a tall matrix in two deterministic levels when f32 scratch
+// (ws, >= 64 * N floats) allows: 64 row segments -> [64][N] partials -> out.
+// Otherwise one level (every row of a column chunk walked by one workgroup).
+int hvit_reduce_rows_ws(const void* x, int dt, long long M, long long N, long long ld, int accumulate, float* out,
+                        float* ws, long long ws_elems, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  constexpr long long P = 64;
+  if (M > 4096 && ws && ws_elems >= P * N) {
+    if (int rc = colsum_launch(x, dt, (M + P - 1) / P, M, N, ld, 0, ws, st)) return rc;
+    const long long S = (M + (M + P - 1) / P - 1) / ((M + P - 1) / P);
+    return colsum_launch(ws, HVIT_F32, S, S, N, N, accumulate, out, st);
+  }
+  return colsum_launch(x, dt, M > 0 ? M : 1, M, N, ld, accumulate, out, st);
+}
+
+extern "C" int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long ld, int accumulate,
+                                float* out, void* stream) {
+  return colsum_launch(x, dt, M > 0 ? M : 1, M, N, ld, accumulate, out, (hipStream_t)stream);
 }
 
 // out[i] = sum_k ws[k * stride + i], i < n (slabs of `stride` elements)

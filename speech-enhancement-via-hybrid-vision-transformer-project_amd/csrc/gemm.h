@@ -369,7 +369,7 @@ struct Epi {
   const float* rowscale = nullptr;
   int rows_per_sample = 1;
   float* stats = nullptr;   // BN partials [64-row tile][N][2] = (mean, M2)
-  float* colsum = nullptr;  // atomic column sums of the final v
+  float* colsum = nullptr;  // column sums of the final v: partial row per 64-row block ([cdiv(M,64)][N])
   long slab_stride = 0;     // EPI_SLAB: elements between split-K slabs (0: M * ldo)
   unsigned* tickets = nullptr;  // EPI_SLAB (ring kernels): per-tile arrival counters, zeroed; the last
   float* red_out = nullptr;     //   slice of a tile sums the slabs into red_out (ld = ldo) in-kernel
@@ -1426,13 +1426,26 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[q0 * BN + c8 * 8 + e] = cs8[e];
       epi_barrier();
-      if (q0 == 0)
+      if (q0 == 0) {
+        // deterministic: the tile's column sums as partial row m0/64 (plain
+        // stores; the tile's other 64-row rows get zeros), summed in row order
+        // by the caller (hvit_epilogue_t.colsum)
+        float t8[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float t = 0.f;
           for (int k = 0; k < RS8; ++k) t += red[k * BN + c8 * 8 + e];
-          atomicAdd(ep.colsum + n8 + e, t);
+          t8[e] = t;
         }
+        float* row = ep.colsum + (long)(m0 / 64) * N + n8;
+        *(f32x4*)row = (f32x4){t8[0], t8[1], t8[2], t8[3]};
+        *(f32x4*)(row + 4) = (f32x4){t8[4], t8[5], t8[6], t8[7]};
+#pragma unroll
+        for (int r = 1; r < BM / 64; ++r) {
+          *(f32x4*)(row + (long)r * N) = (f32x4){0.f, 0.f, 0.f, 0.f};
+          *(f32x4*)(row + (long)r * N + 4) = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      }
     }
     epi_side(ep);
     GEMM_STAMP(2);
@@ -1691,11 +1704,15 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
     for (int e = 0; e < 4; ++e) red[r0 * BN + c4 * 4 + e] = csum[e];
     epi_barrier();
     if (r0 == 0)
+      // deterministic partial row m0/64 (zeros in the tile's other 64-row rows)
       for (int e = 0; e < 4; ++e) {
         if (n + e >= N) break;
         float s = 0.f;
         for (int k = 0; k < RSTEP; ++k) s += red[k * BN + c4 * 4 + e];
-        atomicAdd(ep.colsum + n + e, s);
+        float* row = ep.colsum + (long)(m0 / 64) * N + n + e;
+        *row = s;
+        for (int r = 1; r < BM / 64; ++r)
+          if (m0 + 64 * r < M) row[(long)r * N] = 0.f;
       }
   }
   epi_side(ep);

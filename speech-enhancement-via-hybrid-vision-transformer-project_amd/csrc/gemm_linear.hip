@@ -61,7 +61,9 @@ extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
   // the tall-skinny kernel of wgrad_small.hip)
   int s = std::max(wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN), wgrad_splits(N, K, M, 128, 64));
   const long long g = s > 1 ? (long long)s * ((long long)N * K + N) : 0;
-  return std::max(g, hvit_wgrad_small_ok(HVIT_BF16, M, N, K) ? hvit_wgrad_small_ws(M, N, K) : 0LL);
+  // + room for the two-level bias column sums of a tall dy (hvit_reduce_rows_ws)
+  return std::max(std::max(g, 64LL * N),
+                  hvit_wgrad_small_ok(HVIT_BF16, M, N, K) ? hvit_wgrad_small_ws(M, N, K) : 0LL);
 }
 
 // per-tile arrival counters of the in-kernel split-K reduction (ring kernels;
@@ -178,7 +180,9 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
       if (rc) return rc;
       if (s > 1 && !tk)
         if (int rc2 = slab_reduce(ws, s, NK + N, NK, dw, stream, job)) return rc2;
-      if (db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
+      // (the slabs are consumed on the stream before this reuses ws; a deferred job
+      // has no bias gradient)
+      if (db) return hvit_reduce_rows_ws(dy, dt, M, N, N, 0, db, job ? nullptr : ws, ws_elems, stream);
       return HVIT_OK;
     }
   }
@@ -205,7 +209,7 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
     if (int rc = slab_reduce(ws, splits, NK + N, fused_db ? NK + N : NK, dw, stream, fused_db ? nullptr : job))
       return rc;
   }
-  if (db && !fused_db) return hvit_reduce_rows(dy, dt, M, N, N, 0, db, stream);
+  if (db && !fused_db) return hvit_reduce_rows_ws(dy, dt, M, N, N, 0, db, job ? nullptr : ws, ws_elems, stream);
   return HVIT_OK;
 }
 

@@ -373,13 +373,24 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
 #pragma unroll
     for (int e = 0; e < 8; ++e) red[q0 * BN + c8 * 8 + e] = cs8[e];
     epi_barrier();
-    if (q0 == 0)
+    if (q0 == 0) {
+      // deterministic partial row m0/64 (zeros in the tile's other 64-row rows)
+      float t8[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float t = 0.f;
         for (int k = 0; k < RS8; ++k) t += red[k * BN + c8 * 8 + e];
-        atomicAdd(ep.colsum + n8 + e, t);
+        t8[e] = t;
       }
+      float* row = ep.colsum + (long)(m0 / 64) * N + n8;
+      *(f32x4*)row = (f32x4){t8[0], t8[1], t8[2], t8[3]};
+      *(f32x4*)(row + 4) = (f32x4){t8[4], t8[5], t8[6], t8[7]};
+#pragma unroll
+      for (int r = 1; r < BM / 64; ++r) {
+        *(f32x4*)(row + (long)r * N) = (f32x4){0.f, 0.f, 0.f, 0.f};
+        *(f32x4*)(row + (long)r * N + 4) = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
   }
 }
 

@@ -20,15 +20,26 @@ over xGMI; gloo works for CPU tests and for ranks that share one GPU.
   a launch from ever reducing in place under a ``.grad`` view that a later
   accumulating backward still writes (``zero_grad(set_to_none=False)``).
 * Gradient accumulation (trainer.py:72, :164-183: several backward passes
-  before one optimizer step) is exact: a bucket whose gradients change after
-  its all-reduce was launched is marked stale and re-reduced from the current
-  ``.grad`` in ``finish()``.  ``no_sync()`` skips the wasted early launches.
+  before one optimizer step) is exact.  A bucket is reduced in place (its
+  ``.grad`` views ARE the flat buffer), so when a later backward brings a
+  gradient for a bucket whose all-reduce was already launched, a pre-accumulate
+  hook first waits for that reduction and divides the buffer by the world size:
+  the views then hold mean(g1) on every rank, the backward adds its local g2,
+  and the bucket is reduced again (mean over ranks of mean(g1) + g2 =
+  mean(g1 + g2)).  ``no_sync()`` skips the wasted early launches.
+* Capturable: a whole DP step (forward, backward with the hook-launched bucket
+  all-reduces, ``finish()``, the optimizer) can be captured in one hipGraph and
+  replayed; nothing in the hooks or in ``finish()`` syncs the host with the
+  device.
 * ``sliced={"pos_encoding.pos_embed": R}`` reduces only the first R rows of a
   parameter whose gradient is zero beyond the token count (the 10 000-row
   positional table; 18 % of the default model's gradient bytes at N = 256).
   R must bound the token count of every forward on every rank; the model's
-  ``last_num_tokens`` is checked against it in ``finish()`` and a larger count
-  raises.  Without ``sliced`` the whole table is reduced (exact for any N).
+  ``last_num_tokens`` is agreed over the group (MAX) in ``finish()`` on a gloo
+  group (host memory: no device sync) and a larger count raises on every rank.
+  Under stream capture the agreement is skipped: a captured step replays the
+  shapes of the eager warm-up steps that were checked.  Without ``sliced`` the
+  whole table is reduced (exact for any N).
 * BatchNorm statistics are computed per replica (local BN, as DDP without
   SyncBN; the reference has no distributed code to match).  With
   ``broadcast_buffers`` (default, as DDP) rank 0's running statistics are
@@ -86,10 +97,20 @@ class GradAllReducer:
         self.flats: List[List[Optional[torch.Tensor]]] = [[None, None] for _ in self.buckets]
         self._gen = 0
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        # pre-accumulate hooks: a gradient arriving for an already-reduced bucket
+        self._hooks += [p.register_hook(self._pre_grad_hook(p)) for p in self.params]
         self._fwd_hook = model.register_forward_hook(self._on_forward)
         self._syncing = True
         self.broadcast_buffers = broadcast_buffers
         self._max_tokens = 0
+        # host-side group for the token-bound agreement: a CPU all_reduce on gloo
+        # needs no device sync (on an nccl group an int read back would stall the
+        # host until the whole backward had run)
+        self._agree = bool(self.sliced) and self.world > 1
+        self._host_group = self.group
+        if self._agree and dist.get_backend(self.group) != "gloo":
+            self._host_group = dist.new_group(ranks=dist.get_process_group_ranks(self.group)
+                                              if self.group is not None else None, backend="gloo")
         self.reset()
         self._publish()
 
@@ -145,12 +166,42 @@ class GradAllReducer:
         finally:
             self._syncing = prev
 
-    # ------------------------------------------------------------ the hook --
+    # ----------------------------------------------------------- the hooks --
+    def _pre_grad_hook(self, p):
+        ref = weakref.ref(p)
+
+        def hook(grad):
+            q = ref()
+            if q is not None:
+                self._before_accumulate(q)
+            return None
+
+        return hook
+
+    def _before_accumulate(self, p):
+        """A backward is about to add a gradient to ``p``.  If ``p``'s bucket was
+        already launched this step, its buffer holds the in-place SUM over ranks
+        of the earlier gradients, and the GRAD_DEST ``.grad`` views are that
+        buffer: wait for it and divide by the world size, so the views hold the
+        mean and the bucket can be reduced again after this backward (the
+        reduction is linear).  Copied gradients (biases, norms, sliced rows)
+        still hold their local sums, which the relaunch copies in afresh."""
+        b = self.where[id(p)]
+        w = self.works[b]
+        if w is None:
+            return
+        w.wait()
+        flat = self.flats[b][self._gen]
+        flat.div_(self.world)  # (the copied gradients' regions are re-copied at the relaunch)
+        self.works[b] = None
+        self.stale[b] = False
+        self.seen[b] = set()
+
     def _on_grad(self, p):
         if not self._syncing:
             return
         b = self.where[id(p)]
-        if self.works[b] is not None:  # another backward changed an already-launched bucket
+        if self.works[b] is not None:  # (unreachable: the pre-accumulate hook reset it)
             self.stale[b] = True
             return
         self.seen[b].add(id(p))
@@ -175,16 +226,18 @@ class GradAllReducer:
         unused parameters or a step taken under no_sync, and re-launching stale
         ones), install the averaged gradients, broadcast rank 0's buffers, and
         reset for the next step."""
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         if self.sliced:
             # agree on the largest token count over the group first, so that a
             # rank whose batch exceeds the row bound makes EVERY rank raise here,
-            # before any of them enters the bucket collectives below
+            # before any of them enters the bucket collectives below (host memory
+            # on a gloo group: no device sync; skipped under capture, whose
+            # static shapes the eager warm-up steps already agreed on)
             mt = self._max_tokens
-            if self.world > 1:
-                dev = self.params[0].device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
-                t = torch.tensor([mt], dtype=torch.int64, device=dev)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-                mt = int(t.item())
+            if self._agree and not capturing:
+                t = torch.tensor([mt], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._host_group)
+                mt = int(t[0])
             for name, rows in self.sliced.items():
                 if mt > rows:
                     self._max_tokens = 0

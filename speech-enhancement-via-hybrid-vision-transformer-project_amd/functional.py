@@ -97,12 +97,22 @@ def _record(name, fn):
         REPLAY.setdefault(name, []).append(fn)
 
 
-def _launch(name, work, fn):
+def _launch(name, work, fn, e=None, keep=()):
     """One timed, recorded launch of op class ``name`` (the ViT data gradients:
-    re-runnable in isolation for the roofline loop)."""
+    re-runnable in isolation for the roofline loop).  ``fn(e)`` issues it with
+    epilogue ``e``.  The recorded replay runs the same launch without the
+    epilogue's side job (the carried slab sum belongs to the step, and its
+    slabs and destination are freed after the backward) and holds ``keep`` (the
+    tensors behind the epilogue's raw pointers, e.g. gelu'(h) and the bias-grad
+    accumulator) so the replay never touches freed memory."""
     with timed(name, work):
-        fn()
-    _record(name, (fn, work))
+        fn(e)
+    if REPLAY is not None:
+        er = None
+        if e is not None:
+            er = type(e).from_buffer_copy(e)
+            er.side = L.SlabSum()
+        _record(name, ((lambda er=er, keep=keep: fn(er)), work))
 
 
 def _empty(shape, dt, dev):
@@ -541,7 +551,6 @@ class ConvBNActFn(torch.autograd.Function):
         ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
         ctx.meta = (U, pool, training, dr, dt)
         ctx.sg = sg
-        ctx.zs = _zs(ctx, L.lib().hvit_bn_act_bwd_sums_elems(Cout))
         return y
 
     @staticmethod
@@ -557,7 +566,8 @@ class ConvBNActFn(torch.autograd.Function):
         s = stream_ptr()
         dy = dy.contiguous()
         dz = _empty(z.shape, dt, dev)
-        sums = ctx.zs.take(dev)
+        # [dbeta | dgamma] followed by per-workgroup partial rows (plain stores: no zeroing)
+        sums = torch.empty(L.lib().hvit_bn_act_bwd_sums_elems(Cout), dtype=torch.float32, device=dev)
         with timed("bn_act_bwd", float(2 * z.numel() * z.element_size() + dy.numel() * dy.element_size())):
             call("hvit_bn_act_bwd", dt, z.data_ptr(), N, H, W, Cout, ctx.mean.data_ptr(), ctx.invstd.data_ptr(),
                  gamma.data_ptr(), beta.data_ptr(), dr, pool, dy.data_ptr(), L.dt_of(dy), int(training),
@@ -591,7 +601,7 @@ LNDROP = os.environ.get("HVIT_LNDROP", "1") != "0"  # A/B knob: 0 = separate Lay
 # their own and the qkv bias gradient is a column reduction of dqkv
 DEFER = os.environ.get("HVIT_DEFER", "1") != "0"
 # A/B knob: 0 = the qkv bias gradient by a column reduction of dqkv after the
-# attention backward (instead of the backward's per-workgroup partial sums)
+# attention backward (instead of the backward's partial rows)
 ATTN_DB = os.environ.get("HVIT_ATTN_DB", "1") != "0"
 
 
@@ -644,7 +654,6 @@ class C1BlockFn(torch.autograd.Function):
         ctx.save_for_backward(x1, w, gamma, beta)
         ctx.mean, ctx.invstd = mean, invstd
         ctx.meta = (pool, training, dr, dt)
-        ctx.zs = _zs(ctx, L.lib().hvit_bn_act_bwd_sums_elems(Cout))
         return y
 
     @staticmethod
@@ -658,7 +667,7 @@ class C1BlockFn(torch.autograd.Function):
         dy = dy.contiguous()
         g = geom(x1, 1, None, 0, N, H, W, 1, 3, 1, 1, Cout)
         wp = pack_conv(w, 0, dt)
-        sums = ctx.zs.take(dev)
+        sums = torch.empty(2 * Cout, dtype=torch.float32, device=dev)  # [dbeta | dgamma]
         dwp = torch.empty(w.numel(), dtype=torch.float32, device=dev)
         ws_n = L.lib().hvit_c1block_bwd_ws(C.byref(g), pool)
         ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
@@ -925,10 +934,10 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.ho = (ho_in if LNDROP else None, ho_out)
         ctx.t = (x2d, xn1, m1, r1, qkv, o, lse, x1, xn2, m2, r2, gh, a, Wqkv, Wp, W1, W2, rs1, rs2)
         ctx.meta = (B, Nt, D, H, hid, scale, dt, d_attn.c(), d_proj.c(), d_fc1.c(), d_fc2.c())
-        # LN1, LN2 (dgamma|dbeta); fc1, fc2, proj bias grads (column sums fused into
-        # the GELU-backward epilogue and the two dropout passes)
+        # LN1, LN2 (dgamma|dbeta); fc2, proj bias grads (column sums fused into the
+        # two dropout passes; fc1's comes from the GELU-backward epilogue's partial rows)
         # (LN1's / LN2's slots also hold a bias grad when a dropout pass is fused, LNDROP)
-        ctx.zs = (_zs(ctx, 3 * D), _zs(ctx, 3 * D), _zs(ctx, hid), _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
+        ctx.zs = (_zs(ctx, 3 * D), _zs(ctx, 3 * D), None, _zs(ctx, D), _zs(ctx, D), _zs(ctx, 3 * D))
         if want_probs:
             ctx.mark_non_differentiable(probs)
         return x2.view(B, Nt, D), probs
@@ -945,7 +954,7 @@ class ViTBlockFn(torch.autograd.Function):
         if dx2.dtype != torch.float32:
             dx2 = dx2.float()
         # MLP branch
-        zln1, zln2, zf1b, zf2b, zpb, zqb = ctx.zs
+        zln1, zln2, _, zf2b, zpb, zqb = ctx.zs
         ho_in, ho_out = ctx.ho
         if ho_out is not None and ho_out.g is not None:  # fused into the next consumer's LN backward
             g2, df2b = ho_out.g, ho_out.colsum
@@ -959,17 +968,23 @@ class ViTBlockFn(torch.autograd.Function):
         # that follows it (epilogue side job): no reduction launch of its own
         df2w, j2 = linear_wgrad_deferred(dt, g2, a, M, D, hid, dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
-        df1b = zf1b.take(dev)  # fc1 bias grad: fused column sum (zeroed accumulator)
-        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=df1b, side=j2)
+        # fc1 bias grad: the GELU-backward epilogue's column sums, one partial row per
+        # 64-row block (plain stores: deterministic), summed in row order as the fc1
+        # weight-gradient launch's side job
+        nrow = (M + 63) // 64
+        cparts = torch.empty((nrow, hid), dtype=torch.float32, device=dev)
+        df1b = torch.empty(hid, dtype=torch.float32, device=dev)
+        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=cparts, side=j2)
         _launch("vit_linear_dgrad", 2.0 * M * D * hid,
-                lambda: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt,
-                             e_fc2, s))
-        df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id))
+                lambda e: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt, e,
+                               s), e_fc2, (gh, cparts))
+        jc = Deferred(L.SlabSum(cparts.data_ptr(), df1b.data_ptr(), hid, hid, nrow), cparts)
+        df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id), side=jc)
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         e_fc1 = epilogue(side=j1)
         _launch("vit_linear_dgrad", 2.0 * M * hid * D,
-                lambda: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
-                             e_fc1, s))
+                lambda e: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
+                               e, s), e_fc1)
         if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass
             dx1, dn2w, dn2b, g1, dpb = _ln_bwd_drop(dxn2, x1, m2, r2, n2w, dx2, zln2, drp, rs1, Nt, dt)
         else:
@@ -982,16 +997,16 @@ class ViTBlockFn(torch.autograd.Function):
         do = _empty((M, D), dt, dev)
         e_pr = epilogue(side=jp)
         _launch("vit_linear_dgrad", 2.0 * M * D * D,
-                lambda: call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, e_pr,
-                             s))
+                lambda e: call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, e, s),
+                e_pr)
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
-        # the qkv bias grad: per-workgroup partial column sums of dqkv written by
-        # the attention backward, summed as the qkv weight-gradient launch's side job
+        # the qkv bias grad: partial column sums of dqkv written by the attention
+        # backward (one row per workgroup on the register-resident kernels, one per
+        # sample by a segmented column sum elsewhere; plain stores, summed in row
+        # order: deterministic), summed as the qkv weight-gradient launch's side job
         jb = None
-        # (the register-resident bf16 kernels: hd 64, N <= 256, N % 4 == 0; other
-        # shapes keep the column reduction)
-        if ATTN_DB and dt == BF16 and D // H == 64 and Nt <= 256 and Nt % 4 == 0:
+        if ATTN_DB:
             nbr = L.lib().hvit_mhsa_bias_rows(dt, B, Nt, H, D // H)
             bparts = torch.empty((nbr, 3 * D), dtype=torch.float32, device=dev)
             dqkvb = torch.empty(3 * D, dtype=torch.float32, device=dev)
@@ -1009,8 +1024,8 @@ class ViTBlockFn(torch.autograd.Function):
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         e_qkv = epilogue(side=jq)
         _launch("vit_linear_dgrad", 2.0 * M * 3 * D * D,
-                lambda: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
-                             F32, e_qkv, s))
+                lambda e: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
+                               F32, e, s), e_qkv)
         if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
             dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         else:

@@ -116,6 +116,16 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.state[p]["step"] = buf[i]
         return buf
 
+    def state_dict(self):
+        """torch.optim.AdamW's format.  With ``capturable`` every parameter that
+        requires grad gets a device step view, including ones that never had a
+        gradient; such step-only entries (no ``exp_avg`` / ``exp_avg_sq``) are
+        dropped, so the dict loads into torch.optim.AdamW (whose step raises a
+        KeyError on a non-empty state without the moments)."""
+        sd = super().state_dict()
+        sd["state"] = {k: v for k, v in sd["state"].items() if "exp_avg" in v}
+        return sd
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

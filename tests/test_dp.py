@@ -29,13 +29,43 @@ def _free_port():
     return p
 
 
+class SlotLinear(torch.autograd.Function):
+    """x @ w^T whose weight gradient is written straight into the reducer's
+    bucket slot when one is published (functional.grad_dest), as the HIP
+    linear / conv weight-gradient launches do: .grad then aliases the flat
+    buffer that the bucket all-reduce sums in place."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        import hvit_amd.functional as HF
+
+        x, w = ctx.saved_tensors
+        dw = g.reshape(-1, g.shape[-1]).t() @ x.reshape(-1, x.shape[-1])
+        dest = HF.grad_dest(id(w), tuple(w.shape))
+        if dest is not None:
+            dest.copy_(dw)
+            dw = dest
+        return g @ w, dw
+
+
+class SlotFc(torch.nn.Linear):
+    def forward(self, x):
+        return SlotLinear.apply(x, self.weight) + self.bias
+
+
 class Toy(torch.nn.Module):
-    """Stand-in with HybridViT's gradient shapes of interest."""
+    """Stand-in with HybridViT's gradient shapes of interest (fc1's weight
+    gradient lands in its bucket slot like the HIP weight gradients)."""
 
     def __init__(self):
         super().__init__()
         self.pos_embed = torch.nn.Parameter(torch.randn(1, 50, 8) * 0.1)
-        self.fc1 = torch.nn.Linear(8, 32)
+        self.fc1 = SlotFc(8, 32)
         self.fc2 = torch.nn.Linear(32, 8)
         self.shared = torch.nn.Parameter(torch.randn(8) * 0.1)
         self.unused = torch.nn.Parameter(torch.zeros(3))
@@ -85,7 +115,14 @@ def _worker(rank, world, port, bucket_mb, q):
             for n, p in ref.named_parameters():
                 if p.grad is not None:
                     grads[n] += p.grad / world
-        err = 0.0
+        import hvit_amd.functional as HF
+
+        # the slot path was taken: fc1's .grad is a view of its bucket buffer
+        adopted = any(model.fc1.weight.grad.data_ptr() == f.data_ptr() + 0 or
+                      f.data_ptr() <= model.fc1.weight.grad.data_ptr() < f.data_ptr() + 4 * f.numel()
+                      for fl in red.flats for f in fl if f is not None)
+        assert HF.GRAD_DEST, "no bucket slots published"
+        err = 0.0 if adopted else 1.0
         for n, p in model.named_parameters():
             g = p.grad if p.grad is not None else torch.zeros_like(p)
             err = max(err, (g - grads[n]).abs().max().item())
@@ -121,7 +158,9 @@ def test_grad_allreduce_matches_full_batch(bucket_mb):
 
 def _worker_accum(rank, world, port, mode, q):
     """Gradient accumulation (trainer.py:164-183): two micro-batches per step,
-    with hooks live on both (mode 'hooks': stale buckets re-reduced) or the
+    with hooks live on both (mode 'hooks': buckets already reduced in place --
+    fc1's weight gradient lives in the bucket buffer -- are turned into means
+    before the second micro-batch accumulates, then re-reduced) or the
     first under no_sync() (mode 'no_sync'); zero_grad with set_to_none False
     (grads stay views of the reducer's buffers) or True."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"

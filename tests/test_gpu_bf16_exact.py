@@ -125,9 +125,12 @@ def test_linear_dgrad_kinds_exact(env, cfg):
     w2 = rb(D, HID, scale=D ** -0.5)
     h = rb(M, HID)
     dh = torch.empty(M, HID, device=DEV, dtype=BF)
-    cs = torch.zeros(HID, device=DEV)
+    # colsum: one partial row per 64-row block (deterministic, no atomics), NaN-poisoned
+    # so a row the epilogue fails to write shows up
+    csr = torch.full((M // 64, HID), float("nan"), device=DEV)
     L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh.data_ptr(), L.BF16,
-           HF.epilogue(act=L.ACT_GELU_BWD, aux=h, drop=L.dropout(0.1, 23, 304), colsum=cs), s())
+           HF.epilogue(act=L.ACT_GELU_BWD, aux=h, drop=L.dropout(0.1, 23, 304), colsum=csr), s())
+    cs = csr.sum(0)
     hp = h.float().requires_grad_(True)
     F.gelu(hp).backward(torch.ones_like(hp))
     mk = torch.as_tensor(keep_mask(23, 304, M * HID, 0.1).reshape(M, HID), device=DEV)
@@ -136,9 +139,10 @@ def test_linear_dgrad_kinds_exact(env, cfg):
     check_f32(cs, ref.sum(0), acc=1e-4, what=f"fc2 dgrad colsum cfg {cfg}")
     # the model's form: MUL_AUX with the stored gelu'(h) (bf16) as the multiplier
     gd = hp.grad.to(BF)
-    cs.zero_()
+    csr.fill_(float("nan"))
     L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh.data_ptr(), L.BF16,
-           HF.epilogue(act=L.ACT_MUL_AUX, aux=gd, drop=L.dropout(0.1, 23, 304), colsum=cs), s())
+           HF.epilogue(act=L.ACT_MUL_AUX, aux=gd, drop=L.dropout(0.1, 23, 304), colsum=csr), s())
+    cs = csr.sum(0)
     ref = (g2.float() @ w2.float()) * mk / 0.9 * gd.float()
     check_bf16(dh, ref, what=f"fc2 dgrad MUL_AUX cfg {cfg}")
     check_f32(cs, ref.sum(0), acc=1e-4, what=f"fc2 dgrad MUL_AUX colsum cfg {cfg}")

@@ -141,5 +141,89 @@ def test_rccl_world1_bench_dp_branch():
     out = json.loads(line)
     assert out["config"]["dist_backend"] == "nccl"
     assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1"
-    assert out["launch"] == "eager"
+    # the DP step is captured whole (bucket all-reduces from the hooks included)
+    assert out["launch"] == "hipGraph replay of the whole step"
     assert out["value"] > 0 and abs(out["final_loss"]) < 1e3
+
+
+def test_rccl_world1_dp_graph_matches_eager():
+    """The captured DP step (RCCL, world 1: hook-launched bucket all-reduces,
+    finish(), FusedAdamW capturable, dropout on) replays exactly the steps an
+    eager copy takes from the same dropout seed state: parameters equal after
+    each of 3 replays (bitwise: the train step is deterministic), losses equal,
+    step counters advanced on the device."""
+    import json
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dp_graph_worker.py"), str(_free_port())],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["dropout_state_equal"]
+    assert out["steps"] == 5.0  # 2 warm-up + 3 replays
+    for a, b in out["losses"]:
+        assert abs(a - b) <= 1e-6 * abs(b), out["losses"]
+    assert out["exact"], out["rel"]
+
+
+def _worker_accum(rank, world, port, q):
+    """Two micro-batches per optimizer step with the hooks live on both and
+    zero_grad(set_to_none=True) (trainer.py:164-183 under DP): the ViT and conv
+    weight gradients of the first micro-batch live in the bucket buffers and are
+    reduced there in place before the second backward accumulates."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import copy
+        import importlib
+
+        import hvit_amd_loader
+
+        hv = hvit_amd_loader.load()
+        dp = importlib.import_module("hvit_amd.dp")
+        torch.cuda.set_device(0)
+        torch.manual_seed(11)
+        kw = dict(KW)
+        model = hv.HybridViT(**kw).cuda().train()
+        ref = copy.deepcopy(model)
+        g = torch.Generator().manual_seed(6)
+        xs = [torch.rand((world * 2, 1, 64, 64), generator=g) for _ in range(2)]
+        ts = [torch.rand((world * 2, 1, 64, 64), generator=g) for _ in range(2)]
+        crit = hv.CombinedLoss()
+        red = dp.GradAllReducer(model, bucket_mb=0.05)
+        sl = slice(rank * 2, (rank + 1) * 2)
+        model.zero_grad(set_to_none=True)
+        for x, t in zip(xs, ts):
+            crit(model(x[sl].cuda()), t[sl].cuda()).backward()
+        red.finish()
+        acc = {n: torch.zeros_like(p) for n, p in ref.named_parameters()}
+        for r in range(world):
+            m = copy.deepcopy(ref)
+            s2 = slice(r * 2, (r + 1) * 2)
+            for x, t in zip(xs, ts):
+                crit(m(x[s2].cuda()), t[s2].cuda()).backward()
+            for n, p in m.named_parameters():
+                acc[n] += p.grad / world
+        err = max(((p.grad - acc[n]).norm() / acc[n].norm().clamp_min(1e-20)).item()
+                  for n, p in model.named_parameters())
+        q.put((rank, err))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_accumulation_hooks_set_to_none_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_accum, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err in out:
+        assert err < 1e-5, (rank, err)

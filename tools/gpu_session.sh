@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-3 GPU-box session: steps run in order, each under its own time limit;
-# the script stops at the first crash / timeout.  Usage: tools/r3_check.sh TAG step...
+# GPU-box session: steps run in order, each under its own time limit; the
+# script stops at the first crash / timeout.  Usage: tools/gpu_session.sh TAG step...
 #   tests[:file,...]  GPU test files (default: all tests/test_gpu_*.py)
 #   bench             default bench.py line (graph mode, CPU baseline)
 #   benchq            bench.py without the CPU baseline
@@ -8,6 +8,7 @@
 #   prof              rocprofv3 kernel stats of a short bench
 #   gemm              tools/gemm_bench.py
 #   env:VAR=VAL,...   benchq under extra environment variables (A/B knobs)
+#   py:SCRIPT[:ARGS]  python SCRIPT ARGS (a probe under tools/; ARGS space-separated by '+')
 cd "$(dirname "$0")/.."
 TAG=${1:-run}; shift
 mkdir -p gpurun_out
@@ -32,6 +33,9 @@ for s in "$@"; do
       kv=${s#env:}; tagv=$(echo "$kv" | tr ',=' '__')
       env $(echo "$kv" | tr ',' ' ') timeout -k 10 400 python -u bench.py --no-cpu-baseline \
         > gpurun_out/${TAG}_env_${tagv}.log 2>&1 || exit $? ;;
+    py:*)
+      spec=${s#py:}; script=${spec%%:*}; args=""; [ "$spec" != "$script" ] && args=$(echo "${spec#*:}" | tr '+' ' ')
+      timeout -k 10 300 python -u $script $args > gpurun_out/${TAG}_$(basename $script .py).log 2>&1 || exit $? ;;
     gemm) timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/${TAG}_gemm.log 2>&1 || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

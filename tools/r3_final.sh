@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 TAG=${1:-r3f}; OP=${2:-vit_linear_dgrad}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/r3_check.sh $TAG tests bench prof || exit $?
+bash tools/gpu_session.sh $TAG tests bench prof || exit $?
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof -o run --output-format csv -- \
   python3 bench.py --roofline-only --roofline-op $OP > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $?
 echo "step roofprof ok"

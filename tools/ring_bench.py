@@ -93,12 +93,11 @@ def cases():
     # data gradients (fc2: GELU backward + bias-grad column sums; others plain)
     g2 = r(M, D)
     dh = torch.empty(M, HID, device=DEV, dtype=BF)
-    cs = torch.zeros(HID, device=DEV)
+    cs = torch.zeros((M // 64, HID), device=DEV)  # colsum partial rows (one per 64-row block)
     KEEP.extend([cs, h, a, b1, b2, bp])
     ep_g = HF.epilogue(act=L.ACT_GELU_BWD, aux=h, drop=L.dropout(0.1, 78, 302), colsum=cs)
 
     def fc2d():
-        cs.zero_()
         L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh.data_ptr(), L.BF16, ep_g, s())
     out.append(("dgrad fc2+geluB", 2 * M * D * HID, fc2d, [dh, cs]))
     dxn2 = torch.empty(M, D, device=DEV)
