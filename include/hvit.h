@@ -36,7 +36,8 @@ enum {
   HVIT_ACT_GELU_BWD = 3,
   HVIT_ACT_GELU_DUAL_D = 4, /* GELU_DUAL that stores gelu'(v) instead of v (for MUL_AUX) */
   HVIT_ACT_MUL_AUX = 5,     /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
-  HVIT_ACT_RELU = 6         /* conv forward only: v = max(v + bias, 0) (eval-mode BatchNorm folded) */
+  HVIT_ACT_RELU = 6,        /* conv forward only: v = max(v + bias, 0) (eval-mode BatchNorm folded) */
+  HVIT_ACT_GELU = 7         /* linear forward: y = dropout(gelu(v)) only (fc1 when no backward runs) */
 };
 /* flags of the backward calls that accumulate into caller memory:
  * HVIT_ACC_ZEROED says the caller already zeroed the accumulator outputs (one

@@ -552,7 +552,7 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
     f32x4 g, d;
 #pragma unroll
     for (int e = 0; e < 4; ++e) { const GeluGG t_ = gelu_gg(v[e]); g[e] = t_.g * keep[e]; d[e] = t_.d; }
-    store4v<FAST>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, nv, ep.out_dt);
+    if (ep.out) store4v<FAST>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, nv, ep.out_dt);
     store4v<FAST>(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
     return;
   }
@@ -1372,7 +1372,8 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
             { const GeluGG t_ = gelu_gg(va[e]); ga[e] = t_.g * ka[e]; da[e] = t_.d; }
             { const GeluGG t_ = gelu_gg(vb[e]); gb[e] = t_.g * kb[e]; db[e] = t_.d; }
           }
-          *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? wide8(da, db) : wide8(va, vb);
+          // (no out: the inference form, HVIT_ACT_GELU -- only gelu(v) is stored)
+          if (ep.out) *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? wide8(da, db) : wide8(va, vb);
           *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = wide8(ga, gb);
         } else {
           if (EK != EK_STORE && ep.drop_thr) {
@@ -1534,7 +1535,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           f32x4 g, d;
 #pragma unroll
           for (int e = 0; e < 4; ++e) { const GeluGG t_ = gelu_gg(v[e]); g[e] = t_.g * k[e]; d[e] = t_.d; }
-          store4v<true>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, 4, ep.out_dt);
+          if (ep.out) store4v<true>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, 4, ep.out_dt);
           store4v<true>(ep.out2, (long)m * ep.ldo2 + n, g, 4, ep.out2_dt);
         }
       } else if constexpr (EK == EK_RESID) {

@@ -36,6 +36,12 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
   ep.out2 = e->out2;
   ep.out2_dt = e->out2_dt;
   ep.ldo2 = ldo;
+  if (e->act == HVIT_ACT_GELU) {  // GELU_DUAL storing only dropout(gelu(v)), into y
+    ep.act = HVIT_ACT_GELU_DUAL;
+    ep.out2 = out;
+    ep.out2_dt = out_dt;
+    ep.out = nullptr;
+  }
   ep.aux = e->aux;
   ep.aux_dt = e->aux_dt;
   ep.ldaux = ldo;
@@ -78,7 +84,7 @@ int take_side(const hvit_slab_sum_t* jp, Epi& ep, int M, hipStream_t st) {
 
 int check_epi(const hvit_epilogue_t* e) {
   if (!e) return HVIT_OK;
-  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_RELU, "epilogue: bad act %d", e->act);
+  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_GELU, "epilogue: bad act %d", e->act);
   HVIT_CHECK((e->act != HVIT_ACT_GELU_DUAL && e->act != HVIT_ACT_GELU_DUAL_D) || e->out2,
              "epilogue: GELU_DUAL needs out2");
   HVIT_CHECK((e->act != HVIT_ACT_GELU_BWD && e->act != HVIT_ACT_MUL_AUX) || e->aux, "epilogue: GELU_BWD needs aux");

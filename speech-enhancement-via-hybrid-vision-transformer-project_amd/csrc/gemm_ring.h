@@ -283,7 +283,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
           { const GeluGG t_ = gelu_gg(va[e]); ga[e] = t_.g * ka[e]; da[e] = t_.d; }
           { const GeluGG t_ = gelu_gg(vb[e]); gb[e] = t_.g * kb[e]; db[e] = t_.d; }
         }
-        *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? pack8(da, db) : pack8(va, vb);
+        // (no out: the inference form, HVIT_ACT_GELU -- only gelu(v) is stored)
+        if (ep.out) *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? pack8(da, db) : pack8(va, vb);
         *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = pack8(ga, gb);
         continue;
       }

@@ -211,15 +211,24 @@ class GradAllReducer:
     def _launch(self, b):
         ps = self.buckets[b]
         offs, total = self.offsets[b]
+        dev = ps[0].grad.device
         flat = self.flats[b][self._gen]
-        if flat is None or flat.device != ps[0].grad.device:
-            flat = self.flats[b][self._gen] = torch.empty(total, dtype=torch.float32, device=ps[0].grad.device)
-        for p, o in zip(ps, offs):
-            v = self._view(p)
-            dst = flat[o:o + v.numel()].view_as(v)
-            if dst.data_ptr() != v.data_ptr():
-                dst.copy_(v)
-        self.works[b] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if flat is None or flat.device != dev:
+            flat = self.flats[b][self._gen] = torch.empty(total, dtype=torch.float32, device=dev)
+        ctx = contextlib.nullcontext()
+        if dev.type == "cuda" and HF.side_pending(dev):
+            # weight gradients still in flight on the side stream (functional.on_side):
+            # copy and reduce from there, after everything issued on both streams
+            s = HF.side_stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            ctx = torch.cuda.stream(s)
+        with ctx:
+            for p, o in zip(ps, offs):
+                v = self._view(p)
+                dst = flat[o:o + v.numel()].view_as(v)
+                if dst.data_ptr() != v.data_ptr():
+                    dst.copy_(v)
+            self.works[b] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish(self):
         """Wait for every bucket (launching any whose hooks did not fire, e.g.

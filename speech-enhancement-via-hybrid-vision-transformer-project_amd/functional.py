@@ -326,7 +326,7 @@ def linear_wgrad_deferred(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None,
     return dw, Deferred(job, ws)
 
 
-def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=None, dest=None):
+def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=None, dest=None, out=None):
     """dw [N, K] = dy^T x (f32); with ``bias`` also db [N] = colsum(dy), which
     the bf16 path fuses into the GEMM (db stored right after dw).  ``tickets``
     (a zeroed f32 tensor of at least wgrad_tickets(M, N, K) elements, e.g. a
@@ -335,7 +335,9 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=Non
     if dest is not None and not bias:  # the parameter's data-parallel bucket slot (grad_dest)
         dw, db = dest.view(N, K), None
     else:
-        buf = torch.empty(N * K + (N if bias else 0), dtype=torch.float32, device=dy.device)
+        # (out: a caller's [N*K (+N)] buffer)
+        buf = out if out is not None else torch.empty(N * K + (N if bias else 0), dtype=torch.float32,
+                                                      device=dy.device)
         dw = buf[:N * K].view(N, K)
         db = buf[N * K:] if bias else None
     ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
@@ -355,6 +357,17 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=Non
     return (dw, db) if bias else dw
 
 
+def _linear_wgrad_bias_maybe_side(ctx, dt, dy, x, M, N, K):
+    """(dw, db) of a biased Linear (head / skip projections) on the side stream
+    when side_ok, else on the backward's stream."""
+    if not side_ok(ctx.prefs):
+        return linear_wgrad(dt, dy, x, M, N, K, bias=True)
+    buf = torch.empty(N * K + N, dtype=torch.float32, device=dy.device)
+    with on_side(dy.device, (dy, x, buf)):
+        linear_wgrad(dt, dy, x, M, N, K, bias=True, out=buf)
+    return buf[:N * K].view(N, K), buf[N * K:]
+
+
 def dropout_scale(g, M, N, drop, rowscale, rps, out, colsum=None):
     """out = rowscale * dropout(g) in out's dtype; colsum (f32 [N], zeroed)
     += column sums of it (per-workgroup partials in a scratch slab)."""
@@ -365,6 +378,107 @@ def dropout_scale(g, M, N, drop, rowscale, rps, out, colsum=None):
     with timed("dropout_scale", float(M * N * (g.element_size() + out.element_size()))):  # read g, write out
         call("hvit_dropout_scale", g.data_ptr(), L.dt_of(g), M, N, drop, ptr(rowscale), rps, out.data_ptr(),
              L.dt_of(out), ptr(colsum), ptr(ws), ws_n, stream_ptr())
+
+
+def linear_wgrad_now(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None, side: Optional["Deferred"] = None):
+    """dw [N, K] = dy^T x (f32), complete on the current stream when its
+    launches are: the weight gradient with its split-K slab sum (and an incoming
+    side job) issued back to back (the side-stream form, where no data-gradient
+    launch follows on the same stream to carry the sum)."""
+    dw, d = linear_wgrad_deferred(dt, dy, x, M, N, K, tag=tag, dest=dest, side=side)
+    if d is not None and d.job.n > 0:
+        j = d.job
+
+        def launch():
+            call("hvit_sum_slabs_strided", j.src, j.splits, j.stride, j.n, j.dst, stream_ptr())
+
+        with timed(tag, 0.0):
+            launch()
+        _record(tag, (lambda d=d: launch(), 0.0))
+    return dw
+
+
+# ---------------------------------------------------------------------------
+# Weight gradients on a side stream (round 4).  A weight gradient is off the
+# critical path of the backward (nothing reads it before the optimizer), so
+# the ViT blocks issue theirs on a per-device side stream that forks from the
+# backward's stream where its operands are ready; the data-gradient chain
+# runs on concurrently.  The side stream is joined back into the stream that
+# called backward() by an autograd final callback, before the optimizer, clip
+# or the caller can read a gradient; the data-parallel reducer launches its
+# bucket all-reduces from the side stream while work is pending there.  A
+# weight gradient that a backward ACCUMULATES into an existing .grad stays on
+# the backward's stream (autograd reads it right away).  Tensors crossing the
+# streams are registered with record_stream, so the caching allocator never
+# recycles them under a pending side launch.  Graph capture forks and joins
+# the side stream like any other (parallel branches of the captured step).
+SIDE = os.environ.get("HVIT_SIDE", "1") != "0"  # A/B knob: 0 = every launch on the backward's stream
+_SIDE_STREAMS = {}
+_SIDE_OPEN = set()
+
+
+def _dev_index(dev) -> int:
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def side_stream(dev) -> "torch.cuda.Stream":
+    i = _dev_index(dev)
+    s = _SIDE_STREAMS.get(i)
+    if s is None:
+        s = _SIDE_STREAMS[i] = torch.cuda.Stream(device=i)
+    return s
+
+
+def side_pending(dev) -> bool:
+    """Side-stream work not yet joined back (during a backward)."""
+    return _dev_index(dev) in _SIDE_OPEN
+
+
+def _join_side():
+    for i in list(_SIDE_OPEN):
+        torch.cuda.current_stream(i).wait_stream(_SIDE_STREAMS[i])
+    _SIDE_OPEN.clear()
+
+
+class on_side:
+    """``with on_side(dev, tensors):`` launches on the device's side stream,
+    ordered after everything issued so far on the current stream; ``tensors``
+    (produced or consumed across the two streams) are recorded on the side
+    stream.  Registers the join for the end of this backward."""
+
+    __slots__ = ("dev", "tensors", "ctx")
+
+    def __init__(self, dev, tensors=()):
+        self.dev, self.tensors = dev, tensors
+
+    def __enter__(self):
+        i = _dev_index(self.dev)
+        s = side_stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(i))
+        if i not in _SIDE_OPEN:
+            _SIDE_OPEN.add(i)
+            torch.autograd.Variable._execution_engine.queue_callback(_join_side)
+        for t in self.tensors:
+            if t is not None:
+                t.record_stream(s)
+        self.ctx = torch.cuda.stream(s)
+        self.ctx.__enter__()
+        return s
+
+    def __exit__(self, *exc):
+        return self.ctx.__exit__(*exc)
+
+
+def side_ok(prefs) -> bool:
+    """The weight gradients of these parameters may go to the side stream: no
+    parameter already holds a .grad that this backward would accumulate into."""
+    if not SIDE:
+        return False
+    for r in prefs:
+        p = r()
+        if p is not None and p.grad is not None:
+            return False
+    return True
 
 
 class Deferred:
@@ -420,6 +534,21 @@ def conv_wgrad(dt, g: L.ConvGeom, dz, wshape, dest=None) -> torch.Tensor:
         launch()
     _record("conv_wgrad", (launch, 2.0 * P * co * ci * ks * ks))
     return dw.view(wshape)
+
+
+def _conv_wgrad_maybe_side(ctx, dt, g, dz, w, srcs):
+    """A conv weight gradient on the side stream when side_ok (its operands:
+    dz and the conv input tensors behind the geometry's raw pointers), else on
+    the backward's stream; into the parameter's data-parallel slot when one is
+    published."""
+    dest = grad_dest(*ctx.wid)
+    if not side_ok(ctx.prefs):
+        return conv_wgrad(dt, g, dz, w.shape, dest)
+    if dest is None:
+        dest = torch.empty(w.shape, dtype=torch.float32, device=dz.device)
+    with on_side(dz.device, (dz, dest) + tuple(srcs)):
+        conv_wgrad(dt, g, dz, w.shape, dest)
+    return dest.view(w.shape)
 
 
 @dataclass
@@ -548,6 +677,7 @@ class ConvBNActFn(torch.autograd.Function):
                  gamma.data_ptr(), beta.data_ptr(), dr, pool, y.data_ptr(), dt, s)
         ctx.save_for_backward(x1, x2, w, gamma, beta)
         ctx.wid = (id(w), tuple(w.shape))
+        ctx.prefs = (weakref.ref(w),)
         ctx.z, ctx.mean, ctx.invstd = z, mean, invstd
         ctx.meta = (U, pool, training, dr, dt)
         ctx.sg = sg
@@ -574,7 +704,7 @@ class ConvBNActFn(torch.autograd.Function):
                  dz.data_ptr(), dt, sums.data_ptr(), L.ACC_ZEROED, s)
         dbeta, dgamma = sums[:Cout], sums[Cout:2 * Cout]
         g = geom(x1, C1, x2, C2, N, Hs, Ws, U, KS, 1, KS // 2, Cout)
-        dw = conv_wgrad(dt, g, dz, w.shape, grad_dest(*ctx.wid))
+        dw = _conv_wgrad_maybe_side(ctx, dt, g, dz, w, (x1, x2))
         dx1 = dx2 = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             wd = pack_conv(w, 1, dt)
@@ -708,6 +838,7 @@ class PatchEmbedFn(torch.autograd.Function):
         call("hvit_conv_fwd", dt, g, wp.data_ptr(), b.data_ptr(), x0.data_ptr(), F32, None, e, s)
         ctx.save_for_backward(feat, w)
         ctx.wid = (id(w), tuple(w.shape))
+        ctx.prefs = (weakref.ref(w),)
         ctx.wp = wp
         ctx.meta = (Pp, dr, dt, Nt, None if pos is None else pos.shape)
         ctx.sg = sg
@@ -732,7 +863,7 @@ class PatchEmbedFn(torch.autograd.Function):
             dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
             call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
         g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
-        dw = conv_wgrad(dt, g, gd, w.shape, grad_dest(*ctx.wid))
+        dw = _conv_wgrad_maybe_side(ctx, dt, g, gd, w, (feat,))
         dfeat = None
         if ctx.needs_input_grad[0]:
             dfeat = _empty(feat.shape, dt, dev)
@@ -866,7 +997,7 @@ class ViTBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, H, drops, dpr, training,
                 dt, want_probs, attn_fp8=False, ho_in: Optional[GradHandoff] = None,
-                ho_out: Optional[GradHandoff] = None):
+                ho_out: Optional[GradHandoff] = None, nograd: bool = False):
         B, Nt, D = x.shape
         M = B * Nt
         hd = D // H
@@ -913,12 +1044,19 @@ class ViTBlockFn(torch.autograd.Function):
         xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
         W1 = cast(f1w, dt)
         # the fc1 epilogue keeps gelu'(h) (not h) for the backward: the fc2 dgrad
-        # epilogue then multiplies instead of re-evaluating erf / exp per element
-        gh = _empty((M, hid), dt, dev)
+        # epilogue then multiplies instead of re-evaluating erf / exp per element;
+        # with no backward to run (eval / no-grad inference) it stores gelu(h) only
         a = _empty((M, hid), dt, dev)
-        with timed("vit_linear_fwd", 2.0 * M * hid * D):
-            call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, gh.data_ptr(), dt,
-                 epilogue(act=L.ACT_GELU_DUAL_D, out2=a, drop=d_fc1.c()), s)
+        if not nograd:
+            gh = _empty((M, hid), dt, dev)
+            with timed("vit_linear_fwd", 2.0 * M * hid * D):
+                call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, gh.data_ptr(),
+                     dt, epilogue(act=L.ACT_GELU_DUAL_D, out2=a, drop=d_fc1.c()), s)
+        else:
+            gh = None
+            with timed("vit_linear_fwd", 2.0 * M * hid * D):
+                call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, a.data_ptr(), dt,
+                     epilogue(act=L.ACT_GELU, drop=d_fc1.c()), s)
         W2 = cast(f2w, dt)
         x2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         with timed("vit_linear_fwd", 2.0 * M * D * hid):
@@ -926,6 +1064,8 @@ class ViTBlockFn(torch.autograd.Function):
                  epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
         ctx.save_for_backward(n1w, n2w)
         ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
+        # the parameters whose gradients the side stream may produce (side_ok)
+        ctx.prefs = tuple(weakref.ref(p) for p in (qkvw, qkvb, pw, f1w, f1b, f2w))
         ctx.kbits = kbits
         # the fc2 branch's dropout / DropPath of the incoming gradient, for the
         # next consumer of x2 to fuse into its LayerNorm backward (GradHandoff)
@@ -964,9 +1104,22 @@ class ViTBlockFn(torch.autograd.Function):
             df2b = zf2b.take(dev)
             dropout_scale(dx2, M, D, drf2, rs2, Nt, g2, df2b)
         dq_id, dp_id, d1_id, d2_id = ctx.wid
-        # each weight gradient's split-K slab sum rides on the data-gradient launch
-        # that follows it (epilogue side job): no reduction launch of its own
-        df2w, j2 = linear_wgrad_deferred(dt, g2, a, M, D, hid, dest=grad_dest(*d2_id))
+        # weight gradients: on the side stream, concurrent with this chain of data
+        # gradients (side_ok), or else on this stream with each split-K slab sum riding
+        # on the data-gradient launch that follows it (epilogue side job)
+        side = side_ok(ctx.prefs)
+
+        def wdest(wid, N, K):
+            d = grad_dest(*wid)
+            return d if d is not None else torch.empty((N, K), dtype=torch.float32, device=dev)
+
+        if side:
+            df2w = wdest(d2_id, D, hid)
+            with on_side(dev, (g2, a, df2w)):
+                linear_wgrad_now(dt, g2, a, M, D, hid, dest=df2w)
+            j2 = None
+        else:
+            df2w, j2 = linear_wgrad_deferred(dt, g2, a, M, D, hid, dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
         # fc1 bias grad: the GELU-backward epilogue's column sums, one partial row per
         # 64-row block (plain stores: deterministic), summed in row order as the fc1
@@ -979,7 +1132,13 @@ class ViTBlockFn(torch.autograd.Function):
                 lambda e: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt, e,
                                s), e_fc2, (gh, cparts))
         jc = Deferred(L.SlabSum(cparts.data_ptr(), df1b.data_ptr(), hid, hid, nrow), cparts)
-        df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id), side=jc)
+        if side:
+            df1w = wdest(d1_id, hid, D)
+            with on_side(dev, (dh, xn2, cparts, df1b, df1w)):
+                linear_wgrad_now(dt, dh, xn2, M, hid, D, dest=df1w, side=jc)
+            j1 = None
+        else:
+            df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id), side=jc)
         dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         e_fc1 = epilogue(side=j1)
         _launch("vit_linear_dgrad", 2.0 * M * hid * D,
@@ -993,7 +1152,13 @@ class ViTBlockFn(torch.autograd.Function):
             dpb = zpb.take(dev)
             dropout_scale(dx1, M, D, drp, rs1, Nt, g1, dpb)
         # attention branch
-        dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id))
+        if side:
+            dpw = wdest(dp_id, D, D)
+            with on_side(dev, (g1, o, dpw)):
+                linear_wgrad_now(dt, g1, o, M, D, D, dest=dpw)
+            jp = None
+        else:
+            dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id))
         do = _empty((M, D), dt, dev)
         e_pr = epilogue(side=jp)
         _launch("vit_linear_dgrad", 2.0 * M * D * D,
@@ -1020,7 +1185,13 @@ class ViTBlockFn(torch.autograd.Function):
                      D // H, scale, dra, ptr(ctx.kbits), dqkv.data_ptr(), delta.data_ptr(), None, s)
             dqkvb = zqb.take(dev)
             call("hvit_reduce_rows", dqkv.data_ptr(), dt, M, 3 * D, 3 * D, 1, dqkvb.data_ptr(), s)
-        dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
+        if side:
+            dqkvw = wdest(dq_id, 3 * D, D)
+            with on_side(dev, (dqkv, xn1, dqkvw, dqkvb) + ((jb.ws,) if jb is not None else ())):
+                linear_wgrad_now(dt, dqkv, xn1, M, 3 * D, D, dest=dqkvw, side=jb)
+            jq = None
+        else:
+            dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
         dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         e_qkv = epilogue(side=jq)
         _launch("vit_linear_dgrad", 2.0 * M * 3 * D * D,
@@ -1031,7 +1202,7 @@ class ViTBlockFn(torch.autograd.Function):
         else:
             dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 class HeadFn(torch.autograd.Function):
@@ -1052,6 +1223,7 @@ class HeadFn(torch.autograd.Function):
              stream_ptr())
         ctx.save_for_backward(nw)
         ctx.t = (x2d, xn, m, r, W)
+        ctx.prefs = (weakref.ref(w), weakref.ref(b))
         ctx.meta = (B, Nt, D, C, dt)
         ctx.ho = ho if LNDROP else None
         ctx.zs = _zs(ctx, 3 * D)
@@ -1064,7 +1236,7 @@ class HeadFn(torch.autograd.Function):
         B, Nt, D, C, dt = ctx.meta
         M = B * Nt
         dy = cast(dy, dt)
-        dw, db = linear_wgrad(dt, dy, xn, M, C, D, bias=True)
+        dw, db = _linear_wgrad_bias_maybe_side(ctx, dt, dy, xn, M, C, D)
         dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
         call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32, None,
              stream_ptr())
@@ -1097,6 +1269,7 @@ class SkipFn(torch.autograd.Function):
         M = N * Ho * Wo
         call("hvit_linear_fwd", dt, r.data_ptr(), W.data_ptr(), b.data_ptr(), M, Cd, Ce, y.data_ptr(), dt, None, s)
         ctx.t = (r, W)
+        ctx.prefs = (weakref.ref(w), weakref.ref(b))
         ctx.meta = (N, He, We, Ce, Ho, Wo, Cd, dt, tuple(w.shape))
         ctx.sg = sg
         return y
@@ -1109,7 +1282,7 @@ class SkipFn(torch.autograd.Function):
         dev = r.device
         s = stream_ptr()
         dy = cast(dy, dt)
-        dw, db = linear_wgrad(dt, dy, r, M, Cd, Ce, bias=True)
+        dw, db = _linear_wgrad_bias_maybe_side(ctx, dt, dy, r, M, Cd, Ce)
         dw = dw.view(wshape)
         de = None
         if ctx.needs_input_grad[0]:

@@ -425,7 +425,8 @@ class HybridViT(nn.Module):
             else:
                 h = HF.ConvBNActFn.apply(h, None, blk.conv.weight, bn.weight, bn.bias, bn.running_mean,
                                          bn.running_var, bn.num_batches_tracked, 1, blk.pool, self.training,
-                                         HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt, sg)
+                                         HF.Drop(blk.p, 0, 100 + i, seed), bn.momentum, bn.eps, dt, sg,
+                                         not torch.is_grad_enabled())
             skips.append(h)
         return h, skips
 
@@ -471,7 +472,8 @@ class HybridViT(nn.Module):
                                            a.proj.weight, a.proj.bias, blk.norm2.weight, blk.norm2.bias,
                                            m[0].weight, m[0].bias, m[3].weight, m[3].bias, a.num_heads, drops,
                                            blk.dpr, self.training, dt, want_attn,
-                                           self.attention_precision == "fp8" and dt == L.BF16, ho_in, ho)
+                                           self.attention_precision == "fp8" and dt == L.BF16, ho_in, ho,
+                                           not torch.is_grad_enabled())
             attns.append(probs)
         return t, attns, ho
 
