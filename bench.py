@@ -206,11 +206,24 @@ def cpu_baseline(batch, budget_s):
         print(f"cpu baseline: step {len(times)} {times[-1]:.1f} s", file=sys.stderr, flush=True)
     times.sort()
     dt = times[len(times) // 2]
+    # the B=32 eval forward too (BASELINE config 2's CPU counterpart; the survey's
+    # 1.82 s reference figure is this measurement): 1 warmup + best of 2
+    with torch.no_grad():
+        O.forward(sd, x, cfg, training=False)
+        fts = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            O.forward(sd, x, cfg, training=False)
+            fts.append(time.perf_counter() - t1)
+    ft = min(fts)
+    print(f"cpu baseline: eval forward {ft:.2f} s", file=sys.stderr, flush=True)
     return {"value": round(batch * FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": torch.get_num_threads(),
             "kind": "port", "cpu": cpu_model(),
             "sample": f"oracle/hvit_oracle.py fp32 train step (fwd+CombinedLoss+bwd+clip+AdamW), B={batch}, "
                       f"1x256x256 synthetic spectrograms, 1 warmup + {len(times)} timed steps, median "
-                      f"{dt:.2f} s/step (all: {', '.join(f'{t:.2f}' for t in times)})"}
+                      f"{dt:.2f} s/step (all: {', '.join(f'{t:.2f}' for t in times)})",
+            "fwd_value": round(batch * FRAMES / ft, 2),
+            "fwd_sample": f"the same oracle's B={batch} eval forward (no grad), 1 warmup + best of 2: {ft:.2f} s"}
 
 
 def main():

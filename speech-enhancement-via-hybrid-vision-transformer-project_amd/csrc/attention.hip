@@ -485,7 +485,7 @@ __global__ __launch_bounds__(AT_THREADS) void mhsa_dkv_kernel(const T* __restric
 // operand (V^T, K^T, dO^T, Q^T) is read with ds_read_b64_tr_b16.  A lane's 4
 // keys also form one dropout-hash group (one 64-bit hash per 16x16 tile).
 // ============================================================================
-constexpr int V2_KMAX = 256;
+constexpr int V2_KMAX = 512;  // the largest token count of the register-resident kernels
 constexpr int V2_ROWB = 128;  // bytes per 64-element bf16 row
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
@@ -583,15 +583,21 @@ __device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uin
 // forward: workgroup = (b, h, 16*WAVES queries); wave = 16 queries x all keys.
 // WAVES = 16 covers all N <= 256 queries of a (b, h) in one workgroup, so K
 // and V are staged into LDS once per (b, h) instead of once per 64 queries.
-template <int WAVES>
+// KMAX = 512 (256 < N <= 512, a 4-8 s clip's token count): K and V of all keys
+// in LDS (128 KiB) and the keys taken in chunks of 256 with an online softmax
+// (running max and sum, the output rescaled when the max grows); for N <= 256
+// the one chunk gives exactly the single-pass arithmetic.  The KMAX = 512 form
+// runs 8-wave workgroups (152 VGPRs; at 16 waves the 128-VGPR budget spilled).
+template <int WAVES, int KMAX>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int N, int H, float scale,
                                                          uint32_t thr, float dscale, DSeed seed_,
                                                          uint32_t site, uint32_t* __restrict__ kbits) {
   const unsigned long long seed = seed_;
-  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB];
+  constexpr int CH = 256;  // keys per softmax chunk (the register-resident score block)
+  __shared__ __attribute__((aligned(16))) char smem[2 * KMAX * V2_ROWB];
   char* Ks = smem;
-  char* Vs = smem + V2_KMAX * V2_ROWB;
+  char* Vs = smem + KMAX * V2_ROWB;
   const int D = H * 64;
   const long pitch = 3L * D;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -599,8 +605,6 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   const int frow = lane & 15, fq = lane >> 4;
   const V2Lane LN(lane);
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
-  const int NK = (N + 15) & ~15;
-  const int nkt = NK >> 4;
   const int NK32 = (N + 31) & ~31;  // staged rows: whole tile pairs
   const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;  // this lane's query
   u32x4 qf[2];
@@ -611,95 +615,118 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK32);
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
-  // S^T tiles: st[j][r] = score(key 16j + 4fq + r, query q) in log2 units
-  // (keys >= N of the last, partial tile masked to -inf).  VALU diet: the 1/sum
-  // and the dropout 1/(1-p) on the 16 outputs instead of the 64
-  // probabilities, the dropout mask a select, masking only in a partial tile.
-  f32x4 st[V2_KMAX / 16];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < V2_KMAX / 16; ++j) {
-    if (j < nkt) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      a = v2_mma32(v2_fragj(Ks, LN, j, 0), qf[0], a);
-      a = v2_mma32(v2_fragj(Ks, LN, j, 1), qf[1], a);
-      if (16 * j + 16 > N) {  // wave-uniform: only a partial last tile
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a[r] *= c2;
-        mx = fmaxf(mx, a[r]);
-      }
-      st[j] = a;
-    }
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  // (exp2(fma(s, c2, -mx c2)) on the raw scores measured run-to-run
-  // nondeterministic at the bf16-ulp level in this kernel -- tools/det_check.py
-  // -- so the scores are scaled first, as before)
-  const float mxc = mx;  // the max in log2 units
-  float sum = 0.f;
-#pragma unroll
-  for (int j = 0; j < V2_KMAX / 16; ++j) {
-    if (j < nkt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = __builtin_amdgcn_exp2f(st[j][r] - mxc);
-        st[j][r] = p;
-        sum += p;
-      }
-    }
-  }
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
-  const float inv = 1.f / sum;
   const uint64_t bh = (uint64_t)b * H + h;
-  // O^T[d][q] += V^T[d][keys] P^T[keys][q]   (4 d-blocks of 16), two key tiles
-  // per 16x16x32 MFMA: the B operand is this lane's P of tiles 2jp, 2jp + 1
-  // (keys 16(2jp + e/4) + 4fq + e%4), the A operand the matching transposed
-  // reads of V.  A missing odd tile is P = 0 against staged (finite) V rows.
+  const uint64_t BHN = (uint64_t)gridDim.z * H * N;  // keep-bit chunk stride (queries)
+  const uint32_t rk = rng_key(seed, site);
+  const uint64_t qrow = (bh * N + (q < N ? q : 0)) * (uint64_t)N;
+  // O^T[d][q] += V^T[d][keys] P^T[keys][q]   (4 d-blocks of 16)
   f32x4 ot[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // keep bits for the backward (kbits non-null): bit 8*jp + 4*e + r of this
-  // lane's word pair = keep(q, key 32*jp + 16*e + 4*fq + r)
-  uint32_t kb[2] = {0u, 0u};
-  const uint32_t rk = rng_key(seed, site);
-  const uint64_t qrow = (bh * N + (q < N ? q : 0)) * (uint64_t)N;
+  float mxc = -INFINITY, sum = 0.f;
 #pragma unroll
-  for (int jp = 0; jp < V2_KMAX / 32; ++jp) {
-    if (2 * jp < nkt) {
-      f32x4 p0 = st[2 * jp];
-      f32x4 p1 = (2 * jp + 1 < nkt) ? st[2 * jp + 1] : (f32x4){0.f, 0.f, 0.f, 0.f};
-      if (thr) {
-        uint32_t b8 = 0u;
+  for (int c0 = 0; c0 < KMAX; c0 += CH) {
+    if (c0 >= N) break;
+    // (no scheduling across chunks: the next chunk's score block would be live
+    // beside this one's -- spills at the 128-VGPR budget of 16 waves)
+    __builtin_amdgcn_sched_barrier(0);
+    const int nkt = (min(N - c0, CH) + 15) >> 4;  // key tiles of this chunk
+    const char* Kc = Ks + c0 * V2_ROWB;
+    const char* Vc = Vs + c0 * V2_ROWB;
+    // S^T tiles: st[j][r] = score(key c0 + 16j + 4fq + r, query q) in log2 units
+    // (keys >= N of the last, partial tile masked to -inf).  VALU diet: the 1/sum
+    // and the dropout 1/(1-p) on the 16 outputs instead of the 64
+    // probabilities, the dropout mask a select, masking only in a partial tile.
+    f32x4 st[CH / 16];
+    float mx = -INFINITY;
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          if (2 * jp + e < nkt) {
-            const uint64_t i0 = qrow + 32 * jp + 16 * e + 4 * fq;
-            const uint32_t h0 = rng_pair(rk, i0), h1 = rng_pair(rk, i0 + 2);
-            const bool k0 = (h0 & 0xffffu) >= thr, k1 = (h0 >> 16) >= thr;
-            const bool k2 = (h1 & 0xffffu) >= thr, k3 = (h1 >> 16) >= thr;
-            f32x4& pp = e ? p1 : p0;
-            pp[0] = k0 ? pp[0] : 0.f;
-            pp[1] = k1 ? pp[1] : 0.f;
-            pp[2] = k2 ? pp[2] : 0.f;
-            pp[3] = k3 ? pp[3] : 0.f;
-            b8 |= ((uint32_t)k0 | ((uint32_t)k1 << 1) | ((uint32_t)k2 << 2) | ((uint32_t)k3 << 3)) << (4 * e);
-          }
+    for (int j = 0; j < CH / 16; ++j) {
+      if (j < nkt) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        a = v2_mma32(v2_fragj(Kc, LN, j, 0), qf[0], a);
+        a = v2_mma32(v2_fragj(Kc, LN, j, 1), qf[1], a);
+        if (c0 + 16 * j + 16 > N) {  // wave-uniform: only a partial last tile
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + 16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
         }
-        kb[jp >> 2] |= b8 << (8 * (jp & 3));
-      }
-      const u32x4 pb = v2_cat(v2_pack(p0), v2_pack(p1));
 #pragma unroll
-      for (int t = 0; t < 4; ++t) ot[t] = v2_mma32(v2_trj2(Vs, LN, 2 * jp, t), pb, ot[t]);
+        for (int r = 0; r < 4; ++r) {
+          a[r] *= c2;
+          mx = fmaxf(mx, a[r]);
+        }
+        st[j] = a;
+      }
     }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    // (exp2(fma(s, c2, -mx c2)) on the raw scores measured run-to-run
+    // nondeterministic at the bf16-ulp level in this kernel -- tools/det_check.py
+    // -- so the scores are scaled first, as before)
+    const float mnew = fmaxf(mxc, mx);  // the running max in log2 units
+    if (c0 > 0) {  // online softmax: rescale what the earlier chunks accumulated
+      const float rs = __builtin_amdgcn_exp2f(mxc - mnew);
+      sum *= rs;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ot[t] *= rs;
+    }
+    mxc = mnew;
+    float csum = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH / 16; ++j) {
+      if (j < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(st[j][r] - mxc);
+          st[j][r] = pv;
+          csum += pv;
+        }
+      }
+    }
+    csum += __shfl_xor(csum, 16, 64);
+    csum += __shfl_xor(csum, 32, 64);
+    sum += csum;
+    // two key tiles per 16x16x32 MFMA: the B operand is this lane's P of tiles
+    // 2jp, 2jp + 1 (keys c0 + 16(2jp + e/4) + 4fq + e%4), the A operand the
+    // matching transposed reads of V.  A missing odd tile is P = 0 against
+    // staged (finite) V rows.
+    // keep bits for the backward (kbits non-null): bit 8*jp + 4*e + r of this
+    // lane's word pair of chunk c0/256 = keep(q, key c0 + 32*jp + 16*e + 4*fq + r)
+    uint32_t kb[2] = {0u, 0u};
+#pragma unroll
+    for (int jp = 0; jp < CH / 32; ++jp) {
+      if (2 * jp < nkt) {
+        f32x4 p0 = st[2 * jp];
+        f32x4 p1 = (2 * jp + 1 < nkt) ? st[2 * jp + 1] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (thr) {
+          uint32_t b8 = 0u;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            if (2 * jp + e < nkt) {
+              const uint64_t i0 = qrow + c0 + 32 * jp + 16 * e + 4 * fq;
+              const uint32_t h0 = rng_pair(rk, i0), h1 = rng_pair(rk, i0 + 2);
+              const bool k0 = (h0 & 0xffffu) >= thr, k1 = (h0 >> 16) >= thr;
+              const bool k2 = (h1 & 0xffffu) >= thr, k3 = (h1 >> 16) >= thr;
+              f32x4& pp = e ? p1 : p0;
+              pp[0] = k0 ? pp[0] : 0.f;
+              pp[1] = k1 ? pp[1] : 0.f;
+              pp[2] = k2 ? pp[2] : 0.f;
+              pp[3] = k3 ? pp[3] : 0.f;
+              b8 |= ((uint32_t)k0 | ((uint32_t)k1 << 1) | ((uint32_t)k2 << 2) | ((uint32_t)k3 << 3)) << (4 * e);
+            }
+          }
+          kb[jp >> 2] |= b8 << (8 * (jp & 3));
+        }
+        const u32x4 pb = v2_cat(v2_pack(p0), v2_pack(p1));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ot[t] = v2_mma32(v2_trj2(Vc, LN, 2 * jp, t), pb, ot[t]);
+      }
+    }
+    if (q < N && kbits && thr)
+      *(uint2*)(kbits + (((uint64_t)(c0 / CH) * BHN + bh * N + q) * 4 + fq) * 2) = make_uint2(kb[0], kb[1]);
   }
   if (q < N) {
+    const float inv = 1.f / sum;
     const float os = thr ? inv * dscale : inv;
     bf16_t* op = o + ((long)b * N + q) * D + h * 64;
 #pragma unroll
@@ -710,7 +737,6 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
       *(uint2*)(op + 16 * t + 4 * fq) = u;
     }
     if (fq == 0) lse[bh * N + q] = (mxc + log2f(sum)) * 0.6931471805599453f;
-    if (kbits && thr) *(uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2) = make_uint2(kb[0], kb[1]);
   }
 }
 
@@ -749,8 +775,9 @@ __device__ __forceinline__ void v2_colsum64(const f32x4 (&acc)[4], float mul, fl
 }
 
 // dQ (+ delta = rowsum(dO * O), written for the dK/dV kernel):
-// workgroup = (b, h, 16*WAVES queries); K, V images in LDS
-template <int WAVES>
+// workgroup = (b, h, 16*WAVES queries); K, V images of all keys in LDS
+// (KMAX = 512: 128 KiB; the forward's keep bits come in 256-key chunks)
+template <int WAVES, int KMAX>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                         const bf16_t* __restrict__ dout,
                                                         const float* __restrict__ lse, float* __restrict__ delta,
@@ -759,9 +786,9 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
                                                         uint32_t site, const uint32_t* __restrict__ kbits,
                                                         float* __restrict__ dbias) {
   const unsigned long long seed = seed_;
-  __shared__ __attribute__((aligned(16))) char smem[2 * V2_KMAX * V2_ROWB + WAVES * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * KMAX * V2_ROWB + WAVES * 64 * 4];
   char* Ks = smem;
-  char* Vs = smem + V2_KMAX * V2_ROWB;
+  char* Vs = smem + KMAX * V2_ROWB;
   const int D = H * 64;
   const long pitch = 3L * D;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -793,11 +820,17 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
   dl += __shfl_xor(dl, 32, 64);
   if (qv && fq == 0) delta[bh * N + q] = dl;
   const float lse2 = qv ? lse[bh * N + q] * 1.4426950408889634f : 0.f;
-  // the forward's keep bits of this lane's (query, key quad) positions (mhsa_fwd_v2)
-  unsigned long long kb64 = 0ull;
-  if (kbits && thr && qv) {
-    const uint2 w2 = *(const uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2);
-    kb64 = (unsigned long long)w2.x | ((unsigned long long)w2.y << 32);
+  // the forward's keep bits of this lane's (query, key quad) positions (mhsa_fwd_v2),
+  // one 64-bit word per 256-key chunk
+  unsigned long long kb64[KMAX / 256];
+#pragma unroll
+  for (int c = 0; c < KMAX / 256; ++c) {
+    kb64[c] = 0ull;
+    if (kbits && thr && qv && 256 * c < N) {
+      const uint64_t BHN = (uint64_t)gridDim.z * H * N;
+      const uint2 w2 = *(const uint2*)(kbits + (((uint64_t)c * BHN + bh * N + q) * 4 + fq) * 2);
+      kb64[c] = (unsigned long long)w2.x | ((unsigned long long)w2.y << 32);
+    }
   }
   const int NK32 = (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite, P = 0)
   v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK32);
@@ -821,7 +854,8 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
       dp = v2_mma32(v2_fragj(Vs, LN, j, 1), df[1], dp);
       f32x4 keep = {1.f, 1.f, 1.f, 1.f};
       if (thr && kbits) {
-        const uint32_t b4 = (uint32_t)(kb64 >> (8 * (j >> 1) + 4 * (j & 1))) & 0xFu;
+        const unsigned long long kw = (KMAX > 256 && (j >> 4)) ? kb64[KMAX / 256 - 1] : kb64[0];
+        const uint32_t b4 = (uint32_t)(kw >> (8 * ((j & 15) >> 1) + 4 * (j & 1))) & 0xFu;
 #pragma unroll
         for (int r = 0; r < 4; ++r) keep[r] = (b4 >> r) & 1u ? dscale : 0.f;
       } else if (thr) {
@@ -856,13 +890,14 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dq_v2(const bf16_t* __restric
   }
   // q bias gradient (queries >= N hold dq = 0)
   if (dbias)
-    v2_colsum64<WAVES>(dq, scale, (float*)(smem + 2 * V2_KMAX * V2_ROWB),
+    v2_colsum64<WAVES>(dq, scale, (float*)(smem + 2 * KMAX * V2_ROWB),
                        dbias + (long)(b * gridDim.x + blockIdx.x) * 3 * D + h * 64);
 }
 
 // dK, dV: workgroup = (b, h, 16*WAVES keys); wave = 16 keys x all queries;
-// Q, dO images + lse, delta of all queries in LDS
-template <int WAVES>
+// Q, dO images + lse, delta of all queries in LDS (KMAX = 512: 157 KiB in
+// all); the workgroup's keys lie in one 256-key chunk of the keep bits
+template <int WAVES, int KMAX>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restrict__ qkv,
                                                          const bf16_t* __restrict__ dout,
                                                          const float* __restrict__ lse,
@@ -874,14 +909,15 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
   const unsigned long long seed = seed_;
   // keep bits transposed in LDS: KbT[word][query], pitch KBP words (a lane's 4
   // query rows of one word are one 16-byte read)
-  constexpr int KBP = V2_KMAX + 16;
-  constexpr int RED = 2 * V2_KMAX * V2_ROWB + 2 * V2_KMAX * 4 + 8 * KBP * 4;  // colsum scratch offset
+  constexpr int KBP = KMAX + 16;
+  constexpr int RED = 2 * KMAX * V2_ROWB + 2 * KMAX * 4 + 8 * KBP * 4;  // colsum scratch offset
+  static_assert(RED + 2 * WAVES * 64 * 4 <= 160 * 1024, "mhsa_dkv_v2: LDS");
   __shared__ __attribute__((aligned(16))) char smem[RED + 2 * WAVES * 64 * 4];
   char* Qs = smem;
-  char* Ds = smem + V2_KMAX * V2_ROWB;
-  float* Ls = (float*)(smem + 2 * V2_KMAX * V2_ROWB);
-  float* Dl = Ls + V2_KMAX;
-  uint32_t* Kb = (uint32_t*)(Dl + V2_KMAX);  // the forward's keep bits of this (b, h): KbT[fq*2 + half][query]
+  char* Ds = smem + KMAX * V2_ROWB;
+  float* Ls = (float*)(smem + 2 * KMAX * V2_ROWB);
+  float* Dl = Ls + KMAX;
+  uint32_t* Kb = (uint32_t*)(Dl + KMAX);  // the forward's keep bits of this (b, h): KbT[fq*2 + half][query]
   const int D = H * 64;
   const long pitch = 3L * D;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -908,16 +944,18 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
     Dl[i] = i < N ? delta[bh * N + i] : 0.f;
   }
   const bool use_kb = kbits && thr;
+  const int kchunk = (blockIdx.x * WAVES * 16) >> 8;  // the 256-key chunk of this workgroup's keys
   if (use_kb)
     for (int i = threadIdx.x; i < N * 2; i += WAVES * 64) {
-      const u32x4 v = ((const u32x4*)(kbits + bh * N * 8))[i];
+      const u32x4 v = ((const u32x4*)(kbits + ((uint64_t)kchunk * gridDim.z * H * N + bh * N) * 8))[i];
       const int q = i >> 1, w0 = 4 * (i & 1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) Kb[(w0 + e) * KBP + q] = v[e];
     }
-  // this lane's key inside a query's bit pair: word fq' * 2 + half, bit position
-  const int kbit = 8 * (key >> 5) + 4 * ((key >> 4) & 1) + (key & 3);
-  const int kword = ((key >> 2) & 3) * 2 + (kbit >> 5), kshift = kbit & 31;
+  // this lane's key inside a query's bit pair (chunk-relative key kl): word fq' * 2 + half, bit position
+  const int kl = key & 255;
+  const int kbit = 8 * (kl >> 5) + 4 * ((kl >> 4) & 1) + (kl & 3);
+  const int kword = ((kl >> 2) & 3) * 2 + (kbit >> 5), kshift = kbit & 31;
   __syncthreads();
   const float c2 = scale * 1.4426950408889634f;
   // accumulators: rows = d (16t + 4fq + r), column = this lane's key
@@ -1011,6 +1049,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
 }
 
 static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 && N <= V2_KMAX && N % 4 == 0; }
+static bool v2_big(int N) { return N > 256; }  // the KMAX = 512 instantiations
 // waves per v2 workgroup: 16 = all queries (keys) of a (b, h) in one
 // workgroup, K/V (Q/dO) staged once.  Measured: two 8-wave workgroups per
 // (b, h) are slower both at B*H = 256 (default, B=32) and at B*H = 192
@@ -1019,12 +1058,13 @@ static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 &&
 // and the bias-partial row count both use it, so an unsupported value (clamped
 // to 4, the template the launches fall back to) cannot size the rows apart
 // from the grid.
-static int v2_waves(int) {
+// (N > 256 takes the KMAX = 512 kernels, instantiated for 16 waves only)
+static int v2_waves(int N) {
   static const int w = [] {
     const int e = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
     return (e == 16 || e == 8) ? e : 4;
   }();
-  return w;
+  return v2_big(N) ? 16 : w;
 }
 
 // ------------------------------------------------------------------- host ---
@@ -1096,14 +1136,15 @@ static int mhsa_fwd_impl(int dt, const void* qkv, int B, int N, int H, int hd, f
     const hvit_dropout_t* dr = dropout;
     const uint32_t thr = dr ? drop_threshold(dr->p) : 0;
     const float ds = (dr && dr->p > 0.f) ? 1.f / (1.f - dr->p) : 1.f;
-    const int wv = v2_waves(B * H);
+    const int wv = v2_waves(N);
     auto go = [&](auto kern, int waves) {
       hipLaunchKernelGGL(kern, dim3(cdiv(N, 16 * waves), H, B), dim3(64 * waves), 0, st, (const bf16_t*)qkv,
                          (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dr), dr ? dr->site : 0u, keep_bits);
     };
-    if (wv == 16) go(mhsa_fwd_v2<16>, 16);
-    else if (wv == 8) go(mhsa_fwd_v2<8>, 8);
-    else go(mhsa_fwd_v2<4>, 4);
+    if (v2_big(N)) go(mhsa_fwd_v2<8, 512>, 8);
+    else if (wv == 16) go(mhsa_fwd_v2<16, 256>, 16);
+    else if (wv == 8) go(mhsa_fwd_v2<8, 256>, 8);
+    else go(mhsa_fwd_v2<4, 256>, 4);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
@@ -1113,7 +1154,7 @@ static int mhsa_fwd_impl(int dt, const void* qkv, int B, int N, int H, int hd, f
 // partial rows of the fused bias gradient per sample: one per v2 workgroup
 // along the token axis; one per sample otherwise
 static long long mhsa_bias_rows_per_sample(int dt, int hd, int N) {
-  return v2_ok(dt, hd, N) ? cdiv(N, 16 * v2_waves(0)) : 1;
+  return v2_ok(dt, hd, N) ? cdiv(N, 16 * v2_waves(N)) : 1;
 }
 
 static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N,
@@ -1138,10 +1179,11 @@ static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dou
       hipLaunchKernelGGL(dkvk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
                          (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits, dbias);
     };
-    const int wv = v2_waves(B * H);
-    if (wv == 16) go(mhsa_dq_v2<16>, mhsa_dkv_v2<16>, 16);
-    else if (wv == 8) go(mhsa_dq_v2<8>, mhsa_dkv_v2<8>, 8);
-    else go(mhsa_dq_v2<4>, mhsa_dkv_v2<4>, 4);
+    const int wv = v2_waves(N);
+    if (v2_big(N)) go(mhsa_dq_v2<16, 512>, mhsa_dkv_v2<16, 512>, 16);
+    else if (wv == 16) go(mhsa_dq_v2<16, 256>, mhsa_dkv_v2<16, 256>, 16);
+    else if (wv == 8) go(mhsa_dq_v2<8, 256>, mhsa_dkv_v2<8, 256>, 8);
+    else go(mhsa_dq_v2<4, 256>, mhsa_dkv_v2<4, 256>, 4);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
@@ -1166,11 +1208,11 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
 }
 
 // keep-bit variants: the forward stores its attention-dropout decisions (one
-// bit per (query, key), B*H*N*8 32-bit words for N <= 256) and the backward
-// reads them instead of re-hashing (bf16, head_dim 64, N <= 256, N % 4 == 0;
-// other shapes ignore keep_bits and regenerate the mask)
+// bit per (query, key): B*H*N*8 32-bit words per 256-key chunk, chunk-major)
+// and the backward reads them instead of re-hashing (bf16, head_dim 64,
+// N <= 512, N % 4 == 0; other shapes ignore keep_bits and regenerate the mask)
 extern "C" long long hvit_mhsa_keep_bits_elems(int B, int N, int H) {
-  return (B > 0 && N > 0 && H > 0) ? (long long)B * H * N * 8 : 0;
+  return (B > 0 && N > 0 && H > 0) ? (long long)B * H * N * 8 * cdiv(N, 256) : 0;
 }
 
 extern "C" int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float scale,

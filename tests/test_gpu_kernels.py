@@ -322,7 +322,8 @@ def attn_ref(qkv, B, N, H, hd, p=0.0, mask=None):
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("B,N,H,hd,p", [(2, 256, 8, 64, 0.0), (1, 240, 8, 64, 0.1), (2, 16, 4, 16, 0.0),
                                         (1, 4, 4, 16, 0.2), (3, 100, 2, 32, 0.0), (2, 300, 2, 64, 0.1),
-                                        (2, 228, 4, 64, 0.1)])  # 228: pipelined staging, odd tile count
+                                        (2, 228, 4, 64, 0.1),  # 228: pipelined staging, odd tile count
+                                        (2, 496, 8, 64, 0.1), (1, 512, 4, 64, 0.0)])  # N > 256: chunked softmax
 def test_mhsa_fwd_bwd(hv, dt, B, N, H, hd, p):
     l = L(hv)
     D = H * hd
@@ -363,13 +364,14 @@ def test_mhsa_fwd_bwd(hv, dt, B, N, H, hd, p):
         assert rel(g[:, i], r[:, i]) < (1e-4 if dt == "f32" else 4e-2), "qkv"[i]
 
 
-@pytest.mark.parametrize("B,N,H,p", [(2, 256, 8, 0.1), (3, 100, 2, 0.3), (1, 240, 4, 0.1), (2, 64, 8, 0.5)])
+@pytest.mark.parametrize("B,N,H,p", [(2, 256, 8, 0.1), (3, 100, 2, 0.3), (1, 240, 4, 0.1), (2, 64, 8, 0.5),
+                                     (2, 496, 8, 0.1), (1, 300, 2, 0.3)])
 def test_mhsa_keep_bits_equal_rehash(hv, B, N, H, p):
     """hvit_mhsa_fwd_kb / hvit_mhsa_bwd_kb (forward keeps one dropout bit per
     score, the backward reads them) give bit-identical o, lse and dqkv to the
     re-hashing entry points; the bits themselves match the numpy mirror of
-    the counter hash (word pair (b, h, q, fq): bit 8*jp + 4*e + r = key
-    32*jp + 16*e + 4*fq + r)."""
+    the counter hash (256-key chunk c, word pair (c, b, h, q, fq): bit 8*jp +
+    4*e + r = key 256*c + 32*jp + 16*e + 4*fq + r)."""
     l = L(hv)
     hd, D = 64, H * 64
     qkv = (torch.randn(B * N, 3 * D, device=DEV) * 0.7).to(torch.bfloat16)
@@ -397,11 +399,13 @@ def test_mhsa_keep_bits_equal_rehash(hv, B, N, H, p):
         assert torch.equal(a, b)
     # the stored bits against the hash mirror
     keep = keep_mask(99, 31, B * H * N * N, p).reshape(B * H, N, N)
-    w = kb.cpu().numpy().view(np.uint32).reshape(B * H, N, 4, 2)
+    w = kb.cpu().numpy().view(np.uint32).reshape(-1, B * H, N, 4, 2)
+    assert w.shape[0] == (N + 255) // 256
     for key in range(N):
-        jp, e, fq, r = key >> 5, (key >> 4) & 1, (key >> 2) & 3, key & 3
+        c, kl = key >> 8, key & 255
+        jp, e, fq, r = kl >> 5, (kl >> 4) & 1, (kl >> 2) & 3, kl & 3
         bit = 8 * jp + 4 * e + r
-        got = (w[:, :, fq, bit >> 5] >> np.uint32(bit & 31)) & np.uint32(1)
+        got = (w[c, :, :, fq, bit >> 5] >> np.uint32(bit & 31)) & np.uint32(1)
         assert np.array_equal(got.astype(bool), keep[:, :, key]), key
 
 
@@ -437,13 +441,15 @@ def test_mhsa_v2_deterministic(hv, N):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,N,H,p,kb", [(4, 256, 8, 0.1, True), (3, 100, 2, 0.0, False), (2, 300, 2, 0.1, False)])
+@pytest.mark.parametrize("B,N,H,p,kb", [(4, 256, 8, 0.1, True), (3, 100, 2, 0.0, False), (2, 300, 2, 0.1, False),
+                                        (2, 496, 8, 0.1, True), (2, 520, 2, 0.1, False)])
 def test_mhsa_bwd_fused_qkv_bias(hv, B, N, H, p, kb):
     """hvit_mhsa_bwd_db: dqkv bit-identical to hvit_mhsa_bwd(_kb), and the sum of
     its partial bias rows equal to the f32 column sums of dqkv over the B*N
     tokens (the qkv bias gradient).  The kernel sums the unrounded f32 gradients, the
     check sums the bf16-rounded dqkv: bar = bf16 half-ulp of the column's
-    absolute sum (N=300 takes the flash-style kernels + column reduction)."""
+    absolute sum (N = 300 / 496: the chunked register-resident kernels; N = 520 the
+    flash-style kernels + per-sample segmented column sums)."""
     l = L(hv)
     hd, D = 64, H * 64
     qkv = (torch.randn(B * N, 3 * D, device=DEV) * 0.7).to(torch.bfloat16)

@@ -23,6 +23,9 @@ from oracle import closed_form as CF  # noqa: E402
 from oracle import hvit_oracle as O  # noqa: E402
 
 REF = {"fwd": 1.82, "step": 5.79}  # BASELINE.md §2 (reference, survey container, 8 threads)
+# the reference's B=32 eval-forward time by aten op (share of CPU time)
+REF_SHARES = {"aten::mkldnn_convolution": 38.0, "aten::addmm": 20.0, "aten::copy_": 11.0,
+              "aten::max_pool2d_with_indices": 10.0, "aten::bmm": 5.0, "aten::native_batch_norm": 4.0}
 
 
 def lscpu():
@@ -70,6 +73,16 @@ def main():
 
     f, fs = best3(fwd)
     s, ss = best3(step)
+    # the oracle's own op mix on the same forward (torch.profiler self CPU time):
+    # the same aten ops in the same shares as the reference's profile means the
+    # restatement does the reference's work, and a time ratio is the host's
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        fwd()
+    ka = {e.key: e.self_cpu_time_total for e in prof.key_averages()}
+    tot = sum(ka.values())
+    share_lines = ["", "forward self-CPU share by aten op: oracle (this host) vs reference (SURVEY §6)"]
+    for k, ref in REF_SHARES.items():
+        share_lines.append(f"  {k:34s} {100.0 * ka.get(k, 0.0) / tot:5.1f} %   reference {ref:4.1f} %")
     lines = [
         f"host: {platform.node()}  torch {torch.__version__}  threads {torch.get_num_threads()} "
         f"(affinity cores {cores})",
@@ -82,11 +95,12 @@ def main():
         f"  train step   : {s:6.2f} s  (runs {', '.join(f'{v:.2f}' for v in ss)})  reference 5.79 s  "
         f"ratio {s / REF['step']:.3f}",
         f"  frames/s (train): {32 * 256 / s:8.1f}   reference {32 * 256 / REF['step']:8.1f}",
-    ]
+    ] + share_lines
     out = "\n".join(lines)
     print(out)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "r3_cpu_baseline_check.txt"), "w") as fh:
+    with open(os.path.join(ROOT, "profiles", sys.argv[1] if len(sys.argv) > 1 else "cpu_baseline_check.txt"),
+              "w") as fh:
         fh.write(out + "\n")
 
 
