@@ -233,6 +233,10 @@ int hvit_mhsa_bwd_db(int dt, const void* qkv, const void* o, const void* dout, c
  * its backward. */
 int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
                       void* o, float* lse, void* stream);
+/* The same storing its dropout decisions in hvit_mhsa_fwd_kb's keep-bit layout
+ * (keep_bits nullable; N % 4 == 0), for hvit_mhsa_bwd_kb / _bwd_db. */
+int hvit_mhsa_fwd_fp8_kb(const void* qkv, int B, int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
+                         void* o, float* lse, unsigned* keep_bits, void* stream);
 
 /* ---- LayerNorm eps (attention.py:152-153, :271): x f32 [M, D] -> y; saves
  * mean / rstd [M].  Backward: dx = resid + dLN (resid may be NULL or alias dx),

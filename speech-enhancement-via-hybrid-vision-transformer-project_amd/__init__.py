@@ -6,7 +6,8 @@ plus the factory it forgot to export):
     HybridViT, create_hybrid_vit, ConvBlock, TransposeConvBlock, FeedForward,
     PatchEmbedding, PositionalEncoding, MultiHeadSelfAttention,
     TransformerEncoderBlock, VisionTransformer, CombinedLoss, create_loss_function,
-    FusedAdamW / clip_grad_norm_ / create_optimizer (training/optimizer.py, trainer.py:170-174)
+    FusedAdamW / clip_grad_norm_ / create_optimizer (training/optimizer.py, trainer.py:170-174),
+    GraphedTrainStep (the train step replayed from a hipGraph per input shape, trainer.py:142-183)
 """
 
 from .hybrid_vit import (  # noqa: F401
@@ -24,10 +25,11 @@ from .hybrid_vit import (  # noqa: F401
 )
 from .losses import CombinedLoss, create_loss_function  # noqa: F401
 from .optim import FusedAdamW, clip_grad_norm_, create_optimizer  # noqa: F401
+from .train_step import GraphedTrainStep  # noqa: F401
 from . import _lib  # noqa: F401
 
 __all__ = [
     "HybridViT", "create_hybrid_vit", "ConvBlock", "TransposeConvBlock", "FeedForward", "PatchEmbedding",
     "PositionalEncoding", "MultiHeadSelfAttention", "TransformerEncoderBlock", "VisionTransformer",
-    "CombinedLoss", "create_loss_function", "FusedAdamW", "clip_grad_norm_", "create_optimizer",
+    "CombinedLoss", "create_loss_function", "FusedAdamW", "clip_grad_norm_", "create_optimizer", "GraphedTrainStep",
 ]

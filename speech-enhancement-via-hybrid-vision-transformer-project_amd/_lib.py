@@ -98,6 +98,7 @@ _SIGS = {
     "hvit_bn_fold": ([vp, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp], i32),
     "hvit_mhsa_fwd": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_fwd_fp8": ([vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
+    "hvit_mhsa_fwd_fp8_kb": ([vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_mhsa_keep_bits_elems": ([i32, i32, i32], i64),
     "hvit_mhsa_fwd_kb": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),

@@ -19,7 +19,9 @@
 //                      (E8M0 exponents).
 // The dropout mask is the bf16 kernel's (same hash, same indices), so the
 // backward -- bf16, recomputing P from the saved lse (FlashAttention-3's fp8
-// recipe: fp8 forward, bf16 backward) -- sees the forward's mask.
+// recipe: fp8 forward, bf16 backward) -- sees the forward's mask; with
+// keep_bits the forward also stores the mask in the bf16 kernel's keep-bit
+// layout, so that backward reads it instead of re-hashing.
 #include "common.h"
 
 namespace hvit {
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
                                                                   bf16_t* __restrict__ o, float* __restrict__ lse,
                                                                   int N, int H, float scale, uint32_t thr,
                                                                   float dscale, DSeed seed_,
-                                                                  uint32_t site) {
+                                                                  uint32_t site, uint32_t* __restrict__ kbits) {
   const unsigned long long seed = seed_;
   constexpr int NT = WAVES * 64;
   constexpr int PER = F8_KMAX * 8 / NT;  // 16-byte chunks of K (and of V) per thread
@@ -190,6 +192,9 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
 #pragma unroll
   for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int qq = q < N ? q : 0;
+  // keep bits (mhsa_fwd_v2's layout, one 256-key chunk): bit 4j + r of this
+  // lane's 64-bit word = keep(q, key 16j + 4fq + r)
+  unsigned long long kw = 0ull;
 #pragma unroll
   for (int kb = 0; kb < F8_KMAX / 128; ++kb) {
     if (128 * kb < N) {
@@ -200,7 +205,13 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
         f32x4 p = (j < nkt) ? st[j] * 256.f : (f32x4){0.f, 0.f, 0.f, 0.f};
         // 0/1 keep mask only: 256 P stays <= 256 < 448 (e4m3 max) for any p;
         // the 1/(1-p) scale is folded into the output's 1/sum below
-        if (thr && j < nkt) p *= keep4q(bh, N, qq, 16 * j + 4 * fq, thr, 1.f, seed, site);
+        if (thr && j < nkt) {
+          const f32x4 k4 = keep4q(bh, N, qq, 16 * j + 4 * fq, thr, 1.f, seed, site);
+          p *= k4;
+          kw |= (unsigned long long)((k4[0] > 0.f ? 1u : 0u) | (k4[1] > 0.f ? 2u : 0u) | (k4[2] > 0.f ? 4u : 0u) |
+                                     (k4[3] > 0.f ? 8u : 0u))
+                << (4 * j);
+        }
         pb[m] = (int)f8x4(p[0], p[1], p[2], p[3]);
       }
 #pragma unroll
@@ -225,6 +236,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
       *(uint2*)(op + 16 * t + 4 * fq) = u;
     }
     if (fq == 0) lse[bh * N + q] = (mx + log2f(sum)) * 0.6931471805599453f;
+    if (kbits && thr) *(uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2) = make_uint2((uint32_t)kw, (uint32_t)(kw >> 32));
   }
 }
 
@@ -233,13 +245,16 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
 
 using namespace hvit;
 
-extern "C" int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, float scale,
-                                 const hvit_dropout_t* dropout, void* o, float* lse, void* stream) {
+extern "C" int hvit_mhsa_fwd_fp8_kb(const void* qkv, int B, int N, int H, int hd, float scale,
+                                    const hvit_dropout_t* dropout, void* o, float* lse, unsigned* keep_bits,
+                                    void* stream) {
   HVIT_CHECK(qkv && o && lse, "hvit_mhsa_fwd_fp8: null pointer");
   HVIT_CHECK(B > 0 && N > 0 && H > 0, "hvit_mhsa_fwd_fp8: bad shape B=%d N=%d H=%d", B, N, H);
   HVIT_CHECK(hd == 64, "hvit_mhsa_fwd_fp8: head_dim %d unsupported (64)", hd);
   HVIT_CHECK(N <= F8_KMAX, "hvit_mhsa_fwd_fp8: N=%d exceeds %d tokens", N, F8_KMAX);
   HVIT_CHECK(aligned16(qkv) && aligned16(o), "hvit_mhsa_fwd_fp8: qkv/o must be 16-byte aligned");
+  HVIT_CHECK(!keep_bits || (((uintptr_t)keep_bits & 15) == 0 && N % 4 == 0),
+             "hvit_mhsa_fwd_fp8: keep_bits alignment / N %% 4 (the bf16 backward's keep-bit layout)");
   // P is held as 256 * P * keep (0/1) in e4m3 (max 448), 1/(1-p) applied with
   // the normaliser: no saturation for any dropout p
   const uint32_t thr = dropout ? drop_threshold(dropout->p) : 0;
@@ -249,7 +264,12 @@ extern "C" int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, f
   constexpr int WAVES = 16;
   hipLaunchKernelGGL(mhsa_fwd_fp8_kernel<WAVES>, dim3(cdiv(N, 16 * WAVES), H, B), dim3(64 * WAVES), 0,
                      (hipStream_t)stream, (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds,
-                     dseed(dropout), dropout ? dropout->site : 0u);
+                     dseed(dropout), dropout ? dropout->site : 0u, keep_bits);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
+}
+
+extern "C" int hvit_mhsa_fwd_fp8(const void* qkv, int B, int N, int H, int hd, float scale,
+                                 const hvit_dropout_t* dropout, void* o, float* lse, void* stream) {
+  return hvit_mhsa_fwd_fp8_kb(qkv, B, N, H, hd, scale, dropout, o, lse, nullptr, stream);
 }

@@ -1020,12 +1020,15 @@ class ViTBlockFn(torch.autograd.Function):
         probs = torch.empty((B, H, Nt, Nt), dtype=torch.float32, device=dev) if want_probs else None
         if attn_fp8 and not want_probs:
             # fp8 (e4m3) QK^T / PV forward (BASELINE config 5); the backward
-            # below is the bf16 kernel, recomputing P from this lse
+            # below is the bf16 kernel, recomputing P from this lse and reading
+            # the dropout decisions the fp8 forward kept (same keep-bit layout)
             if dt != BF16:
                 raise ValueError("hvit: the fp8 attention path runs inside the bf16 model (precision='bf16')")
+            if d_attn.p > 0 and KEEPBITS and Nt % 4 == 0:
+                kbits = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, Nt, H), dtype=torch.int32, device=dev)
             with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
-                call("hvit_mhsa_fwd_fp8", qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
-                     lse.data_ptr(), s)
+                call("hvit_mhsa_fwd_fp8_kb", qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
+                     lse.data_ptr(), ptr(kbits), s)
         elif probs is None and d_attn.p > 0 and KEEPBITS:
             # the dropout decisions are kept (1 bit per score) so the backward does not re-hash them
             kbits = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, Nt, H), dtype=torch.int32, device=dev)

@@ -1,0 +1,115 @@
+"""A whole training step captured in a hipGraph per input shape (SURVEY §8(f)
+rank 3: variable-length batches).
+
+The reference trainer steps through batches whose time axis varies from batch
+to batch: ``collate_fn`` right-pads T to the batch maximum
+(data/dataset.py:297-347), so a VoiceBank epoch sees many [B, 1, 257, T]
+shapes, and ``Trainer.train_epoch`` runs forward, loss, backward, clip and the
+optimizer on each (training/trainer.py:142-183).  Replaying one captured graph
+needs one static shape, so ``GraphedTrainStep`` keeps one graph per input
+shape (LRU-capped):
+
+* the first ``warmup`` steps of a new shape run eagerly (they are real steps:
+  they allocate the step's memory, build the bf16 weight shadows and optimizer
+  state, and agree the data-parallel token bound); the next step of that shape
+  is captured -- capture executes nothing -- and replayed, and every later
+  step of that shape is a replay: the batch is copied into the graph's static
+  input buffers first;
+* every replay is a full, distinct step: the model draws its dropout seeds
+  from a device-side counter and FusedAdamW(capturable=True) keeps its step
+  counters on the device, so a replayed step equals the eager step it stands
+  for (the train step is deterministic: bit for bit, tests/test_gpu_graph_cache.py);
+* each graph has its own memory pool; evicting the least recently used graph
+  (``max_graphs``) frees its pool.
+
+``step(noisy, clean)`` returns the loss as a device tensor (the graph's static
+output for replays: read it before the next call with the same shape).
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Callable, Optional
+
+import torch
+
+
+class _Entry:
+    __slots__ = ("seen", "graph", "x", "t", "loss")
+
+    def __init__(self):
+        self.seen = 0
+        self.graph = None
+        self.x = self.t = self.loss = None
+
+
+class GraphedTrainStep:
+    """forward + ``loss_fn`` + backward [+ ``reducer.finish()``] +
+    ``optimizer.step()`` + ``zero_grad(set_to_none=True)``, replayed from a
+    per-shape hipGraph after ``warmup`` eager steps of that shape."""
+
+    def __init__(self, model: torch.nn.Module, loss_fn: Callable, optimizer, reducer=None, max_graphs: int = 8,
+                 warmup: int = 2):
+        if getattr(optimizer, "capturable", True) is False:
+            raise ValueError("hvit GraphedTrainStep: the optimizer must keep its step counters on the device "
+                             "(FusedAdamW(..., capturable=True))")
+        if max_graphs < 1 or warmup < 1:
+            raise ValueError("hvit GraphedTrainStep: max_graphs and warmup must be >= 1")
+        self.model, self.loss_fn, self.opt, self.reducer = model, loss_fn, optimizer, reducer
+        self.max_graphs, self.warmup = max_graphs, warmup
+        self.cache: "OrderedDict[tuple, _Entry]" = OrderedDict()
+        self.captures = 0
+        self.replays = 0
+        self._side: Optional[torch.cuda.Stream] = None
+
+    def _eager(self, x, t):
+        loss = self.loss_fn(self.model(x), t)
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        return loss
+
+    @staticmethod
+    def _key(x, t):
+        return (tuple(x.shape), x.dtype, tuple(t.shape), t.dtype, x.device)
+
+    def __call__(self, noisy: torch.Tensor, clean: torch.Tensor) -> torch.Tensor:
+        key = self._key(noisy, clean)
+        e = self.cache.get(key)
+        if e is None:
+            e = self.cache[key] = _Entry()
+            while len(self.cache) > self.max_graphs:
+                self.cache.popitem(last=False)  # the graph and its pool go with the entry
+        self.cache.move_to_end(key)
+        if e.graph is not None:
+            e.x.copy_(noisy)
+            e.t.copy_(clean)
+            e.graph.replay()
+            self.replays += 1
+            return e.loss
+        if e.seen < self.warmup:
+            # eager steps of a new shape (on a side stream, as capture warm-ups must be,
+            # so the allocations they leave are not tied to the capture stream)
+            e.seen += 1
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=noisy.device)
+            side = self._side
+            side.wait_stream(torch.cuda.current_stream(noisy.device))
+            with torch.cuda.stream(side):
+                loss = self._eager(noisy, clean)
+            torch.cuda.current_stream(noisy.device).wait_stream(side)
+            return loss
+        # capture (executes nothing), then replay it as this call's step
+        e.x = noisy.detach().clone()
+        e.t = clean.detach().clone()
+        torch.cuda.synchronize(noisy.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            e.loss = self._eager(e.x, e.t)
+        e.graph = g
+        self.captures += 1
+        g.replay()
+        self.replays += 1
+        return e.loss

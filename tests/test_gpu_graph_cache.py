@@ -1,0 +1,49 @@
+"""GPU: variable-length batches through the per-shape graph cache
+(…_amd/train_step.py; data/dataset.py:297-347 pads T per
+batch).  A bf16 HybridViT with dropout trained through GraphedTrainStep on a
+sequence of batches of three different T (with an LRU cap of two graphs, so a
+shape's graph is evicted and captured again) equals, bit for bit after every
+step, an identical copy trained eagerly from the same dropout seed state."""
+
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+KW = dict(encoder_channels=[8, 16, 32], embed_dim=128, num_heads=2, num_layers=2, decoder_channels=[32, 16, 8, 1],
+          precision="bf16")
+
+
+def test_graph_cache_variable_length_matches_eager(hv):
+    import importlib
+
+    ts = importlib.import_module("hvit_amd.train_step")
+    torch.manual_seed(0)
+    ma = hv.HybridViT(**KW).to(DEV).train()
+    mb = copy.deepcopy(ma)
+    oa = hv.FusedAdamW(ma.parameters(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, capturable=True)
+    ob = hv.FusedAdamW(mb.parameters(), lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, capturable=True)
+    crit = hv.CombinedLoss()
+    step = ts.GraphedTrainStep(ma, crit, oa, max_graphs=2, warmup=1)
+    ma.set_dropout_state(31337)
+    mb.set_dropout_state(31337)
+    g = torch.Generator().manual_seed(3)
+    Ts = [64, 64, 64, 48, 48, 48, 64, 80, 80, 80, 64, 64, 48, 48]
+    for i, T in enumerate(Ts):
+        x = torch.rand(2, 1, 48, T, generator=g).to(DEV)
+        t = torch.rand(2, 1, 48, T, generator=g).to(DEV)
+        la = step(x, t)
+        lb = crit(mb(x), t)
+        lb.backward()
+        ob.step()
+        ob.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        assert la.item() == lb.item(), (i, T, la.item(), lb.item())
+        for (k, pa), pb in zip(ma.named_parameters(), mb.parameters()):
+            assert torch.equal(pa.detach(), pb.detach()), (i, T, k)
+    assert step.captures >= 4  # 64, 48, 80, and 64 again after its eviction (cap 2)
+    assert step.replays >= 6
+    assert len(step.cache) <= 2
+    assert torch.equal(ma.dropout_state(), mb.dropout_state())

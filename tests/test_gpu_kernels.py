@@ -817,6 +817,83 @@ def test_mhsa_fwd_fp8_dropout_matches_bf16_mask(hv, p):
     assert ((got - emu).norm() / emu.norm()).item() < 8e-3
 
 
+@pytest.mark.parametrize("N,p", [(256, 0.1), (100, 0.3)])
+def test_mhsa_fwd_fp8_keep_bits(hv, N, p):
+    """hvit_mhsa_fwd_fp8_kb: the same o / lse as hvit_mhsa_fwd_fp8 and keep bits
+    equal to the bf16 forward's (hvit_mhsa_fwd_kb) bit for bit, so the bf16
+    backward reading them equals the one re-hashing the mask."""
+    l = L(hv)
+    torch.manual_seed(N)
+    B, H, hd = 2, 12, 64
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device=DEV).to(torch.bfloat16)
+    dr = l.dropout(p, 4321, 11)
+    nkb = l.lib().hvit_mhsa_keep_bits_elems(B, N, H)
+    o8, o8k, ob = (torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    lse8, lse8k, lseb = (torch.empty(B, H, N, device=DEV) for _ in range(3))
+    kb8, kbb = (torch.full((nkb,), -1, dtype=torch.int32, device=DEV) for _ in range(2))
+    l.call("hvit_mhsa_fwd_fp8", qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o8.data_ptr(), lse8.data_ptr(), s())
+    l.call("hvit_mhsa_fwd_fp8_kb", qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o8k.data_ptr(), lse8k.data_ptr(),
+           kb8.data_ptr(), s())
+    l.call("hvit_mhsa_fwd_kb", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, ob.data_ptr(), lseb.data_ptr(),
+           kbb.data_ptr(), s())
+    torch.cuda.synchronize()
+    assert torch.equal(o8, o8k) and torch.equal(lse8, lse8k)
+    assert torch.equal(kb8, kbb)
+    go = torch.randn(B * N, D, device=DEV).to(torch.bfloat16)
+    outs = []
+    for bits in (kb8, None):
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B, H, N, device=DEV)
+        l.call("hvit_mhsa_bwd_kb", l.BF16, qkv.data_ptr(), o8.data_ptr(), go.data_ptr(), lse8.data_ptr(), B, N, H, hd,
+               hd ** -0.5, dr, bits.data_ptr() if bits is not None else None, dqkv.data_ptr(), delta.data_ptr(), s())
+        outs.append(dqkv)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_mhsa_fp8_forward_gradient_bound(hv):
+    """The fp8 path's gradient (e4m3 forward, bf16 backward recomputing P from
+    the fp8 forward's lse -- whose recomputed rows need not sum to exactly 1)
+    against exact fp32 attention, next to the bf16 path's own error on the same
+    inputs (config-5 head shape, unit-variance q, k, v, dropout 0.1).  Bar:
+    within 3x the bf16 path's max-relative error and below 0.1 (measured values
+    printed)."""
+    l = L(hv)
+    torch.manual_seed(21)
+    B, N, H, hd, p = 2, 256, 12, 64, 0.1
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device=DEV).to(torch.bfloat16)
+    dr = l.dropout(p, 99, 7)
+    mask = torch.as_tensor(keep_mask(99, 7, B * H * N * N, p).reshape(B, H, N, N), device=DEV).float()
+    xr = qkv.float().requires_grad_(True)
+    o_ref, _ = attn_ref(xr, B, N, H, hd, p, mask)
+    go = torch.randn_like(o_ref)
+    o_ref.backward(go)
+    ref = xr.grad
+    gq = go.to(torch.bfloat16).contiguous()
+    nkb = l.lib().hvit_mhsa_keep_bits_elems(B, N, H)
+    errs = {}
+    for name in ("bf16", "fp8"):
+        o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, N, device=DEV)
+        kb = torch.empty(nkb, dtype=torch.int32, device=DEV)
+        if name == "fp8":
+            l.call("hvit_mhsa_fwd_fp8_kb", qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+                   kb.data_ptr(), s())
+        else:
+            l.call("hvit_mhsa_fwd_kb", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(),
+                   lse.data_ptr(), kb.data_ptr(), s())
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B, H, N, device=DEV)
+        l.call("hvit_mhsa_bwd_kb", l.BF16, qkv.data_ptr(), o.data_ptr(), gq.data_ptr(), lse.data_ptr(), B, N, H, hd,
+               hd ** -0.5, dr, kb.data_ptr(), dqkv.data_ptr(), delta.data_ptr(), s())
+        errs[name] = rel(dqkv.float(), ref)
+    print(f"dqkv max-rel vs fp32: bf16 path {errs['bf16']:.3e}, fp8 path {errs['fp8']:.3e}")
+    assert errs["fp8"] < 0.1
+    assert errs["fp8"] < 3.0 * errs["bf16"]
+
+
 def test_pos_dropout_matches_fused_patch_embed(hv):
     """PosDropFn (forward_transformer's entry and the CLS-token layout) applies
     the same pos-embed add and counter-hash dropout mask (site 200) as the
