@@ -37,7 +37,9 @@ enum {
   HVIT_ACT_GELU_DUAL_D = 4, /* GELU_DUAL that stores gelu'(v) instead of v (for MUL_AUX) */
   HVIT_ACT_MUL_AUX = 5,     /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
   HVIT_ACT_RELU = 6,        /* conv forward only: v = max(v + bias, 0) (eval-mode BatchNorm folded) */
-  HVIT_ACT_GELU = 7         /* linear forward: y = dropout(gelu(v)) only (fc1 when no backward runs) */
+  HVIT_ACT_GELU = 7,        /* linear forward: y = dropout(gelu(v)) only (fc1 when no backward runs) */
+  HVIT_ACT_RELU_POOL2 = 8   /* conv forward only (bf16, even Ho / Wo, 64-channel-multiple sources): relu(v + bias)
+                               then 2x2 max-pool, y = [N, Ho/2, Wo/2, Cout] (eval BatchNorm folded, pooled block) */
 };
 /* flags of the backward calls that accumulate into caller memory:
  * HVIT_ACC_ZEROED says the caller already zeroed the accumulator outputs (one

@@ -215,8 +215,28 @@ struct LdConvF {
   int KS, S, Pd;
   int Ho, Wo, P, Kt;
   unsigned bytes1, bytes2;     // buffer extents
+  int pool2 = 0;               // row order: 0 pixel-major (n, oy, ox); 1 pooling windows (n, oy/2, ox/2, 2x2 position)
 
   __device__ __forceinline__ bool fast() const { return true; }
+  // output pixel of GEMM row p.  pool2: rows 4w .. 4w+3 are the 2x2 window w of the
+  // pooled image (window-major, NHWC order of the pooled output), so a 2x2 max-pool
+  // is a max over 4 consecutive rows in the epilogue
+  __device__ __forceinline__ void pix(int p, int& n, int& oy, int& ox) const {
+    if (pool2) {
+      const int q = p & 3, w = p >> 2, hw = (Ho >> 1) * (Wo >> 1);
+      n = w / hw;
+      const int rem = w - n * hw;
+      const int wy = rem / (Wo >> 1), wx = rem - wy * (Wo >> 1);
+      oy = 2 * wy + (q >> 1);
+      ox = 2 * wx + (q & 1);
+    } else {
+      const int hw = Ho * Wo;
+      n = p / hw;
+      const int rem = p - n * hw;
+      oy = rem / Wo;
+      ox = rem - oy * Wo;
+    }
+  }
   struct Sh {
     int c0, kx, ky;  // stage tap (uniform)
     int klane;       // this thread's channel offset inside the stage
@@ -225,9 +245,8 @@ struct LdConvF {
     int rb, iy0, ix0;  // n*Hs (source row base), oy*S - Pd, ox*S - Pd
   };
   __device__ __forceinline__ void init(Sh& sh, Cur& cu, int a, int b) const {
-    const int hw = Ho * Wo;
-    const int n = a / hw, rem = a - n * hw;
-    const int oy = rem / Wo, ox = rem - oy * Wo;
+    int n, oy, ox;
+    pix(a, n, oy, ox);
     cu.rb = n * Hs;
     cu.iy0 = oy * S - Pd;
     cu.ix0 = ox * S - Pd;
@@ -356,6 +375,7 @@ struct Epi {
   const void* aux = nullptr;  // GELU_BWD: pre-activation h[m][n] (gd: gelu'(h) itself)
   int gd = 0;  // GELU_DUAL: out receives gelu'(h) instead of h; GELU_BWD: aux already is gelu'(h)
   int relu = 0;  // v = max(v, 0) after bias (the eval-mode folded BatchNorm + ReLU of the conv blocks)
+  int pool2 = 0;  // EK_STORE of a pooled conv (LdConvF::pool2 row order): 2x2 max of each 4-row window, row m/4
   int aux_dt = HVIT_F32;
   long ldaux = 0;
   uint32_t drop_thr = 0;  // dropout keep test (0 = off)
@@ -975,12 +995,11 @@ struct GemmCoreDma {
       ra = __builtin_amdgcn_make_buffer_rsrc((void*)la.src1, (short)0, (int)la.bytes1, 0x00020000);
       ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)la.src2, (short)0, (int)la.bytes2, 0x00020000);
       cl8 = ((lane & 7) ^ ((lane >> 3) & 7)) << 3;
-      const int hw = la.Ho * la.Wo;
 #pragma unroll
       for (int i = 0; i < PA; ++i) {
         const int p = m0 + (wid + 4 * i) * IA::RPP + (lane >> 3);
-        const int n = p / hw, rem = p - n * hw;
-        const int oy = rem / la.Wo, ox = rem - oy * la.Wo;
+        int n, oy, ox;
+        la.pix(p, n, oy, ox);
         crb[i] = n * la.Hs;
         ciy[i] = oy * la.S - la.Pd;
         cix[i] = ox * la.S - la.Pd;
@@ -1499,6 +1518,31 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
         }
       } else if constexpr (EK == EK_STORE) {
         // host guarantees N % 4 == 0, ldo % 4 == 0 and an aligned output
+        if (ep.pool2) {
+          // pooled conv (eval BatchNorm folded, ReLU): window w = rows 4w .. 4w+3 of
+          // this half (LdConvF::pool2 order); relu(max + bias) = max of relu(v + bias)
+          // (uniform branch; host: bf16 output, every window inside the tile)
+#pragma unroll
+          for (int i = 0; i < (16 + RSTEP - 1) / RSTEP; ++i) {
+            const int wi = r0 + i * RSTEP;
+            if (wi >= 16 || 4 * wi >= rows_here || !nok) continue;
+            f32x4 v = *(const f32x4*)(Cs + (4 * wi) * CP + c4 * 4);
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+              const f32x4 u = *(const f32x4*)(Cs + (4 * wi + q) * CP + c4 * 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], u[e]);
+            }
+            v += bias4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            uint2 u;
+            u.x = f2bf2(v[0], v[1]);
+            u.y = f2bf2(v[2], v[3]);
+            *(uint2*)((bf16_t*)ep.out + (long)((mbase >> 2) + wi) * ep.ldo + n) = u;
+          }
+          return;
+        }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
           const int row = r0 + i * RSTEP;

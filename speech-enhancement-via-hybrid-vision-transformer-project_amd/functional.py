@@ -640,9 +640,12 @@ class ConvBNActFn(torch.autograd.Function):
         P = N * H * W
         es = 4 if dt == F32 else 2
         cflops = 2.0 * P * Cout * Cin * KS * KS
-        if nograd and not training and pool == 1 and EVALFOLD:
+        pooled = (pool == 2 and dt == BF16 and C1 % 64 == 0 and C2 % 64 == 0 and H % 2 == 0 and W % 2 == 0
+                  and Cout % 4 == 0)
+        if nograd and not training and (pool == 1 or pooled) and EVALFOLD:
             # eval, no backward (the caller ran outside grad mode): BatchNorm folded into the conv weights and bias, ReLU
-            # in the conv epilogue (Dropout2d is the identity): z is never stored
+            # in the conv epilogue (Dropout2d is the identity): z is never stored.  A pooling block (enc1) walks
+            # its output pixels window by window and keeps each 2x2 window's maximum in the epilogue.
             call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
                  invstd.data_ptr(), s)
             wf = _empty((w.numel(),), dt, dev)
@@ -650,10 +653,10 @@ class ConvBNActFn(torch.autograd.Function):
             call("hvit_bn_fold", w.detach().contiguous().data_ptr(), Cout, Cin, KS, mean.data_ptr(),
                  invstd.data_ptr(), gamma.detach().contiguous().data_ptr(), beta.detach().contiguous().data_ptr(),
                  wf.data_ptr(), dt, bias.data_ptr(), s)
-            y = _empty((N, H, W, Cout), dt, dev)
+            y = _empty((N, H // pool, W // pool, Cout), dt, dev)
             with timed("conv_fwd", cflops):
                 call("hvit_conv_fwd", dt, g, wf.data_ptr(), bias.data_ptr(), y.data_ptr(), dt, None,
-                     epilogue(act=L.ACT_RELU), s)
+                     epilogue(act=L.ACT_RELU_POOL2 if pool == 2 else L.ACT_RELU), s)
             return y
         wp = pack_conv(w, 0, dt)
         z = _empty((N, H, W, Cout), dt, dev)

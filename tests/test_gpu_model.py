@@ -132,6 +132,23 @@ def test_bf16_path(hv, name, kw):
     assert abs(gq.double().norm().item() - float(g[f"gnorm.{qk}"])) < 0.1 * float(g[f"gnorm.{qk}"])
 
 
+def test_inference_fusions_match_training_graph_path(hv):
+    """Inference (eval + no_grad, BASELINE config 2) takes the fused forms: eval
+    BatchNorm folded into every conv block (the pooling encoder block keeping
+    each 2x2 window's maximum in the conv epilogue, z never stored) and fc1
+    storing gelu(h) only.  Same model, same input with grad enabled (the
+    unfused eval path that keeps z and gelu'(h) for a backward): equal within
+    bf16 rounding of the folded weights."""
+    m = build(hv, {}, "bf16", False).eval()
+    g = golden("default_256")
+    x = torch.as_tensor(g["x"]).cuda()
+    with torch.no_grad():
+        y_fused = m(x)
+    y_plain = m(x).detach()
+    assert relnorm(y_fused.cpu(), y_plain.cpu()) < 1e-2
+    assert rel(y_fused.cpu(), y_plain.cpu()) < 3e-2
+
+
 def test_autocast_selects_bf16(hv):
     m = build(hv, O.TINY, "auto", False).eval()
     x = torch.as_tensor(CF.spectrogram((2, 1, 64, 64), 5)).cuda()
