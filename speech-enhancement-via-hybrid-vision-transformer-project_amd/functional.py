@@ -415,6 +415,7 @@ def linear_wgrad_now(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None, side
 SIDE = os.environ.get("HVIT_SIDE", "1") != "0"  # A/B knob: 0 = every launch on the backward's stream
 _SIDE_STREAMS = {}
 _SIDE_OPEN = set()
+_SIDE_TASKS = set()  # autograd graph tasks that have the join queued
 
 
 def _dev_index(dev) -> int:
@@ -438,6 +439,7 @@ def _join_side():
     for i in list(_SIDE_OPEN):
         torch.cuda.current_stream(i).wait_stream(_SIDE_STREAMS[i])
     _SIDE_OPEN.clear()
+    _SIDE_TASKS.clear()
 
 
 class on_side:
@@ -455,8 +457,10 @@ class on_side:
         i = _dev_index(self.dev)
         s = side_stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(i))
-        if i not in _SIDE_OPEN:
-            _SIDE_OPEN.add(i)
+        _SIDE_OPEN.add(i)
+        task = torch._C._current_graph_task_id()
+        if task not in _SIDE_TASKS:  # once per backward (also after one that raised before its join)
+            _SIDE_TASKS.add(task)
             torch.autograd.Variable._execution_engine.queue_callback(_join_side)
         for t in self.tensors:
             if t is not None:
