@@ -269,12 +269,13 @@ int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* m
  * output NHWC [N, H, W, C] (C a power of two <= 256).  Train mode: mean /
  * invstd from hvit_bn_finalize (which also updates running stats with
  * momentum and the unbiased variance, and increments num_batches_tracked);
- * eval: hvit_bn_eval_prep.  Backward: dz from dy = grad of the pooled output;
+ * eval: hvit_bn_eval_prep (hvit_bn_finalize uses its partials buffer as scratch: overwritten).
+ * Backward: dz from dy = grad of the pooled output;
  * sums (hvit_bn_act_bwd_sums_elems(C) floats: [2][C] result followed by
  * per-workgroup partial rows, all overwritten -- no zeroing needed, flags is
  * ignored) receives (dbeta, dgamma) in its first 2*C entries. */
 long long hvit_bn_act_bwd_sums_elems(int C);
-int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C, float* mean,
+int hvit_bn_finalize(float* partials, int ntiles, int tile_rows, long long M, int C, float* mean,
                      float* invstd, float* running_mean, float* running_var, long long* num_batches_tracked,
                      float momentum, float eps, void* stream);
 int hvit_bn_eval_prep(const float* running_mean, const float* running_var, int C, float eps, float* mean,

@@ -262,49 +262,74 @@ __global__ __launch_bounds__(256) void ln_slab_sum_kernel(const float* __restric
 
 // ------------------------------------------------------------- BatchNorm ---
 // partials[t][c] = (mean, M2) over cnt_t rows; cnt_t = tile_rows except the last.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int ntiles, int tile_rows,
-                                                         long M, int C, float* __restrict__ mean_out,
-                                                         float* __restrict__ invstd_out, float* __restrict__ rmean,
-                                                         float* __restrict__ rvar, float momentum, float eps,
-                                                         long long* nbt) {
-  __shared__ float sn[256], sm[256], sq[256];
-  int c = blockIdx.x;
+// Two levels, both in a fixed order (deterministic) with coalesced reads:
+//  1. bn_merge_chunks: workgroup (64 channels, chunk of BNF_CHUNK tiles), thread
+//     (channel, group g) Chan-merges tiles g, g + 4, ... of the chunk (each tile
+//     row of 64 channels is one 512-B read), the 4 groups merged in order through
+//     LDS; the chunk's (mean, M2) overwrites the chunk's first tile slot (read
+//     only by this workgroup, and only before the merge).
+//  2. bn_final: one thread per channel merges the chunks in order, then the
+//     batch statistics and the running-stat update (momentum, unbiased var).
+// (A single level -- one workgroup per channel walking every tile with
+// C-strided loads -- took ~12 us per call at the encoder shapes.)
+constexpr int BNF_CHUNK = 128;
+
+__device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float nb, float mb, float qb) {
+  if (nb <= 0.f) return;
+  const float nn = n + nb;
+  const float d = mb - mu;
+  mu += d * (nb / nn);
+  m2 += qb + d * d * (n * nb / nn);
+  n = nn;
+}
+
+__global__ __launch_bounds__(256) void bn_merge_chunks_kernel(float* __restrict__ part, int ntiles, int tile_rows,
+                                                              long M, int C) {
+  __shared__ float sn[4][64], sm[4][64], sq[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int t0 = blockIdx.y * BNF_CHUNK, t1 = min(ntiles, t0 + BNF_CHUNK);
   float n = 0.f, mu = 0.f, m2 = 0.f;
-  for (int t = threadIdx.x; t < ntiles; t += 256) {
-    float nb = (float)min((long)tile_rows, M - (long)t * tile_rows);
-    float mb = part[((long)t * C + c) * 2], qb = part[((long)t * C + c) * 2 + 1];
-    float nn = n + nb;
-    float d = mb - mu;
-    mu += d * (nb / nn);
-    m2 += qb + d * d * (n * nb / nn);
-    n = nn;
-  }
-  sn[threadIdx.x] = n; sm[threadIdx.x] = mu; sq[threadIdx.x] = m2;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      float na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
-      float nn = na + nb;
-      if (nb > 0.f) {
-        float d = sm[threadIdx.x + s] - sm[threadIdx.x];
-        sm[threadIdx.x] += d * (nb / nn);
-        sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * (na * nb / nn);
-        sn[threadIdx.x] = nn;
-      }
+  if (c < C)
+    for (int t = t0 + g; t < t1; t += 4) {
+      const float nb = (float)min((long)tile_rows, M - (long)t * tile_rows);
+      const float2 v = *(const float2*)(part + ((long)t * C + c) * 2);
+      chan_merge(n, mu, m2, nb, v.x, v.y);
     }
-    __syncthreads();
+  sn[g][cl] = n;
+  sm[g][cl] = mu;
+  sq[g][cl] = m2;
+  __syncthreads();
+  if (g == 0 && c < C) {
+#pragma unroll
+    for (int k = 1; k < 4; ++k) chan_merge(n, mu, m2, sn[k][cl], sm[k][cl], sq[k][cl]);
+    *(float2*)(part + ((long)t0 * C + c) * 2) = make_float2(mu, m2);
   }
-  if (threadIdx.x == 0) {
-    float mean = sm[0], var = sq[0] / (float)M;
-    mean_out[c] = mean;
+}
+
+__global__ __launch_bounds__(256) void bn_final_kernel(const float* __restrict__ part, int ntiles, int tile_rows,
+                                                       long M, int C, float* __restrict__ mean_out,
+                                                       float* __restrict__ invstd_out, float* __restrict__ rmean,
+                                                       float* __restrict__ rvar, float momentum, float eps,
+                                                       long long* nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    float n = 0.f, mu = 0.f, m2 = 0.f;
+    for (int t0 = 0; t0 < ntiles; t0 += BNF_CHUNK) {
+      const long rows = min((long)BNF_CHUNK * tile_rows, M - (long)t0 * tile_rows);
+      const float2 v = *(const float2*)(part + ((long)t0 * C + c) * 2);
+      chan_merge(n, mu, m2, (float)rows, v.x, v.y);
+    }
+    const float var = m2 / (float)M;
+    mean_out[c] = mu;
     invstd_out[c] = rsqrtf(var + eps);
     if (rmean) {
-      float unb = M > 1 ? sq[0] / (float)(M - 1) : var;
-      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      const float unb = M > 1 ? m2 / (float)(M - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
       rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
     }
-    if (nbt && c == 0) *nbt += 1;
   }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
 }
 
 __global__ void bn_eval_prep_kernel(const float* rmean, const float* rvar, int C, float eps, float* mean_out,
@@ -430,15 +455,19 @@ extern "C" int hvit_layernorm_bwd_drop(const void* dy, int dy_dt, const float* x
   return hvit_reduce_rows(ws, HVIT_F32, nblk, 3 * D, 3 * D, (flags & HVIT_ACC_ZEROED) ? 1 : 0, acc3, stream);
 }
 
-extern "C" int hvit_bn_finalize(const float* partials, int ntiles, int tile_rows, long long M, int C,
+extern "C" int hvit_bn_finalize(float* partials, int ntiles, int tile_rows, long long M, int C,
                                 float* mean, float* invstd, float* running_mean, float* running_var,
                                 long long* num_batches_tracked, float momentum, float eps, void* stream) {
   HVIT_CHECK(partials && mean && invstd, "hvit_bn_finalize: null pointer");
   HVIT_CHECK(M > 0 && C > 0 && ntiles > 0, "hvit_bn_finalize: bad sizes");
   HVIT_CHECK((running_mean == nullptr) == (running_var == nullptr), "hvit_bn_finalize: running stats pair");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partials, ntiles,
-                     tile_rows, (long)M, C, mean, invstd, running_mean, running_var, momentum, eps,
-                     num_batches_tracked);
+  hipStream_t st = (hipStream_t)stream;
+  // (the partials buffer is the first level's scratch: overwritten)
+  hipLaunchKernelGGL(bn_merge_chunks_kernel, dim3(cdiv(C, 64), cdiv(ntiles, BNF_CHUNK)), dim3(256), 0, st,
+                     (float*)partials, ntiles, tile_rows, (long)M, C);
+  HVIT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, partials, ntiles, tile_rows, (long)M, C,
+                     mean, invstd, running_mean, running_var, momentum, eps, num_batches_tracked);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }
