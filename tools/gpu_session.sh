@@ -5,6 +5,8 @@
 #   bench             default bench.py line (graph mode, CPU baseline)
 #   benchq            bench.py without the CPU baseline
 #   eager             bench.py --graph 0 --no-cpu-baseline
+#   infer             bench.py --mode infer (BASELINE config 2)
+#   large / largefp8  bench.py --variant large [--attn fp8] (BASELINE config 5)
 #   prof              rocprofv3 kernel stats of a short bench
 #   gemm              tools/gemm_bench.py
 #   env:VAR=VAL,...   benchq under extra environment variables (A/B knobs)
@@ -27,6 +29,9 @@ for s in "$@"; do
       done ;;
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 || exit $? ;;
     benchq) timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/${TAG}_benchq.log 2>&1 || exit $? ;;
+    infer) timeout -k 10 400 python -u bench.py --mode infer --no-cpu-baseline > gpurun_out/${TAG}_infer.log 2>&1 || exit $? ;;
+    large) timeout -k 10 400 python -u bench.py --variant large --no-cpu-baseline > gpurun_out/${TAG}_large.log 2>&1 || exit $? ;;
+    largefp8) timeout -k 10 400 python -u bench.py --variant large --attn fp8 --no-cpu-baseline > gpurun_out/${TAG}_largefp8.log 2>&1 || exit $? ;;
     eager) timeout -k 10 400 python -u bench.py --graph 0 --no-cpu-baseline > gpurun_out/${TAG}_eager.log 2>&1 || exit $? ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
     env:*)  # env:VAR=VAL[,VAR=VAL]: bench.py --no-cpu-baseline under those variables
