@@ -149,3 +149,39 @@ def test_train_step_bitwise_repeatable_poisoned_cache(hv, kw):
             assert torch.equal(runs[0][1][n], r[1][n]), n
         for n in runs[0][2]:
             assert torch.equal(runs[0][2][n], r[2][n]), n
+
+
+@pytest.mark.parametrize("kw", [dict(KW, embed_dim=128, num_heads=2, precision="bf16"), dict(precision="bf16")],
+                         ids=["hd64", "default"])
+def test_side_stream_weight_gradients_equal_single_stream(hv, kw):
+    """Weight gradients issued on the side stream (functional.SIDE, joined back
+    by the autograd final callback) equal the single-stream backward bit for
+    bit, and a second backward that accumulates (its launches stay on the
+    backward's stream) adds to them correctly."""
+    import sys
+
+    HF = sys.modules["hvit_amd.functional"]
+    torch.manual_seed(0)
+    m0 = hv.HybridViT(**kw).to(DEV).train()
+    crit = hv.CombinedLoss()
+    shape = (2, 1, 48, 64) if "embed_dim" in kw else (4, 1, 256, 256)
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand(shape, generator=g).to(DEV)
+    t = torch.rand(shape, generator=g).to(DEV)
+    runs = []
+    old = HF.SIDE
+    try:
+        for side in (False, True):
+            HF.SIDE = side
+            m = copy.deepcopy(m0)
+            m.set_dropout_state(77)
+            crit(m(x), t).backward()
+            first = {n: p.grad.clone() for n, p in m.named_parameters()}
+            crit(m(x), t).backward()  # accumulates (.grad exists): the single-stream form
+            torch.cuda.synchronize()
+            runs.append((first, {n: p.grad.clone() for n, p in m.named_parameters()}))
+    finally:
+        HF.SIDE = old
+    for n in runs[0][0]:
+        assert torch.equal(runs[0][0][n], runs[1][0][n]), n
+        assert torch.equal(runs[0][1][n], runs[1][1][n]), n
