@@ -492,16 +492,6 @@ typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
 
 __device__ __forceinline__ int v2_off(int row, int chunk) { return row * V2_ROWB + ((chunk ^ (row & 7)) << 4); }
 
-// rows [0, rows) of a [*, 64] bf16 matrix with element pitch `pitch` -> LDS
-// image (rows >= n zero-filled; `rows` a multiple of 16)
-__device__ __forceinline__ void v2_stage(char* dst, const bf16_t* src, long pitch, int n, int rows) {
-  for (int ch = threadIdx.x; ch < rows * 8; ch += AT_THREADS) {
-    const int r = ch >> 3, c = ch & 7;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (r < n) v = *(const u32x4*)(src + (long)r * pitch + c * 8);
-    *(u32x4*)(dst + v2_off(r, c)) = v;
-  }
-}
 // Same image filled by LDS-DMA (global_load_lds_dwordx4): no registers, no
 // per-chunk load->store latency chain.  One wave-instruction writes 1 KiB =
 // 8 rows; the destination is lane-linear, so the XOR swizzle moves to the
@@ -558,6 +548,11 @@ __device__ __forceinline__ f32x4 v2_mma32(u32x4 a, u32x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, a), __builtin_bit_cast(s16x8, b), c, 0,
                                                  0, 0);
 }
+// Score tile straight from its MFMAs into a branch (the partial-tile mask):
+// hipcc pads the MFMA -> VALU-read distance on the fall-through edge but not
+// on the taken one (1-3 wait states in the .s where an 8-pass XDL result needs
+// 11), so the wait goes inside a statement that takes the tile as an operand.
+__device__ __forceinline__ void v2_settle(f32x4& a) { asm volatile("s_nop 7\n\ts_nop 3" : "+v"(a)); }
 // 16x16x32 operand from two transposed 4-row reads (tiles jj and jj + 1):
 // k = 8g + e  <->  row 16*(jj + e/4) + 4g + e%4
 __device__ __forceinline__ u32x4 v2_cat(v4s_t lo, v4s_t hi) {
@@ -587,7 +582,7 @@ __device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uin
 // in LDS (128 KiB) and the keys taken in chunks of 256 with an online softmax
 // (running max and sum, the output rescaled when the max grows); for N <= 256
 // the one chunk gives exactly the single-pass arithmetic.  The KMAX = 512 form
-// runs 8-wave workgroups (152 VGPRs; at 16 waves the 128-VGPR budget spilled).
+// runs 8-wave workgroups (at 16 waves the 128-VGPR budget spilled).
 template <int WAVES, int KMAX>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int N, int H, float scale,
@@ -624,16 +619,14 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
 #pragma unroll
   for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float mxc = -INFINITY, sum = 0.f;
-#pragma unroll
-  for (int c0 = 0; c0 < KMAX; c0 += CH) {
-    if (c0 >= N) break;
-    // (no scheduling across chunks: the next chunk's score block would be live
-    // beside this one's -- spills at the 128-VGPR budget of 16 waves)
-    __builtin_amdgcn_sched_barrier(0);
+  // one 256-key chunk (C0 = 0 or 256, compile time): its scores, the online
+  // softmax update, P V; its keep bits
+  auto chunk = [&](auto c0c) {
+    constexpr int c0 = decltype(c0c)::value;
     const int nkt = (min(N - c0, CH) + 15) >> 4;  // key tiles of this chunk
     const char* Kc = Ks + c0 * V2_ROWB;
     const char* Vc = Vs + c0 * V2_ROWB;
-    // S^T tiles: st[j][r] = score(key c0 + 16j + 4fq + r, query q) in log2 units
+    // S^T tiles: st[j][r] = raw score(key c0 + 16j + 4fq + r, query q)
     // (keys >= N of the last, partial tile masked to -inf).  VALU diet: the 1/sum
     // and the dropout 1/(1-p) on the 16 outputs instead of the 64
     // probabilities, the dropout mask a select, masking only in a partial tile.
@@ -645,26 +638,25 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
         a = v2_mma32(v2_fragj(Kc, LN, j, 0), qf[0], a);
         a = v2_mma32(v2_fragj(Kc, LN, j, 1), qf[1], a);
+        v2_settle(a);
         if (c0 + 16 * j + 16 > N) {  // wave-uniform: only a partial last tile
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (c0 + 16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          a[r] *= c2;
-          mx = fmaxf(mx, a[r]);
-        }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, a[r]);
         st[j] = a;
       }
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    // (exp2(fma(s, c2, -mx c2)) on the raw scores measured run-to-run
-    // nondeterministic at the bf16-ulp level in this kernel -- tools/det_check.py
-    // -- so the scores are scaled first, as before)
-    const float mnew = fmaxf(mxc, mx);  // the running max in log2 units
-    if (c0 > 0) {  // online softmax: rescale what the earlier chunks accumulated
+    // raw scores kept; the scale folds into the exponent's fma (c2 > 0, so the
+    // max commutes with it).  (Round 3 measured this form run-to-run
+    // nondeterministic at the bf16-ulp level and scaled every score first: that
+    // was the missing MFMA -> VALU wait of v2_settle, not the fma.)
+    const float mnew = fmaxf(mxc, mx * c2);  // the running max in log2 units
+    if constexpr (c0 > 0) {  // online softmax: rescale what the earlier chunks accumulated
       const float rs = __builtin_amdgcn_exp2f(mxc - mnew);
       sum *= rs;
 #pragma unroll
@@ -677,7 +669,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
       if (j < nkt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(st[j][r] - mxc);
+          const float pv = __builtin_amdgcn_exp2f(fmaf(st[j][r], c2, -mxc));
           st[j][r] = pv;
           csum += pv;
         }
@@ -724,6 +716,10 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
     }
     if (q < N && kbits && thr)
       *(uint2*)(kbits + (((uint64_t)(c0 / CH) * BHN + bh * N + q) * 4 + fq) * 2) = make_uint2(kb[0], kb[1]);
+  };
+  chunk(std::integral_constant<int, 0>());
+  if constexpr (KMAX > CH) {
+    if (N > CH) chunk(std::integral_constant<int, CH>());
   }
   if (q < N) {
     const float inv = 1.f / sum;
