@@ -142,7 +142,9 @@ int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, in
 /* Tuning knobs (A/B measurements, tests): what 0 = GEMM pipeline of the bf16
  * linears (-1 automatic, 0: two-stage kernels; 1-5: LDS-ring configurations,
  * gemm_ring.h); what 1 = the fused first block's matrix-core kernels (1 on, 0:
- * the VALU kernels).  Returns the previous value (-1 for an unknown knob). */
+ * the VALU kernels); what 2 = workgroup target of the linear weight gradients'
+ * split-K choice for the calls that follow (0: default 256; also sizes
+ * hvit_wgrad_workspace).  Returns the previous value (-1 for an unknown knob). */
 int hvit_gemm_tune(int what, int value);
 /* dw[N,K] = dy^T x; db[N] = colsum(dy) (nullable; fused when db == dw + N*K) */
 int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,

@@ -99,11 +99,15 @@ int check_epi(const hvit_epilogue_t* e) {
 // (conv: the implicit-im2col weight gradient, whose 128x64 tiles fit more
 // workgroups per CU; HVIT_WG_TARGET / HVIT_CONV_WG_TARGET override the targets
 // for A/B measurements only)
+// wg_target: the caller's workgroup target for the linear weight gradients
+// that follow (hvit_set_wgrad_target; 0 = the default above) -- the side-stream
+// weight gradients, which share the chip with the data-gradient chain
+long wg_target = 0;
 int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64, bool conv = false) {
   long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
   static const long big = getenv("HVIT_WG_TARGET") ? atol(getenv("HVIT_WG_TARGET")) : 256;
   static const long cbig = getenv("HVIT_CONV_WG_TARGET") ? atol(getenv("HVIT_CONV_WG_TARGET")) : 256;
-  const long target = bm * bn <= 64 * 64 ? 512 : conv ? cbig : big;
+  const long target = bm * bn <= 64 * 64 ? 512 : conv ? cbig : wg_target > 0 ? wg_target : big;
   long want = (target + tiles - 1) / tiles;
   long maxs = K / (4 * bk);
   // a multiple of 8 slices: with the XCD-aware tile order (gemm.h tile_of)

@@ -230,6 +230,11 @@ int hvit_c1_tune(int value);  // c1block.hip
 
 extern "C" int hvit_gemm_tune(int what, int value) {
   if (what == 1) return hvit_c1_tune(value);
+  if (what == 2) {  // workgroup target of the linear weight gradients' split-K (0: default)
+    const int old = (int)wg_target;
+    wg_target = value > 0 ? value : 0;
+    return old;
+  }
   if (what != 0) return -1;
   const int old = ring_cfg_ref();
   ring_cfg_ref() = value;

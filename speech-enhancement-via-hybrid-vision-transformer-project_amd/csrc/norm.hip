@@ -262,17 +262,23 @@ __global__ __launch_bounds__(256) void ln_slab_sum_kernel(const float* __restric
 
 // ------------------------------------------------------------- BatchNorm ---
 // partials[t][c] = (mean, M2) over cnt_t rows; cnt_t = tile_rows except the last.
-// Two levels, both in a fixed order (deterministic) with coalesced reads:
+// Two levels, both in a fixed order (deterministic) with coalesced reads and
+// short dependent chains (a Chan merge is a division deep):
 //  1. bn_merge_chunks: workgroup (64 channels, chunk of BNF_CHUNK tiles), thread
-//     (channel, group g) Chan-merges tiles g, g + 4, ... of the chunk (each tile
-//     row of 64 channels is one 512-B read), the 4 groups merged in order through
-//     LDS; the chunk's (mean, M2) overwrites the chunk's first tile slot (read
-//     only by this workgroup, and only before the merge).
-//  2. bn_final: one thread per channel merges the chunks in order, then the
+//     (channel, group g) loads tiles g, g + 4, ... of the chunk up front (each
+//     tile row of 64 channels is one 512-B read) and Chan-merges them in order;
+//     the 4 groups are merged in order through LDS; the chunk's (mean, M2)
+//     overwrites the chunk's first tile slot (read only by this workgroup, and
+//     only before the merge).
+//  2. bn_final: workgroup (64 channels), thread (channel, group g of 16) merges
+//     chunks g, g + 16, ... in order, the 16 groups in order through LDS, then the
 //     batch statistics and the running-stat update (momentum, unbiased var).
-// (A single level -- one workgroup per channel walking every tile with
-// C-strided loads -- took ~12 us per call at the encoder shapes.)
-constexpr int BNF_CHUNK = 128;
+// (Round 4's first form -- 128-tile chunks, one thread per channel walking all
+// chunk results -- ran 64-256 workgroups with 32- and 128-deep chains: 13.6 +
+// 8.2 us per call; a single level with C-strided loads took ~12 us.)
+constexpr int BNF_CHUNK = 32;
+constexpr int BNF_G1 = 4;   // tile groups per chunk workgroup (BNF_CHUNK / BNF_G1 tiles per thread)
+constexpr int BNF_G2 = 16;  // chunk groups of the final workgroup
 
 __device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float nb, float mb, float qb) {
   if (nb <= 0.f) return;
@@ -283,18 +289,56 @@ __device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float
   n = nn;
 }
 
-__global__ __launch_bounds__(256) void bn_merge_chunks_kernel(float* __restrict__ part, int ntiles, int tile_rows,
-                                                              long M, int C) {
-  __shared__ float sn[4][64], sm[4][64], sq[4][64];
+__global__ __launch_bounds__(64 * BNF_G1) void bn_merge_chunks_kernel(float* __restrict__ part, int ntiles,
+                                                                      int tile_rows, long M, int C) {
+  constexpr int PER = BNF_CHUNK / BNF_G1;
+  __shared__ float sn[BNF_G1][64], sm[BNF_G1][64], sq[BNF_G1][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  const int t0 = blockIdx.y * BNF_CHUNK, t1 = min(ntiles, t0 + BNF_CHUNK);
+  const int t0 = blockIdx.y * BNF_CHUNK;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  if (c < C) {
+    float2 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int t = t0 + g + BNF_G1 * i;
+      v[i] = t < ntiles ? *(const float2*)(part + ((long)t * C + c) * 2) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const long t = t0 + g + BNF_G1 * i;
+      const float nb = t < ntiles ? (float)min((long)tile_rows, M - t * tile_rows) : 0.f;
+      chan_merge(n, mu, m2, nb, v[i].x, v[i].y);
+    }
+  }
+  sn[g][cl] = n;
+  sm[g][cl] = mu;
+  sq[g][cl] = m2;
+  __syncthreads();
+  if (g == 0 && c < C) {
+#pragma unroll
+    for (int k = 1; k < BNF_G1; ++k) chan_merge(n, mu, m2, sn[k][cl], sm[k][cl], sq[k][cl]);
+    *(float2*)(part + ((long)t0 * C + c) * 2) = make_float2(mu, m2);
+  }
+}
+
+__global__ __launch_bounds__(64 * BNF_G2) void bn_final_kernel(const float* __restrict__ part, int ntiles,
+                                                               int tile_rows, long M, int C,
+                                                               float* __restrict__ mean_out,
+                                                               float* __restrict__ invstd_out,
+                                                               float* __restrict__ rmean, float* __restrict__ rvar,
+                                                               float momentum, float eps, long long* nbt) {
+  __shared__ float sn[BNF_G2][64], sm[BNF_G2][64], sq[BNF_G2][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int nch = (ntiles + BNF_CHUNK - 1) / BNF_CHUNK;
   float n = 0.f, mu = 0.f, m2 = 0.f;
   if (c < C)
-    for (int t = t0 + g; t < t1; t += 4) {
-      const float nb = (float)min((long)tile_rows, M - (long)t * tile_rows);
-      const float2 v = *(const float2*)(part + ((long)t * C + c) * 2);
-      chan_merge(n, mu, m2, nb, v.x, v.y);
+    for (int k = g; k < nch; k += BNF_G2) {
+      const long t0 = (long)k * BNF_CHUNK;
+      const float rows = (float)min((long)BNF_CHUNK * tile_rows, M - t0 * tile_rows);
+      const float2 v = *(const float2*)(part + (t0 * C + c) * 2);
+      chan_merge(n, mu, m2, rows, v.x, v.y);
     }
   sn[g][cl] = n;
   sm[g][cl] = mu;
@@ -302,24 +346,7 @@ __global__ __launch_bounds__(256) void bn_merge_chunks_kernel(float* __restrict_
   __syncthreads();
   if (g == 0 && c < C) {
 #pragma unroll
-    for (int k = 1; k < 4; ++k) chan_merge(n, mu, m2, sn[k][cl], sm[k][cl], sq[k][cl]);
-    *(float2*)(part + ((long)t0 * C + c) * 2) = make_float2(mu, m2);
-  }
-}
-
-__global__ __launch_bounds__(256) void bn_final_kernel(const float* __restrict__ part, int ntiles, int tile_rows,
-                                                       long M, int C, float* __restrict__ mean_out,
-                                                       float* __restrict__ invstd_out, float* __restrict__ rmean,
-                                                       float* __restrict__ rvar, float momentum, float eps,
-                                                       long long* nbt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < C) {
-    float n = 0.f, mu = 0.f, m2 = 0.f;
-    for (int t0 = 0; t0 < ntiles; t0 += BNF_CHUNK) {
-      const long rows = min((long)BNF_CHUNK * tile_rows, M - (long)t0 * tile_rows);
-      const float2 v = *(const float2*)(part + ((long)t0 * C + c) * 2);
-      chan_merge(n, mu, m2, (float)rows, v.x, v.y);
-    }
+    for (int k = 1; k < BNF_G2; ++k) chan_merge(n, mu, m2, sn[k][cl], sm[k][cl], sq[k][cl]);
     const float var = m2 / (float)M;
     mean_out[c] = mu;
     invstd_out[c] = rsqrtf(var + eps);
@@ -463,11 +490,11 @@ extern "C" int hvit_bn_finalize(float* partials, int ntiles, int tile_rows, long
   HVIT_CHECK((running_mean == nullptr) == (running_var == nullptr), "hvit_bn_finalize: running stats pair");
   hipStream_t st = (hipStream_t)stream;
   // (the partials buffer is the first level's scratch: overwritten)
-  hipLaunchKernelGGL(bn_merge_chunks_kernel, dim3(cdiv(C, 64), cdiv(ntiles, BNF_CHUNK)), dim3(256), 0, st,
+  hipLaunchKernelGGL(bn_merge_chunks_kernel, dim3(cdiv(C, 64), cdiv(ntiles, BNF_CHUNK)), dim3(64 * BNF_G1), 0, st,
                      (float*)partials, ntiles, tile_rows, (long)M, C);
   HVIT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, partials, ntiles, tile_rows, (long)M, C,
-                     mean, invstd, running_mean, running_var, momentum, eps, num_batches_tracked);
+  hipLaunchKernelGGL(bn_final_kernel, dim3(cdiv(C, 64)), dim3(64 * BNF_G2), 0, st, partials, ntiles, tile_rows,
+                     (long)M, C, mean, invstd, running_mean, running_var, momentum, eps, num_batches_tracked);
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

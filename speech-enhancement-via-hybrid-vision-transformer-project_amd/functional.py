@@ -412,7 +412,16 @@ def linear_wgrad_now(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None, side
 # streams are registered with record_stream, so the caching allocator never
 # recycles them under a pending side launch.  Graph capture forks and joins
 # the side stream like any other (parallel branches of the captured step).
-SIDE = os.environ.get("HVIT_SIDE", "1") != "0"  # A/B knob: 0 = every launch on the backward's stream
+# Off by default: measured on the MI355X (B=32 graph step, tools/gpu_session.sh
+# env:HVIT_SIDE=...), the single-stream step is faster -- 5.62 vs 5.70 ms: the
+# data-gradient GEMMs already fill the 256 CUs, so the concurrent weight
+# gradients only add their split-K slab sums (a launch each on the side stream,
+# where no following launch carries them) and contend for the CUs; fewer
+# side-stream splits (HVIT_SIDE_WG 128 / 64) were slower still (5.79 / 6.10).
+SIDE = os.environ.get("HVIT_SIDE", "0") == "1"  # A/B knob: 1 = weight gradients on the side stream
+# workgroup target of the side stream's linear weight gradients (split-K
+# choice; 0 = the library default) -- A/B knob
+SIDE_WG = int(os.environ.get("HVIT_SIDE_WG", "0"))
 _SIDE_STREAMS = {}
 _SIDE_OPEN = set()
 _SIDE_TASKS = set()  # autograd graph tasks that have the join queued
@@ -448,7 +457,7 @@ class on_side:
     (produced or consumed across the two streams) are recorded on the side
     stream.  Registers the join for the end of this backward."""
 
-    __slots__ = ("dev", "tensors", "ctx")
+    __slots__ = ("dev", "tensors", "ctx", "wg")
 
     def __init__(self, dev, tensors=()):
         self.dev, self.tensors = dev, tensors
@@ -467,9 +476,12 @@ class on_side:
                 t.record_stream(s)
         self.ctx = torch.cuda.stream(s)
         self.ctx.__enter__()
+        self.wg = L.lib().hvit_gemm_tune(2, SIDE_WG) if SIDE_WG > 0 else None
         return s
 
     def __exit__(self, *exc):
+        if self.wg is not None:
+            L.lib().hvit_gemm_tune(2, self.wg)
         return self.ctx.__exit__(*exc)
 
 
