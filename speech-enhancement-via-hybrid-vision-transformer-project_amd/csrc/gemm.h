@@ -410,27 +410,60 @@ struct Epi {
 };
 
 // dst[i] = sum_z src[z * stride + i] over the side job's granules, spread over
-// every workgroup of the launch; the same pairing as sum_slabs_strided_kernel
-// (even slabs | odd slabs), so the result is bit-identical to that launch.
-// gemm_kernel runs it after its tile's epilogue (two or three workgroups per
-// CU, out of phase: the load latency overlaps a co-resident workgroup's K
-// loop); the ring kernels after issuing their DMA prologue (one workgroup per
-// CU: the latency overlaps the first stages' flight).  Any in-flight stores
-// only make a later counted vmcnt wait stricter.
+// every workgroup of the launch.  gemm_kernel runs it after its tile's
+// epilogue (two or three workgroups per CU, out of phase: the load latency
+// overlaps a co-resident workgroup's K loop); the ring kernels after issuing
+// their DMA prologue (one workgroup per CU: the latency overlaps the first
+// stages' flight).  Any in-flight stores only make a later counted vmcnt wait
+// stricter.  Two forms, both a fixed summation order (deterministic):
+//  * many granules (split-K weight-gradient slabs: ~10^5 granules, 4-32 slabs):
+//    a granule per thread, even | odd slabs paired as sum_slabs_strided_kernel
+//    (bit-identical to that launch), eight slabs' loads in flight per step;
+//  * at most one granule per wave (partial column-sum rows: ~500 granules x
+//    128 slabs): a granule per wave, its slabs over the lanes, then a
+//    butterfly.  (One thread walking 128 slabs held its workgroup ~20 us past
+//    the others: round 4, the fc1 weight gradient carrying the fc1 bias rows.)
 __device__ __forceinline__ void epi_side(const Epi& ep) {
   if (!ep.sj_n4) return;
-  const long nthr = (long)gridDim.x * gridDim.y * gridDim.z * blockDim.x;
+  const long nwg = (long)gridDim.x * gridDim.y * gridDim.z;
   const long b = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
   const f32x4* src = (const f32x4*)ep.sj_src;
   f32x4* dst = (f32x4*)ep.sj_dst;
+  const long st = ep.sj_stride4;
+  const int wpb = blockDim.x >> 6;
+  if (ep.sj_n4 <= nwg * wpb) {
+    const int lane = threadIdx.x & 63;
+    const long i = b * wpb + (threadIdx.x >> 6);
+    if (i >= ep.sj_n4) return;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = lane; k < ep.sj_splits; k += 64) s += src[(long)k * st + i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += __shfl_xor(s[e], o, 64);
+    }
+    if (lane == 0) dst[i] = s;
+    return;
+  }
+  const long nthr = nwg * blockDim.x;
   for (long i = b * blockDim.x + threadIdx.x; i < ep.sj_n4; i += nthr) {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
     int k = 0;
-    for (; k + 1 < ep.sj_splits; k += 2) {
-      s0 += src[(long)k * ep.sj_stride4 + i];
-      s1 += src[(long)(k + 1) * ep.sj_stride4 + i];
+    for (; k + 7 < ep.sj_splits; k += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(long)(k + u) * st + i];
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        s0 += v[u];
+        s1 += v[u + 1];
+      }
     }
-    if (k < ep.sj_splits) s0 += src[(long)k * ep.sj_stride4 + i];
+    for (; k + 1 < ep.sj_splits; k += 2) {
+      s0 += src[(long)k * st + i];
+      s1 += src[(long)(k + 1) * st + i];
+    }
+    if (k < ep.sj_splits) s0 += src[(long)k * st + i];
     dst[i] = s0 + s1;
   }
 }
