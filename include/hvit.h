@@ -327,13 +327,20 @@ int hvit_cast(const void* src, int src_dt, void* dst, int dst_dt, long long n, v
 /* Multi-tensor weight preparation, one launch for many parameters (replaces
  * per-weight hvit_cast / hvit_conv_weight_pack in the module forward):
  * kind 0 = cast f32 -> dt (numel elements), kind 1 / 2 = conv packing mode 0 / 1
- * of a [cout][cin][ks][ks] f32 weight.  numel % 4 == 0, 16-byte aligned src. */
+ * of a [cout][cin][ks][ks] f32 weight, kind 3 = eval BatchNorm folded into a
+ * mode-0 packing (hvit_bn_fold's result with mean = rmean, invstd =
+ * rsqrt(rvar + eps): dst = w * gamma * invstd per output channel, bias[cout] =
+ * beta - rmean * gamma * invstd; the bn fields are read for kind 3 only).
+ * numel % 4 == 0, 16-byte aligned src. */
 typedef struct {
   const float* src;
   void* dst;
   long long numel;
   int kind, dt;
   int cout, cin, ks;
+  const float *gamma, *beta, *rmean, *rvar;
+  float* bias;
+  float eps;
 } hvit_wprep_item_t;
 int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void* stream);
 long long hvit_dropout_colsum_ws_elems(int N);

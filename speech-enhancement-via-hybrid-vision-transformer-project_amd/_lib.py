@@ -55,7 +55,8 @@ class ConvGeom(C.Structure):
 
 class WPrepItem(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("numel", i64), ("kind", i32), ("dt", i32),
-                ("cout", i32), ("cin", i32), ("ks", i32)]
+                ("cout", i32), ("cin", i32), ("ks", i32), ("gamma", vp), ("beta", vp), ("rmean", vp),
+                ("rvar", vp), ("bias", vp), ("eps", f32)]
 
 
 class LossCfg(C.Structure):

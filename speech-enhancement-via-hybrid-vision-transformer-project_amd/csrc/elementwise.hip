@@ -291,23 +291,30 @@ __global__ void sum_slabs4_kernel(const float* ws, int splits, int n4, float* ou
 
 // Multi-tensor weight preparation (one launch per forward instead of one per
 // weight): f32 master parameters -> bf16/f32 copies (kind 0) or conv packings
-// (kind 1: [Cout][KS][KS][Cin], kind 2: flipped [Cin][KS][KS][Cout]).  The
-// flattened index space is split into 4-element units (every item's numel is
-// a multiple of 4); a thread locates its item in the prefix table.
-constexpr int WPREP_MAX = 32;
+// (kind 1: [Cout][KS][KS][Cin], kind 2: flipped [Cin][KS][KS][Cout], kind 3:
+// kind 1 with eval BatchNorm folded in, bn_fold_kernel's arithmetic with the
+// running statistics -- inference no longer spends an eval-prep and a fold
+// launch per conv block).  The flattened index space is split into 4-element
+// units (every item's numel is a multiple of 4); a thread locates its item in
+// the prefix table.
+constexpr int WPREP_MAX = 24;
 struct WPrepItem {
   const float* src;
   void* dst;
   int n4;    // numel / 4
-  int kind;  // 0 cast, 1 pack mode 0, 2 pack mode 1
+  int kind;  // 0 cast, 1 pack mode 0, 2 pack mode 1, 3 pack mode 0 with eval BN folded
   int dt;
   int co, ci, ks;
+  const float *gamma, *beta, *rmean, *rvar;
+  float* bias;
+  float eps;
 };
 struct WPrepArgs {
   int count;
   int start[WPREP_MAX + 1];  // prefix sums of n4
   WPrepItem it[WPREP_MAX];
 };
+static_assert(sizeof(WPrepArgs) <= 4096, "weight_prep: kernel argument size");
 
 __global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
   const int total = a.start[a.count];
@@ -337,9 +344,14 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
       t /= w.ks;
       const int ci = t % w.ci;
       const int co = t / w.ci;
-      const long o = w.kind == 1 ? (((long)co * w.ks + ky) * w.ks + kx) * w.ci + ci
+      const long o = w.kind != 2 ? (((long)co * w.ks + ky) * w.ks + kx) * w.ci + ci
                                  : (((long)ci * w.ks + (w.ks - 1 - ky)) * w.ks + (w.ks - 1 - kx)) * w.co + co;
-      st_dt(w.dst, o, v[e], w.dt);
+      float x = v[e];
+      if (w.kind == 3) {
+        x *= w.gamma[co] * rsqrtf(w.rvar[co] + w.eps);
+        if (i < w.co) w.bias[i] = w.beta[i] - w.rmean[i] * (w.gamma[i] * rsqrtf(w.rvar[i] + w.eps));
+      }
+      st_dt(w.dst, o, x, w.dt);
     }
   }
 }
@@ -609,12 +621,15 @@ extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void*
       const hvit_wprep_item_t& it = items[base + k];
       HVIT_CHECK(it.src && it.dst && it.numel >= 0 && it.numel % 4 == 0 && it.numel < (1LL << 31),
                  "hvit_weight_prep: item %d: null pointer or numel %% 4 != 0", base + k);
-      HVIT_CHECK(it.kind >= 0 && it.kind <= 2, "hvit_weight_prep: item %d: kind", base + k);
+      HVIT_CHECK(it.kind >= 0 && it.kind <= 3, "hvit_weight_prep: item %d: kind", base + k);
+      HVIT_CHECK(it.kind != 3 || (it.gamma && it.beta && it.rmean && it.rvar && it.bias),
+                 "hvit_weight_prep: item %d: BN fold needs gamma, beta, rmean, rvar, bias", base + k);
       HVIT_CHECK(it.kind == 0 || (long long)it.cout * it.cin * it.ks * it.ks == it.numel,
                  "hvit_weight_prep: item %d: conv shape", base + k);
       HVIT_CHECK(aligned16(it.src) && (it.kind != 0 || aligned16(it.dst)), "hvit_weight_prep: item %d: alignment",
                  base + k);
-      a.it[k] = WPrepItem{it.src, it.dst, (int)(it.numel / 4), it.kind, it.dt, it.cout, it.cin, it.ks};
+      a.it[k] = WPrepItem{it.src,   it.dst,  (int)(it.numel / 4), it.kind, it.dt,   it.cout, it.cin,
+                          it.ks,    it.gamma, it.beta,             it.rmean, it.rvar, it.bias, it.eps};
       a.start[k + 1] = a.start[k] + (int)(it.numel / 4);
     }
     const int total = a.start[a.count];

@@ -203,12 +203,19 @@ def shadow_mark(p):
 
 
 def prep_weights(items, dev):
-    """items: [(param, kind, dt)], kind 0 = cast, 1/2 = conv pack mode 0/1.
-    Replaces the cache with freshly prepared copies (one kernel launch); bf16
-    casts whose shadow is current are reused without a launch."""
+    """items: [(param, kind, dt)] or, kind 3, [(param, 3, dt, (gamma, beta,
+    running_mean, running_var, eps))]; kind 0 = cast, 1/2 = conv pack mode 0/1,
+    3 = mode-0 pack with eval BatchNorm folded in (prepared value: (packed
+    weight, f32 bias)).  Replaces the cache with freshly prepared copies (one
+    kernel launch); bf16 casts whose shadow is current are reused without a
+    launch."""
     _PREP.clear()
     todo = []
-    for w, kind, dt in items:
+    for w, kind, dt, *bn in items:
+        if kind == 3:
+            out = (_empty((w.numel(),), dt, dev), torch.empty(w.shape[0], dtype=torch.float32, device=dev))
+            todo.append((w, kind, dt, out, bn[0]))
+            continue
         if kind == 0 and L.dt_of(w) == dt:
             continue
         if kind == 0 and dt == BF16:
@@ -218,18 +225,23 @@ def prep_weights(items, dev):
             if e[2] == w._version:
                 _PREP[(id(w), kind, dt)] = (w._version, e[1], w)
                 continue
-            todo.append((w, kind, dt, e[1]))
+            todo.append((w, kind, dt, e[1], None))
             continue
         out = _empty(w.shape if kind == 0 else (w.numel(),), dt, dev)
-        todo.append((w, kind, dt, out))
+        todo.append((w, kind, dt, out, None))
     if not todo:
         return
     arr = (L.WPrepItem * len(todo))()
-    for i, (w, kind, dt, out) in enumerate(todo):
+    for i, (w, kind, dt, out, bn) in enumerate(todo):
         co, ci, ks = (w.shape[0], w.shape[1], w.shape[2]) if kind else (0, 0, 0)
-        arr[i] = L.WPrepItem(w.data_ptr(), out.data_ptr(), w.numel(), kind, dt, co, ci, ks)
+        if kind == 3:
+            gamma, beta, rmean, rvar, eps = bn
+            arr[i] = L.WPrepItem(w.data_ptr(), out[0].data_ptr(), w.numel(), kind, dt, co, ci, ks, gamma.data_ptr(),
+                                 beta.data_ptr(), rmean.data_ptr(), rvar.data_ptr(), out[1].data_ptr(), eps)
+        else:
+            arr[i] = L.WPrepItem(w.data_ptr(), out.data_ptr(), w.numel(), kind, dt, co, ci, ks)
     call("hvit_weight_prep", len(todo), arr, stream_ptr())
-    for w, kind, dt, out in todo:
+    for w, kind, dt, out, _ in todo:
         _PREP[(id(w), kind, dt)] = (w._version, out, w)
         if kind == 0 and dt == BF16:
             shadow_mark(w)
@@ -662,13 +674,17 @@ class ConvBNActFn(torch.autograd.Function):
             # eval, no backward (the caller ran outside grad mode): BatchNorm folded into the conv weights and bias, ReLU
             # in the conv epilogue (Dropout2d is the identity): z is never stored.  A pooling block (enc1) walks
             # its output pixels window by window and keeps each 2x2 window's maximum in the epilogue.
-            call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
-                 invstd.data_ptr(), s)
-            wf = _empty((w.numel(),), dt, dev)
-            bias = torch.empty(Cout, dtype=torch.float32, device=dev)
-            call("hvit_bn_fold", w.detach().contiguous().data_ptr(), Cout, Cin, KS, mean.data_ptr(),
-                 invstd.data_ptr(), gamma.detach().contiguous().data_ptr(), beta.detach().contiguous().data_ptr(),
-                 wf.data_ptr(), dt, bias.data_ptr(), s)
+            folded = _prep_get(w, 3, dt)  # (the module forward's weight_prep launch folded it)
+            if folded is not None:
+                wf, bias = folded
+            else:
+                call("hvit_bn_eval_prep", rmean.data_ptr(), rvar.data_ptr(), Cout, eps, mean.data_ptr(),
+                     invstd.data_ptr(), s)
+                wf = _empty((w.numel(),), dt, dev)
+                bias = torch.empty(Cout, dtype=torch.float32, device=dev)
+                call("hvit_bn_fold", w.detach().contiguous().data_ptr(), Cout, Cin, KS, mean.data_ptr(),
+                     invstd.data_ptr(), gamma.detach().contiguous().data_ptr(),
+                     beta.detach().contiguous().data_ptr(), wf.data_ptr(), dt, bias.data_ptr(), s)
             y = _empty((N, H // pool, W // pool, Cout), dt, dev)
             with timed("conv_fwd", cflops):
                 call("hvit_conv_fwd", dt, g, wf.data_ptr(), bias.data_ptr(), y.data_ptr(), dt, None,

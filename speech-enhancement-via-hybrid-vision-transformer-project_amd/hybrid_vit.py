@@ -379,9 +379,23 @@ class HybridViT(nn.Module):
         """Cast / pack every weight this forward (and its backward) will use
         in one multi-tensor launch instead of one launch per weight."""
         grads = torch.is_grad_enabled()
+        # inference (eval, no grad): the conv blocks' eval BatchNorm folded into their packed weights in the
+        # same launch (kind 3; HF.ConvBNActFn takes it) -- a pooling block also keeps the plain packing, used
+        # should the pooled fused form not apply to the input's shape
+        fold = not grads and not self.training and HF.EVALFOLD
+
+        def conv_items(blk, plain):
+            bn = blk.bn
+            w = blk.conv.weight
+            out = [(w, 3, dt, (bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.eps)))]
+            return out + [(w, 1, dt)] if plain else out
+
         items = []
         for i, blk in enumerate(self.encoder):
-            items.append((blk.conv.weight, 1, dt))
+            if fold and i > 0:
+                items += conv_items(blk, blk.pool != 1)
+            else:
+                items.append((blk.conv.weight, 1, dt))
             if grads and i > 0:
                 items.append((blk.conv.weight, 2, dt))
         items.append((self.patch_embed.projection.weight, 1, dt))
@@ -392,7 +406,10 @@ class HybridViT(nn.Module):
         if self.use_skip_connections:
             items += [(sp.weight, 0, dt) for sp in self.skip_projections]
         for blk in self.decoder:
-            items.append((blk.conv.weight, 1, dt))
+            if fold and not blk.final:
+                items += conv_items(blk, False)
+            else:
+                items.append((blk.conv.weight, 1, dt))
             if grads:
                 items.append((blk.conv.weight, 2, dt))
         HF.prep_weights(items, dev)
