@@ -1356,18 +1356,23 @@ class FinalFn(torch.autograd.Function):
         if (H, W) != (F, T):
             out = torch.empty((N, F, T, Cout), dtype=torch.float32, device=dev)
             call("hvit_bilinear_fwd", y.data_ptr(), F32, N, H, W, Cout, F, T, out.data_ptr(), F32, s)
+            ctx.save_for_backward(x, w)
+            ctx.y = y
         else:
-            out = y.clone()
-        ctx.save_for_backward(x, w)
-        ctx.y = y
+            # no resize: the conv output is the result, saved as an output (autograd's version check
+            # guards the tanh backward's y against in-place edits by the caller) instead of a copy
+            out = y
+            ctx.save_for_backward(x, w, out)
+            ctx.y = None
         ctx.meta = (U, out_hw, dt)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, w = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        x, w = saved[0], saved[1]
         U, (F, T), dt = ctx.meta
-        y = ctx.y
+        y = ctx.y if ctx.y is not None else saved[2]
         N, H, W, Cout = y.shape
         Hs, Ws, C = x.shape[1], x.shape[2], x.shape[3]
         KS = w.shape[2]
