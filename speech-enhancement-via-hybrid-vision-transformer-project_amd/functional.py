@@ -328,13 +328,14 @@ def linear_wgrad_deferred(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None,
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
     job = L.SlabSum()
 
-    def launch():
+    def launch(sj=side):
         call("hvit_linear_wgrad_defer", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), ws.data_ptr(), ws_n,
-             C.byref(side.job) if side is not None else None, C.byref(job), stream_ptr())
+             C.byref(sj.job) if sj is not None else None, C.byref(job), stream_ptr())
 
     with timed(tag, 2.0 * M * N * K):
         launch()
-    _record(tag, (launch, 2.0 * M * N * K))
+    # (the isolated replay re-runs the GEMM alone: the side job's slabs and destination belong to the step)
+    _record(tag, (lambda: launch(None), 2.0 * M * N * K))
     return dw, Deferred(job, ws)
 
 
@@ -406,7 +407,7 @@ def linear_wgrad_now(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None, side
 
         with timed(tag, 0.0):
             launch()
-        _record(tag, (lambda d=d: launch(), 0.0))
+        _record(tag, (lambda d=d, dw=dw: launch(), 0.0))  # (d, dw: the slabs and the destination stay alive)
     return dw
 
 
