@@ -5,6 +5,8 @@
 #   bench             default bench.py line (graph mode, CPU baseline)
 #   benchq            bench.py without the CPU baseline
 #   eager             bench.py --graph 0 --no-cpu-baseline
+#   dp1               bench.py's DP branch (RCCL, GradAllReducer, captured step) at world 1 under torchrun
+#   roof:OP           op class OP re-run in isolation: rocprofv3 kernel stats and FETCH/WRITE_SIZE passes
 #   infer             bench.py --mode infer (BASELINE config 2)
 #   large / largefp8  bench.py --variant large [--attn fp8] (BASELINE config 5)
 #   prof              rocprofv3 kernel stats of a short bench
@@ -33,6 +35,16 @@ for s in "$@"; do
     large) timeout -k 10 400 python -u bench.py --variant large --no-cpu-baseline > gpurun_out/${TAG}_large.log 2>&1 || exit $? ;;
     largefp8) timeout -k 10 400 python -u bench.py --variant large --attn fp8 --no-cpu-baseline > gpurun_out/${TAG}_largefp8.log 2>&1 || exit $? ;;
     eager) timeout -k 10 400 python -u bench.py --graph 0 --no-cpu-baseline > gpurun_out/${TAG}_eager.log 2>&1 || exit $? ;;
+    dp1) HVIT_FORCE_DIST=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+           --master-addr 127.0.0.1 --master-port 29531 bench.py --no-cpu-baseline > gpurun_out/${TAG}_dp1.log 2>&1 || exit $? ;;
+    roof:*)  # roof:OP -- the op class re-run in isolation: rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes
+      op=${s#roof:}
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof -o run --output-format csv -- \
+        python3 bench.py --roofline-only --roofline-op $op > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $?
+      for set in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/${TAG}_rpmc_$set -o run -- \
+          python3 bench.py --roofline-only --roofline-op $op > gpurun_out/${TAG}_rpmc_$set.log 2>&1 || exit $?
+      done ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
     env:*)  # env:VAR=VAL[,VAR=VAL]: bench.py --no-cpu-baseline under those variables
       kv=${s#env:}; tagv=$(echo "$kv" | tr ',=' '__')
