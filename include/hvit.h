@@ -48,7 +48,12 @@ enum {
  * per-workgroup partial rows (plain stores), so results are bit-identical from
  * run to run and between eager launches and hipGraph replays.  The one
  * exception is hvit_layernorm_bwd called WITHOUT a workspace (float atomics). */
-enum { HVIT_ACC_ZEROED = 1 };
+enum { HVIT_ACC_ZEROED = 1,
+       /* hvit_layernorm_bwd_drop only: leave the per-workgroup partial rows in
+        * ws ([ws_elems / (3*D)][3*D] f32, row order = summation order) for the
+        * caller to sum -- e.g. as the side job {ws, acc3, 3*D, 3*D, rows} of its
+        * next GEMM launch; acc3 is not touched */
+       HVIT_ACC_DEFER = 2 };
 
 /* Counter-based dropout: element i is kept iff a 16-bit hash of (seed, site, i)
  * is >= round(p * 65536); kept values are scaled by 1/(1-p).  Forward and

@@ -17,6 +17,7 @@ F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD, ACT_GELU_DUAL_D, ACT_MUL_AUX, ACT_RELU, ACT_GELU, ACT_RELU_POOL2 = (
     0, 1, 2, 3, 4, 5, 6, 7, 8)
 ACC_ZEROED = 1
+ACC_DEFER = 2
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # HVIT_LIB selects an alternative in-tree build (kernel A/B benchmarking only)

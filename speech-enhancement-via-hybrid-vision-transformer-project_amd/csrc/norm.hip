@@ -43,14 +43,20 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   int lane = threadIdx.x & 63;
   if (row >= M) return;
   const float* xr = x + (long)row * D;
-  f32x4 v[MAXV];
+  f32x4 v[MAXV], gv[MAXV], bv[MAXV];
   float s = 0.f;
+  // every load issued up front: at B=32 the whole launch is one round of waves
+  // (a row per wave), so the time is one row's latency chain, and gamma / beta
+  // loaded after the two reductions were a second memory round trip
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     int c = lane * 4 + i * 256;
     v[i] = c < D ? *(const f32x4*)(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    gv[i] = c < D ? *(const f32x4*)(g + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    bv[i] = c < D ? *(const f32x4*)(b + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   float mean = wave_sum_dpp(s) / (float)D;
   float q = 0.f;
 #pragma unroll
@@ -65,11 +71,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     int c = lane * 4 + i * 256;
-    if (c < D) {  // D % 4 == 0: one vector load of gamma / beta, one vector store
-      const f32x4 gv = *(const f32x4*)(g + c), bv = *(const f32x4*)(b + c);
+    if (c < D) {  // D % 4 == 0: one vector store
       f32x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * gv[e] + bv[e];
+      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * gv[i][e] + bv[i][e];
       if constexpr (sizeof(TY) == 4) {
         *(f32x4*)((float*)y + (long)row * D + c) = o;
       } else {
@@ -149,12 +154,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
   constexpr int RPW = LNB_ROWS / 4;
   const int row0 = blockIdx.x * LNB_ROWS + w * RPW;
   f32x4 xv[RPW][MAXV], dv[RPW][MAXV], rv[RPW][MAXV];
-  float mu[RPW], rs[RPW];
+  float mu[RPW], rs[RPW], rsc[RPW];
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int row = min(row0 + r, M - 1);  // rows past M re-read the last row; never stored
     mu[r] = mean[row];
     rs[r] = rstd[row];
+    rsc[r] = (DROP && dr.rowscale) ? dr.rowscale[row / dr.rps] : 1.f;  // (with the rows: no later round trip)
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int c = lane * 4 + i * 256;
@@ -191,7 +197,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     }
     s1 = wave_sum_dpp(s1) / (float)D;
     s2 = wave_sum_dpp(s2) / (float)D;
-    const float rsc = (DROP && dr.rowscale) ? dr.rowscale[row / dr.rps] : 1.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int c = lane * 4 + i * 256;
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
         if constexpr (DROP) {
           f32x4 k = {dr.ds, dr.ds, dr.ds, dr.ds};
           if (dr.thr) k = keep4_at(dkey, (uint64_t)row * D + c, dr.thr, dr.ds);
-          const f32x4 gv = o * k * rsc;
+          const f32x4 gv = o * k * rsc[r];
           if (dr.g_bf16) {
             *(uint2*)((bf16_t*)dr.g + (long)row * D + c) = make_uint2(f2bf2(gv[0], gv[1]), f2bf2(gv[2], gv[3]));
           } else {
@@ -478,6 +483,7 @@ extern "C" int hvit_layernorm_bwd_drop(const void* dy, int dy_dt, const float* x
   else { if (D <= 256) LNBD(bf16_t, 1); else if (D <= 512) LNBD(bf16_t, 2); else LNBD(bf16_t, 4); }
 #undef LNBD
   HVIT_LAUNCH_CHECK();
+  if (flags & HVIT_ACC_DEFER) return HVIT_OK;  // the caller sums the partial rows (a later launch's side job)
   // one column reduction of the [nblk][3D] slab into [dgamma | dbeta | colsum]
   return hvit_reduce_rows(ws, HVIT_F32, nblk, 3 * D, 3 * D, (flags & HVIT_ACC_ZEROED) ? 1 : 0, acc3, stream);
 }

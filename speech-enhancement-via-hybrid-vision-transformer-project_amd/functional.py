@@ -970,22 +970,28 @@ def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):
     return dx, dgw, dgb
 
 
-def _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs: ZSlot, drop, rowscale, rps, g_dt):
+def _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs: ZSlot, drop, rowscale, rps, g_dt, defer=False):
     """_ln_bwd fused with dropout_scale of its output: returns dx (f32), dgamma,
     dbeta, g = rowscale * dropout(dx) in g_dt and colsum(g).  zs: a zslot(3 * D)
-    (dgamma | dbeta | colsum)."""
+    (dgamma | dbeta | colsum).  ``defer``: the [dgamma | dbeta | colsum] row sum
+    is left to a later launch -- a sixth value, the Deferred job to pass as its
+    side job (the three results are final once that launch is)."""
     M, D = x.shape
     dx = torch.empty((M, D), dtype=torch.float32, device=x.device)
     g = _empty((M, D), g_dt, x.device)
-    acc = zs.take(x.device)
+    acc = zs.take(x.device) if not defer else torch.empty(3 * D, dtype=torch.float32, device=x.device)
     ws_n = L.lib().hvit_layernorm_bwd_drop_ws_elems(M, D)
     ws = torch.empty(ws_n, dtype=torch.float32, device=x.device)
     es = g.element_size()
     with timed("layernorm_bwd", float(M * D * (dy.element_size() + 8 + (4 if resid is not None else 0) + es))):
         call("hvit_layernorm_bwd_drop", dy.data_ptr(), L.dt_of(dy), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
              gw.data_ptr(), M, D, ptr(resid), dx.data_ptr(), acc.data_ptr(), drop, ptr(rowscale), rps, g.data_ptr(),
-             g_dt, ws.data_ptr(), ws_n, L.ACC_ZEROED, stream_ptr())
-    return dx, acc[:D], acc[D:2 * D], g, acc[2 * D:3 * D]
+             g_dt, ws.data_ptr(), ws_n, L.ACC_DEFER if defer else L.ACC_ZEROED, stream_ptr())
+    out = (dx, acc[:D], acc[D:2 * D], g, acc[2 * D:3 * D])
+    if defer:
+        rows = ws_n // (3 * D)
+        out += (Deferred(L.SlabSum(ws.data_ptr(), acc.data_ptr(), 3 * D, 3 * D, rows), (ws, acc)),)
+    return out
 
 
 class GradHandoff:
@@ -1183,8 +1189,11 @@ class ViTBlockFn(torch.autograd.Function):
         _launch("vit_linear_dgrad", 2.0 * M * hid * D,
                 lambda e: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
                                e, s), e_fc1)
-        if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass
-            dx1, dn2w, dn2b, g1, dpb = _ln_bwd_drop(dxn2, x1, m2, r2, n2w, dx2, zln2, drp, rs1, Nt, dt)
+        jln = None
+        if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass; its
+            # [dgamma | dbeta | proj bias] partial rows summed by the proj weight-gradient launch (side job)
+            dx1, dn2w, dn2b, g1, dpb, jln = _ln_bwd_drop(dxn2, x1, m2, r2, n2w, dx2, zln2, drp, rs1, Nt, dt,
+                                                         defer=True)
         else:
             dx1, dn2w, dn2b = _ln_bwd(dxn2, x1, m2, r2, n2w, dx2, zln2)
             g1 = _empty((M, D), dt, dev)
@@ -1193,11 +1202,11 @@ class ViTBlockFn(torch.autograd.Function):
         # attention branch
         if side:
             dpw = wdest(dp_id, D, D)
-            with on_side(dev, (g1, o, dpw)):
-                linear_wgrad_now(dt, g1, o, M, D, D, dest=dpw)
+            with on_side(dev, (g1, o, dpw) + (jln.ws if jln is not None else ())):
+                linear_wgrad_now(dt, g1, o, M, D, D, dest=dpw, side=jln)
             jp = None
         else:
-            dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id))
+            dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id), side=jln)
         do = _empty((M, D), dt, dev)
         e_pr = epilogue(side=jp)
         _launch("vit_linear_dgrad", 2.0 * M * D * D,
