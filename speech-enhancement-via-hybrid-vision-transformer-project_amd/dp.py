@@ -223,11 +223,17 @@ class GradAllReducer:
             s.wait_stream(torch.cuda.current_stream(dev))
             ctx = torch.cuda.stream(s)
         with ctx:
+            # the gradients not already in the bucket (biases, norms, sliced rows, accumulated ones):
+            # one multi-tensor copy instead of a copy launch per tensor (~85 per step at ~5 us each)
+            dsts, srcs = [], []
             for p, o in zip(ps, offs):
                 v = self._view(p)
                 dst = flat[o:o + v.numel()].view_as(v)
                 if dst.data_ptr() != v.data_ptr():
-                    dst.copy_(v)
+                    dsts.append(dst)
+                    srcs.append(v)
+            if dsts:
+                torch._foreach_copy_(dsts, srcs)
             self.works[b] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish(self):
@@ -280,10 +286,11 @@ class GradAllReducer:
             with torch.no_grad():
                 fb = torch.cat([t.reshape(-1).float() for t in bufs])
                 dist.broadcast(fb, src, group=self.group)
-                o = 0
+                views, o = [], 0
                 for t in bufs:
-                    t.copy_(fb[o:o + t.numel()].view_as(t))
+                    views.append(fb[o:o + t.numel()].view_as(t))
                     o += t.numel()
+                torch._foreach_copy_(bufs, views)  # (one multi-tensor launch)
         self._max_tokens = 0
         self._gen ^= 1
         self.reset()
