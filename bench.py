@@ -306,7 +306,10 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture: under DP the process group's watchdog thread
+        # polls the events of earlier collectives; in the default (global) mode
+        # that poll during the capture invalidates it (hipErrorStreamCaptureUnsupported)
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             static_loss = step()
 
         def step():

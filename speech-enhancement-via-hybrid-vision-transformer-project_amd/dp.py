@@ -43,8 +43,12 @@ over xGMI; gloo works for CPU tests and for ranks that share one GPU.
 * BatchNorm statistics are computed per replica (local BN, as DDP without
   SyncBN; the reference has no distributed code to match).  With
   ``broadcast_buffers`` (default, as DDP) rank 0's running statistics are
-  broadcast to every rank in ``finish()`` (one coalesced broadcast), so replicas
-  never diverge and any rank's ``state_dict`` equals rank 0's.
+  broadcast to every rank (one coalesced broadcast launched when a training
+  forward ends, overlapped with the backward, installed in ``finish()``), so
+  replicas never diverge and any rank's ``state_dict`` equals rank 0's.
+* Buckets close at 25 MB and, once past 4 MB, where the top-level component
+  changes, so the last bucket (the exposed tail of the step) is the encoder's
+  1.5 MB rather than a mix with the first ViT block's gradients.
 """
 
 from __future__ import annotations
@@ -76,14 +80,21 @@ class GradAllReducer:
         self.bucket_mb = bucket_mb
         cap = int(bucket_mb * 1024 * 1024)
         self.buckets: List[List[torch.nn.Parameter]] = []
-        cur, size = [], 0
+        cur, size, top = [], 0, None
         for n, p in reversed(named):
             nbytes = self._numel(p) * 4
-            if cur and size + nbytes > cap:
+            # a bucket of at least 4 MB also closes where the top-level component
+            # changes: the last bucket launched is then the early encoder's few
+            # weights alone, not a 25 MB mix with the first ViT block's, whose
+            # gradients were ready long before (the last bucket's all-reduce is the
+            # exposed tail of the step); smaller ones merge on (collective latency)
+            t = n.split(".")[0]
+            if cur and (size + nbytes > cap or (t != top and size >= (4 << 20))):
                 self.buckets.append(cur)
                 cur, size = [], 0
             cur.append(p)
             size += nbytes
+            top = t
         if cur:
             self.buckets.append(cur)
         self.where = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
@@ -99,6 +110,7 @@ class GradAllReducer:
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         # pre-accumulate hooks: a gradient arriving for an already-reduced bucket
         self._hooks += [p.register_hook(self._pre_grad_hook(p)) for p in self.params]
+        self._bcast = []  # (work, flat, buffers) of the buffer broadcasts launched by training forwards
         self._fwd_hook = model.register_forward_hook(self._on_forward)
         self._syncing = True
         self.broadcast_buffers = broadcast_buffers
@@ -142,6 +154,24 @@ class GradAllReducer:
         n = getattr(module, "last_num_tokens", None)
         if n is not None:
             self._max_tokens = max(self._max_tokens, int(n))
+        if self.broadcast_buffers and self.world > 1 and module.training:
+            # the running statistics are final for this step once the forward has
+            # run (the backward does not touch them): broadcast them now, overlapped
+            # with the whole backward, and install them in finish()
+            bufs = self._float_buffers()
+            if bufs:
+                with torch.no_grad():
+                    fb = torch.cat([t.reshape(-1).float() for t in bufs])
+                    work = dist.broadcast(fb, self._bcast_src(), group=self.group, async_op=True)
+                self._bcast.append((work, fb, bufs))
+
+    def _float_buffers(self):
+        # the module's current buffers (a .to() / .cuda() since construction replaces them)
+        return [b for b in self.model.buffers() if b.is_floating_point()]
+
+    def _bcast_src(self):
+        # the group's rank 0 as a global rank
+        return dist.get_global_rank(self.group, 0) if self.group is not None else 0
 
     def set_rows(self, name: str, rows: int):
         """Change a sliced parameter's row bound (bucket sizes follow)."""
@@ -278,14 +308,22 @@ class GradAllReducer:
                     v.copy_(flat[o:o + v.numel()].view_as(v))
                 else:
                     p.grad = flat[o:o + p.numel()].view_as(p)
-        # the module's current buffers (a .to() / .cuda() since construction
-        # replaces them); the source is the group's rank 0 as a global rank
-        bufs = [b for b in self.model.buffers() if b.is_floating_point()]
-        if self.broadcast_buffers and self.world > 1 and bufs:
-            src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        # rank 0's buffers: the broadcast the last training forward launched, or
+        # (no forward through the module this step) one issued now
+        pending, self._bcast = self._bcast, []
+        for work, _, _ in pending[:-1]:
+            work.wait()
+        bcast = pending[-1] if pending else None
+        if bcast is None and self.broadcast_buffers and self.world > 1:
+            bufs = self._float_buffers()
+            if bufs:
+                with torch.no_grad():
+                    fb = torch.cat([t.reshape(-1).float() for t in bufs])
+                    bcast = (dist.broadcast(fb, self._bcast_src(), group=self.group, async_op=True), fb, bufs)
+        if bcast is not None:
+            work, fb, bufs = bcast
+            work.wait()
             with torch.no_grad():
-                fb = torch.cat([t.reshape(-1).float() for t in bufs])
-                dist.broadcast(fb, src, group=self.group)
                 views, o = [], 0
                 for t in bufs:
                     views.append(fb[o:o + t.numel()].view_as(t))

@@ -106,7 +106,10 @@ class GraphedTrainStep:
         e.t = clean.detach().clone()
         torch.cuda.synchronize(noisy.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture: a data-parallel reducer's process-group watchdog
+        # thread polls earlier collectives' events, which a global-mode capture
+        # would count as an illegal call and abort on
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             e.loss = self._eager(e.x, e.t)
         e.graph = g
         self.captures += 1

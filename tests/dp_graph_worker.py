@@ -63,7 +63,7 @@ def main():
             step(ma, ra, oa)
     torch.cuda.current_stream().wait_stream(side)
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # (the watchdog thread polls events)
         static_loss = step(ma, ra, oa)
     for _ in range(2):
         step(mb, rb, ob)
