@@ -138,18 +138,22 @@ def roofline_loop(step, name=None, reps=20):
     return roofline_of(t)
 
 
+WORKLOAD = {"variant": "default", "mode": "train", "batch": 32}  # this run's (set in main)
+
+
 def measured_traffic(name):
     """HBM bytes per launch of op class ``name`` from the committed PMC pass
-    (profiles/roofline_pmc.json, written by tools/pmc_summary.py from
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over ``bench.py
-    --roofline-only``; FETCH_SIZE doubled per the gfx950 correction).  None
-    when absent or recorded for another op."""
+    (profiles/roofline_pmc.json, written from rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes over ``bench.py --roofline-only``; FETCH_SIZE doubled per
+    the gfx950 correction).  None when absent or recorded for another op or
+    another workload (the pass is of the default B=32 train step)."""
     p = os.path.join(ROOT, "profiles", "roofline_pmc.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch") if d.get("op") == name else None
+    same = all(d.get(k, v) == v for k, v in WORKLOAD.items())
+    return d.get("hbm_bytes_per_launch") if d.get("op") == name and same else None
 
 
 def cpu_model():
@@ -228,6 +232,7 @@ def cpu_baseline(batch, budget_s):
 
 def main():
     args = parse()
+    WORKLOAD.update(variant=args.variant, mode=args.mode, batch=args.batch)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
