@@ -278,6 +278,19 @@ __global__ void sum_slabs4_kernel(const float* ws, int splits, int n4, float* ou
     const f32x4* p = (const f32x4*)ws + i;
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
     int k = 0;
+    for (; k + 8 <= splits; k += 8) {  // eight slabs in flight, the same accumulator order
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * n4];
+      s0 += v[0];
+      s1 += v[1];
+      s2 += v[2];
+      s3 += v[3];
+      s0 += v[4];
+      s1 += v[5];
+      s2 += v[6];
+      s3 += v[7];
+    }
     for (; k + 4 <= splits; k += 4) {
       s0 += p[(long)k * n4];
       s1 += p[(long)(k + 1) * n4];
@@ -417,6 +430,20 @@ __global__ void sum_slabs_unpack4_kernel(const float* ws, int splits, long slab4
     const f32x4* p = (const f32x4*)ws + i;
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
     int k = 0;
+    // eight slabs' loads in flight per step (the same four-accumulator order)
+    for (; k + 8 <= splits; k += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * slab4];
+      s0 += v[0];
+      s1 += v[1];
+      s2 += v[2];
+      s3 += v[3];
+      s0 += v[4];
+      s1 += v[5];
+      s2 += v[6];
+      s3 += v[7];
+    }
     for (; k + 4 <= splits; k += 4) {
       s0 += p[(long)k * slab4];
       s1 += p[(long)(k + 1) * slab4];
