@@ -164,6 +164,8 @@ class GradAllReducer:
                     fb = torch.cat([t.reshape(-1).float() for t in bufs])
                     work = dist.broadcast(fb, self._bcast_src(), group=self.group, async_op=True)
                 self._bcast.append((work, fb, bufs))
+                if len(self._bcast) > 4:  # forwards without a finish() (no-grad passes in train mode): keep the last
+                    self._bcast.pop(0)[0].wait()
 
     def _float_buffers(self):
         # the module's current buffers (a .to() / .cuda() since construction replaces them)
