@@ -132,6 +132,44 @@ def test_bf16_path(hv, name, kw):
     assert abs(gq.double().norm().item() - float(g[f"gnorm.{qk}"])) < 0.1 * float(g[f"gnorm.{qk}"])
 
 
+def test_long_clip_bf16_vs_oracle(hv):
+    """A ~4 s clip: the default model on a [1, 1, 256, 496] spectrogram, 496
+    tokens -- the register-resident attention's chunked N > 256 forward (8-wave
+    workgroups, two 256-key chunks, online softmax) and its KMAX = 512 backward
+    (data/dataset.py:297-347 pads T per batch).  bf16 eval forward
+    against the fp32 CPU oracle (closed-form weights) within the bf16 bar, and a
+    dropout-free bf16 train step: the loss within 2 %, every ViT qkv weight
+    gradient within 5e-2 relative L2 of the oracle's autograd (measured values
+    printed)."""
+    cfg = O.HViTConfig()
+    cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
+    shapes = O.state_dict_shapes(cfg)
+    W = CF.weights(shapes)
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(1, 1, 256, 496, generator=g)
+    t = torch.rand(1, 1, 256, 496, generator=g)
+    m = hv.HybridViT(**cfg.as_kwargs(), precision="bf16").cuda()
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
+    sd = O.make_state(shapes, W, requires_grad=False)
+    with torch.no_grad():
+        y = m.eval()(x.cuda()).cpu()
+        yo = O.forward(sd, x, cfg)
+    assert m.last_num_tokens == 496
+    e_fwd = rel(y, yo)
+    sdg = O.make_state(shapes, W, requires_grad=True)
+    lo = O.combined_loss(O.forward(sdg, x, cfg, training=True), t)
+    lo.backward()
+    lg = hv.CombinedLoss()(m.train()(x.cuda()), t.cuda())
+    lg.backward()
+    torch.cuda.synchronize()
+    e_qkv = max(relnorm(blk.attn.qkv.weight.grad.cpu(), sdg[f"transformer.blocks.{i}.attn.qkv.weight"].grad)
+                for i, blk in enumerate(m.transformer.blocks))
+    print(f"N=496: fwd rel {e_fwd:.2e}, loss {lg.item():.6f} vs {lo.item():.6f}, worst qkv grad relnorm {e_qkv:.2e}")
+    assert e_fwd < BF16_TOL
+    assert abs(lg.item() - lo.item()) < 2e-2 * abs(lo.item())
+    assert e_qkv < 5e-2
+
+
 def test_inference_fusions_match_training_graph_path(hv):
     """Inference (eval + no_grad, BASELINE config 2) takes the fused forms: eval
     BatchNorm folded into every conv block (the pooling encoder block keeping
