@@ -360,6 +360,9 @@ int hvit_reduce_rows(const void* x, int dt, long long M, long long N, long long 
 int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* stream);
 int hvit_droppath_scale(int B, const hvit_dropout_t* dropout, float* out, void* stream);  /* DropPath
                                                                      components.py:407-427 */
+int hvit_droppath_scales(int B, int n, const hvit_dropout_t* dropouts, float* out, void* stream);
+                     /* n <= 32 sites in one launch: out[j*B + b] = hvit_droppath_scale(B, &dropouts[j])[b]
+                        (every transformer block's two branch multipliers, components.py:407-427) */
 
 /* ---- Train-step neighbours.
  * CombinedLoss (training/losses.py:286-387; STOILoss :109-141, PerceptualLoss

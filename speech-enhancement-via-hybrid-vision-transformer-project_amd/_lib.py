@@ -134,6 +134,7 @@ _SIGS = {
     "hvit_reduce_rows": ([vp, i32, i64, i64, i64, i32, vp, vp], i32),
     "hvit_sum_slabs": ([vp, i32, i64, vp, vp], i32),
     "hvit_droppath_scale": ([i32, P(Dropout), vp, vp], i32),
+    "hvit_droppath_scales": ([i32, i32, P(Dropout), vp, vp], i32),
     "hvit_weight_prep": ([i32, P(WPrepItem), vp], i32),
     "hvit_conv_bn_tile_rows": ([P(ConvGeom)], i32),
     "hvit_loss_ws_elems": ([i32, i64], i64),

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import math
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import ctypes as C
@@ -590,6 +590,9 @@ class Drop:
     seed: int = 0
     site: int = 0
     seed_t: Optional[torch.Tensor] = None
+    # DropPath sites only: this block's [2B] multipliers, already drawn by the
+    # forward's one droppath_scales_all launch (used instead of a launch of its own)
+    pre: Optional[torch.Tensor] = field(default=None, compare=False, repr=False)
 
     def c(self):
         return L.dropout(self.p, self.seed, self.site, self.seed_t)
@@ -1024,10 +1027,32 @@ def droppath_scales(B, p, seed, dev):
     whose (seed, seed_t) are used (site 1, its p ignored)."""
     if p <= 0:
         return None, None
+    if isinstance(seed, Drop) and seed.pre is not None and seed.pre.numel() == 2 * B:
+        return seed.pre[:B], seed.pre[B:]
     out = torch.empty(2 * B, dtype=torch.float32, device=dev)
     d = L.dropout(p, seed.seed, 1, seed.seed_t) if isinstance(seed, Drop) else L.dropout(p, seed, 1)
     call("hvit_droppath_scale", 2 * B, d, out.data_ptr(), stream_ptr())
     return out[:B], out[B:]
+
+
+def droppath_scales_all(B, sites, dev):
+    """droppath_scales for several blocks from ONE launch: ``sites`` are the
+    blocks' (p, Drop) pairs (p > 0); each Drop's ``pre`` is set to its [2B]
+    multipliers (the same values droppath_scales(B, p, drop) draws)."""
+    sites = [(p, d) for p, d in sites if p > 0]
+    if not sites:
+        return
+    out = torch.empty((len(sites), 2 * B), dtype=torch.float32, device=dev)
+    for k in range(0, len(sites), 32):
+        part = sites[k:k + 32]
+        arr = (L.Dropout * len(part))()
+        keep = []
+        for i, (p, d) in enumerate(part):
+            arr[i] = L.dropout(p, d.seed, 1, d.seed_t)
+            keep.append(arr[i])
+        call("hvit_droppath_scales", 2 * B, len(part), arr, out[k].data_ptr(), stream_ptr())
+    for i, (_, d) in enumerate(sites):
+        d.pre = out[i]
 
 
 class ViTBlockFn(torch.autograd.Function):

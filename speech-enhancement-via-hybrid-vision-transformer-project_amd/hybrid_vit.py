@@ -478,12 +478,15 @@ class HybridViT(nn.Module):
             warnings.warn("hvit: attention_precision='fp8' is ignored: this forward runs the fp32 path "
                           "(precision='auto' outside an autocast region)")
             self._fp8_warned = True
+        dps = [HF.Drop(0.0, (300 + 10 * l) << 20, 1, seed) for l in range(len(self.transformer.blocks))]
+        if self.training:  # every block's DropPath multipliers from one launch
+            HF.droppath_scales_all(t.shape[0], [(blk.dpr, d) for blk, d in zip(self.transformer.blocks, dps)],
+                                   t.device)
         for l, blk in enumerate(self.transformer.blocks):
             a, m = blk.attn, blk.mlp.net
             base = 300 + 10 * l
             drops = (HF.Drop(blk.p_attn, 0, base, seed), HF.Drop(blk.p, 0, base + 1, seed),
-                     HF.Drop(blk.p, 0, base + 2, seed), HF.Drop(blk.p, 0, base + 3, seed),
-                     HF.Drop(0.0, base << 20, 1, seed))
+                     HF.Drop(blk.p, 0, base + 2, seed), HF.Drop(blk.p, 0, base + 3, seed), dps[l])
             ho_in, ho = ho, (HF.GradHandoff() if HF.LNDROP and self.training else None)
             t, probs = HF.ViTBlockFn.apply(t, blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias,
                                            a.proj.weight, a.proj.bias, blk.norm2.weight, blk.norm2.bias,

@@ -690,6 +690,28 @@ def test_droppath_scale_mask_and_rate(hv, p):
     sigma = (p * (1 - p) / B) ** 0.5
     assert abs(rate - (1 - p)) < 4 * sigma
 
+def test_droppath_scales_batched_equals_per_block(hv):
+    """hvit_droppath_scales (every block's DropPath multipliers in one launch, the
+    model's train forward) is bit-exact against one hvit_droppath_scale launch
+    per block -- varied p, seeds and a device seed word -- and against the hash
+    mirror; 40 sites cross the 32-per-launch split."""
+    import sys
+    HF = sys.modules["hvit_amd.functional"]
+    B = 300
+    seed_t = torch.tensor([0x5DEECE66D], dtype=torch.int64, device=DEV)
+    sites = [(0.02 + 0.01 * (j % 9), HF.Drop(0.0, (300 + 10 * j) << 20, 1, seed_t if j % 2 else None))
+             for j in range(40)]
+    HF.droppath_scales_all(B, sites, DEV)
+    l = L(hv)
+    for j, (p, d) in enumerate(sites):
+        ref = torch.empty(2 * B, device=DEV)
+        l.call("hvit_droppath_scale", 2 * B, l.dropout(p, d.seed, 1, d.seed_t), ref.data_ptr(), s())
+        assert torch.equal(d.pre, ref), j
+        if d.seed_t is None:
+            kept = torch.as_tensor(keep_mask(d.seed, 1, 2 * B, p), device=DEV)
+            assert torch.equal(d.pre != 0, kept), j
+
+
 def test_vit_block_droppath_matches_torch(hv):
     """A whole TransformerEncoderBlock (attention.py:176-213) in train mode with
     drop_path = 0.5 and dropout off, against torch ops on the same weights with

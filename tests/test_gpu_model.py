@@ -137,37 +137,52 @@ def test_long_clip_bf16_vs_oracle(hv):
     tokens -- the register-resident attention's chunked N > 256 forward (8-wave
     workgroups, two 256-key chunks, online softmax) and its KMAX = 512 backward
     (data/dataset.py:297-347 pads T per batch).  bf16 eval forward
-    against the fp32 CPU oracle (closed-form weights) within the bf16 bar, and a
-    dropout-free bf16 train step: the loss within 2 %, every ViT qkv weight
-    gradient within 5e-2 relative L2 of the oracle's autograd (measured values
-    printed)."""
+    against the fp32 CPU oracle (closed-form weights) within the bf16 bar; a
+    dropout-free bf16 train step with the loss within 2 % and EVERY parameter
+    gradient held to the bar of test_batch32_train_step_bf16_vs_oracle_grads:
+    within 2x (+1e-2) of what torch bf16 autocast of the same oracle gives
+    (one sample: the weight gradients sum over 496 rows instead of 8192, so
+    their bf16 noise is larger than at B=32 -- the calibration carries that)."""
     cfg = O.HViTConfig()
     cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
     shapes = O.state_dict_shapes(cfg)
     W = CF.weights(shapes)
-    g = torch.Generator().manual_seed(11)
-    x = torch.rand(1, 1, 256, 496, generator=g)
-    t = torch.rand(1, 1, 256, 496, generator=g)
+    x = torch.as_tensor(CF.spectrogram((1, 1, 256, 496), 81))
+    t = torch.as_tensor(CF.spectrogram((1, 1, 256, 496), 82))
     m = hv.HybridViT(**cfg.as_kwargs(), precision="bf16").cuda()
     m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
-    sd = O.make_state(shapes, W, requires_grad=False)
     with torch.no_grad():
         y = m.eval()(x.cuda()).cpu()
-        yo = O.forward(sd, x, cfg)
+        yo = O.forward(O.make_state(shapes, W, requires_grad=False), x, cfg)
     assert m.last_num_tokens == 496
     e_fwd = rel(y, yo)
-    sdg = O.make_state(shapes, W, requires_grad=True)
-    lo = O.combined_loss(O.forward(sdg, x, cfg, training=True), t)
-    lo.backward()
-    lg = hv.CombinedLoss()(m.train()(x.cuda()), t.cuda())
-    lg.backward()
+    sd = O.make_state(shapes, W, requires_grad=True)
+    lo_t = O.combined_loss(O.forward(sd, x, cfg, training=True), t)
+    lo_t.backward()
+    lo = lo_t.item()
+    sdg = {k: v.detach().cuda().requires_grad_(v.requires_grad) for k, v in sd.items()}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = O.forward(sdg, x.cuda(), cfg, training=True)
+    O.combined_loss(yb.float(), t.cuda()).backward()
+    loss = hv.CombinedLoss()(m.train()(x.cuda()), t.cuda())
+    loss.backward()
     torch.cuda.synchronize()
-    e_qkv = max(relnorm(blk.attn.qkv.weight.grad.cpu(), sdg[f"transformer.blocks.{i}.attn.qkv.weight"].grad)
-                for i, blk in enumerate(m.transformer.blocks))
-    print(f"N=496: fwd rel {e_fwd:.2e}, loss {lg.item():.6f} vs {lo.item():.6f}, worst qkv grad relnorm {e_qkv:.2e}")
+    worst, bad = {}, []
+    for k, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), k
+        got, ref, tb = p.grad.detach().cpu(), sd[k].grad, sdg[k].grad.detach().float().cpu()
+        if k == "pos_encoding.pos_embed":
+            got, ref, tb = got[:, :496], ref[:, :496], tb[:, :496]
+        e, et = relnorm(got, ref), relnorm(tb, ref)
+        grp = k.split(".")[0]
+        worst[grp] = max(worst.get(grp, (0.0, 0.0, "")), (e, et, k))
+        if e > 2 * et + 1e-2:
+            bad.append((k, round(e, 4), round(et, 4)))
+    print(f"N=496: fwd rel {e_fwd:.2e}, loss {loss.item():.6f} vs {lo:.6f}; worst rel-L2 per group (ours, autocast):",
+          {g: f"{v[0]:.2e} / {v[1]:.2e} ({v[2]})" for g, v in worst.items()})
     assert e_fwd < BF16_TOL
-    assert abs(lg.item() - lo.item()) < 2e-2 * abs(lo.item())
-    assert e_qkv < 5e-2
+    assert abs(loss.item() - lo) < 2e-2 * abs(lo)
+    assert not bad, bad
 
 
 def test_inference_fusions_match_training_graph_path(hv):
