@@ -162,6 +162,14 @@ int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K
  * side (nullable): an earlier launch's slabs, summed by this launch. */
 int hvit_linear_wgrad_defer(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* ws,
                             long long ws_elems, const hvit_slab_sum_t* side, hvit_slab_sum_t* job, void* stream);
+/* The same with the bias gradient db = colsum(dy) (db == dw + N*K, or NULL) of
+ * a biased Linear (the head, hybrid_vit.py:153, and the skip projections,
+ * :158-165): the tall-skinny kernel defers its [dw | db] slabs as one job;
+ * the other paths defer dw's (when split) and write db now.  dw and db are
+ * final once job (if job->n > 0) has been carried. */
+int hvit_linear_wgrad_bias_defer(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
+                                 float* ws, long long ws_elems, const hvit_slab_sum_t* side, hvit_slab_sum_t* job,
+                                 void* stream);
 int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream);
 
 /* ---- Convolution as implicit GEMM (ConvBlock conv components.py:55-62,

@@ -88,6 +88,8 @@ _SIGS = {
     "hvit_linear_wgrad": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp], i32),
     "hvit_wgrad_tickets": ([i32, i32, i32], i64),
     "hvit_linear_wgrad_defer": ([i32, vp, vp, i32, i32, i32, vp, vp, i64, P(SlabSum), P(SlabSum), vp], i32),
+    "hvit_linear_wgrad_bias_defer": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, P(SlabSum), P(SlabSum), vp],
+                                     i32),
     "hvit_mhsa_bias_rows": ([i32, i32, i32, i32, i32], i64),
     "hvit_sum_slabs_strided": ([vp, i32, i64, i64, vp, vp], i32),
     "hvit_linear_wgrad_tk": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp, i64, i32, vp], i32),

@@ -212,3 +212,20 @@ struct FastDiv {
     return (int)(hi >> s);
   }
 };
+
+// A slab sum's per-granule form for many slabs (epi_side in gemm.h and
+// sum_slabs_wave_kernel: one order for both): granule i (4 floats) of
+// sum_k src[k * st + i] by one wave -- slabs k = lane, lane + 64, ... per lane,
+// then a butterfly.  Result in every lane.
+constexpr int SIDE_WAVE_SPLITS = 64;
+__device__ __forceinline__ f32x4 side_wave_granule(const f32x4* src, long st, int splits, long i) {
+  const int lane = threadIdx.x & 63;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int k = lane; k < splits; k += 64) s += src[(long)k * st + i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] += __shfl_xor(s[e], o, 64);
+  }
+  return s;
+}

@@ -627,10 +627,28 @@ __global__ void sum_slabs_strided_kernel(const float* ws, int splits, long strid
   }
 }
 
+// the many-slab form: a granule per wave (side_wave_granule)
+__global__ __launch_bounds__(256) void sum_slabs_wave_kernel(const float* ws, int splits, long stride4, long n4,
+                                                             float* out) {
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n4) return;  // (whole waves)
+  const f32x4 s = side_wave_granule((const f32x4*)ws, stride4, splits, i);
+  if ((threadIdx.x & 63) == 0) ((f32x4*)out)[i] = s;
+}
+
+// A deferred slab-sum job run as a launch of its own: the same summation order
+// as the epilogue side job that would otherwise carry it (gemm.h epi_side: a
+// wave per granule from SIDE_WAVE_SPLITS slabs, else even | odd pairs)
 int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream) {
-  if (stride == n) return hvit_sum_slabs(ws, splits, n, out, stream);
   HVIT_CHECK(ws && out && splits > 0 && stride >= n, "hvit_sum_slabs_strided: bad args");
   if (n <= 0) return HVIT_OK;
+  if (splits >= SIDE_WAVE_SPLITS && n % 4 == 0 && stride % 4 == 0 && ((uintptr_t)ws & 15) == 0 &&
+      ((uintptr_t)out & 15) == 0) {
+    hipLaunchKernelGGL(sum_slabs_wave_kernel, dim3((unsigned)cdiv(n / 4, 4)), dim3(256), 0, (hipStream_t)stream, ws,
+                       splits, (long)(stride / 4), (long)(n / 4), out);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   hipLaunchKernelGGL(sum_slabs_strided_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, splits,
                      (long)stride, (long)n, out);
   HVIT_LAUNCH_CHECK();

@@ -415,14 +415,18 @@ struct Epi {
 // overlaps a co-resident workgroup's K loop); the ring kernels after issuing
 // their DMA prologue (one workgroup per CU: the latency overlaps the first
 // stages' flight).  Any in-flight stores only make a later counted vmcnt wait
-// stricter.  Two forms, both a fixed summation order (deterministic):
-//  * many granules (split-K weight-gradient slabs: ~10^5 granules, 4-32 slabs):
-//    a granule per thread, even | odd slabs paired as sum_slabs_strided_kernel
-//    (bit-identical to that launch), eight slabs' loads in flight per step;
-//  * at most one granule per wave (partial column-sum rows: ~500 granules x
-//    128 slabs): a granule per wave, its slabs over the lanes, then a
-//    butterfly.  (One thread walking 128 slabs held its workgroup ~20 us past
-//    the others: round 4, the fc1 weight gradient carrying the fc1 bias rows.)
+// stricter.  Two forms by the job's slab count alone -- so the order is the
+// job's, whatever launch carries it, and hvit_sum_slabs_strided (the job run
+// as a launch of its own: side stream, M = 0 carriers) is bit-identical:
+//  * fewer than SIDE_WAVE_SPLITS slabs (split-K weight-gradient slabs: ~10^5
+//    granules, 4-32 slabs): a granule per thread, even | odd slabs paired as
+//    sum_slabs_strided_kernel, eight slabs' loads in flight per step;
+//  * SIDE_WAVE_SPLITS or more (partial column-sum rows, the tall-skinny weight
+//    gradients' slabs: 10^2-10^3 granules x 128-512 slabs): a granule per wave,
+//    its slabs over the lanes, then a butterfly, as sum_slabs_wave_kernel.  (One
+//    thread walking 128 slabs held its workgroup ~20 us past the others: round
+//    4, the fc1 weight gradient carrying the fc1 bias rows.)
+// (SIDE_WAVE_SPLITS, side_wave_granule: common.h)
 __device__ __forceinline__ void epi_side(const Epi& ep) {
   if (!ep.sj_n4) return;
   const long nwg = (long)gridDim.x * gridDim.y * gridDim.z;
@@ -431,18 +435,11 @@ __device__ __forceinline__ void epi_side(const Epi& ep) {
   f32x4* dst = (f32x4*)ep.sj_dst;
   const long st = ep.sj_stride4;
   const int wpb = blockDim.x >> 6;
-  if (ep.sj_n4 <= nwg * wpb) {
-    const int lane = threadIdx.x & 63;
-    const long i = b * wpb + (threadIdx.x >> 6);
-    if (i >= ep.sj_n4) return;
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int k = lane; k < ep.sj_splits; k += 64) s += src[(long)k * st + i];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] += __shfl_xor(s[e], o, 64);
+  if (ep.sj_splits >= SIDE_WAVE_SPLITS) {
+    for (long i = b * wpb + (threadIdx.x >> 6); i < ep.sj_n4; i += nwg * wpb) {
+      const f32x4 s = side_wave_granule(src, st, ep.sj_splits, i);
+      if ((threadIdx.x & 63) == 0) dst[i] = s;
     }
-    if (lane == 0) dst[i] = s;
     return;
   }
   const long nthr = nwg * blockDim.x;

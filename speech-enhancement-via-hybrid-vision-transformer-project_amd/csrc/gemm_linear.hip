@@ -52,7 +52,8 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
 bool hvit_wgrad_small_ok(int dt, int M, int N, int K);  // wgrad_small.hip
 long long hvit_wgrad_small_ws(int M, int N, int K);
 int hvit_wgrad_small(const void* dy, const void* x, int M, int N, int K, float* dw, float* db, float* ws,
-                     long long ws_elems, void* stream);
+                     long long ws_elems, void* stream,
+                     hvit_slab_sum_t* job = nullptr);
 
 extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
   // dw is [N_out x K_in] reduced over M rows; slabs only when splitting, each
@@ -98,6 +99,17 @@ extern "C" int hvit_linear_wgrad_defer(int dt, const void* dy, const void* x, in
   HVIT_CHECK(job, "hvit_linear_wgrad_defer: null job");
   *job = hvit_slab_sum_t{nullptr, nullptr, 0, 0, 0};
   return linear_wgrad_impl(dt, dy, x, M, N, K, dw, nullptr, ws, ws_elems, nullptr, 0, 0, stream, job, side);
+}
+
+// hvit_linear_wgrad_defer with the bias gradient: db == dw + N*K (or NULL);
+// the tall-skinny path defers [dw | db] as one job, the others defer dw (when
+// split) and finish db now
+extern "C" int hvit_linear_wgrad_bias_defer(int dt, const void* dy, const void* x, int M, int N, int K, float* dw,
+                                            float* db, float* ws, long long ws_elems, const hvit_slab_sum_t* side,
+                                            hvit_slab_sum_t* job, void* stream) {
+  HVIT_CHECK(job, "hvit_linear_wgrad_bias_defer: null job");
+  *job = hvit_slab_sum_t{nullptr, nullptr, 0, 0, 0};
+  return linear_wgrad_impl(dt, dy, x, M, N, K, dw, db, ws, ws_elems, nullptr, 0, 0, stream, job, side);
 }
 
 // the split-K slab sum: deferred into *job when the caller asked, else launched
@@ -149,7 +161,7 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
   if (small_on && !tickets && hvit_wgrad_small_ok(dt, M, N, K) && (!db || db == dw + NK) &&
       ws_elems >= hvit_wgrad_small_ws(M, N, K)) {
     if (int rc = side_alone()) return rc;
-    return hvit_wgrad_small(dy, x, M, N, K, dw, db, ws, ws_elems, stream);
+    return hvit_wgrad_small(dy, x, M, N, K, dw, db, ws, ws_elems, stream, job);
   }
   // HVIT_NO_RS=1: bias grad by a separate column reduction (A/B measurements only)
   static const bool no_rs = getenv("HVIT_NO_RS") && atoi(getenv("HVIT_NO_RS"));

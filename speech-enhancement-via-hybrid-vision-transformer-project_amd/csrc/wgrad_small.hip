@@ -158,7 +158,7 @@ int hvit_sum_slabs(const float* ws, int splits, long long n, float* out, void* s
 
 // dw [N][K] (and db [N] when db == dw + N*K, or NULL) from the slab reduction
 int hvit_wgrad_small(const void* dy, const void* x, int M, int N, int K, float* dw, float* db, float* ws,
-                     long long ws_elems, void* stream) {
+                     long long ws_elems, void* stream, hvit_slab_sum_t* job) {
   int rows, splits;
   plan(M, N, K, rows, splits);
   HVIT_CHECK(ws && ws_elems >= (long long)splits * ((long long)N * K + N), "hvit_wgrad_small: workspace too small");
@@ -168,6 +168,12 @@ int hvit_wgrad_small(const void* dy, const void* x, int M, int N, int K, float* 
   hipLaunchKernelGGL(wgrad_small_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
                      (const bf16_t*)x, M, N, K, rows, db ? 1 : 0, ws);
   HVIT_LAUNCH_CHECK();
-  // db sits in each slab right after dW: one reduction covers [dW | db]
-  return hvit_sum_slabs(ws, splits, (long long)N * K + (db ? N : 0), dw, stream);
+  // db sits in each slab right after dW: one reduction covers [dW | db] -- or,
+  // with a job, the caller's next GEMM launch sums it (epilogue side job)
+  const long long n = (long long)N * K + (db ? N : 0);
+  if (job) {
+    *job = hvit_slab_sum_t{ws, dw, n, n, splits};
+    return HVIT_OK;
+  }
+  return hvit_sum_slabs(ws, splits, n, dw, stream);
 }

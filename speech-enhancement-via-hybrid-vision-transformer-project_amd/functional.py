@@ -370,15 +370,42 @@ def linear_wgrad(dt, dy, x, M, N, K, bias=False, tag="linear_wgrad", tickets=Non
     return (dw, db) if bias else dw
 
 
+def linear_wgrad_bias_deferred(dt, dy, x, M, N, K, tag="linear_wgrad", out=None):
+    """(dw, db, Deferred or None) of a biased Linear: the tall-skinny kernel's
+    [dw | db] slab sum is left to the next linear launch on this stream (pass
+    the Deferred as its epilogue side job; dw and db are final once it ran)."""
+    if not DEFER:
+        dw, db = linear_wgrad(dt, dy, x, M, N, K, bias=True, out=out)
+        return dw, db, None
+    buf = out if out is not None else torch.empty(N * K + N, dtype=torch.float32, device=dy.device)
+    dw, db = buf[:N * K].view(N, K), buf[N * K:]
+    ws_n = L.lib().hvit_wgrad_workspace(M, N, K)
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dy.device)
+    job = L.SlabSum()
+
+    def launch():
+        call("hvit_linear_wgrad_bias_defer", dt, dy.data_ptr(), x.data_ptr(), M, N, K, dw.data_ptr(), db.data_ptr(),
+             ws.data_ptr(), ws_n, None, C.byref(job), stream_ptr())
+
+    with timed(tag, 2.0 * M * N * K):
+        launch()
+    _record(tag, (launch, 2.0 * M * N * K))  # (the isolated replay times the GEMM alone)
+    return dw, db, (Deferred(job, ws) if job.n > 0 else None)
+
+
 def _linear_wgrad_bias_maybe_side(ctx, dt, dy, x, M, N, K):
-    """(dw, db) of a biased Linear (head / skip projections) on the side stream
-    when side_ok, else on the backward's stream."""
+    """(dw, db, Deferred or None) of a biased Linear (head / skip projections):
+    on the side stream when side_ok (complete there), else on the backward's
+    stream with the slab sum deferred to the data-gradient launch after it."""
     if not side_ok(ctx.prefs):
-        return linear_wgrad(dt, dy, x, M, N, K, bias=True)
+        return linear_wgrad_bias_deferred(dt, dy, x, M, N, K)
     buf = torch.empty(N * K + N, dtype=torch.float32, device=dy.device)
     with on_side(dy.device, (dy, x, buf)):
-        linear_wgrad(dt, dy, x, M, N, K, bias=True, out=buf)
-    return buf[:N * K].view(N, K), buf[N * K:]
+        # the same launches, the slab sum as one of its own (the carried job's order)
+        dw, db, j = linear_wgrad_bias_deferred(dt, dy, x, M, N, K, out=buf)
+        if j is not None:
+            call("hvit_sum_slabs_strided", j.job.src, j.job.splits, j.job.stride, j.job.n, j.job.dst, stream_ptr())
+    return dw, db, None
 
 
 def dropout_scale(g, M, N, drop, rowscale, rps, out, colsum=None):
@@ -1309,10 +1336,10 @@ class HeadFn(torch.autograd.Function):
         B, Nt, D, C, dt = ctx.meta
         M = B * Nt
         dy = cast(dy, dt)
-        dw, db = _linear_wgrad_bias_maybe_side(ctx, dt, dy, xn, M, C, D)
+        dw, db, jw = _linear_wgrad_bias_maybe_side(ctx, dt, dy, xn, M, C, D)
         dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
-        call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32, None,
-             stream_ptr())
+        call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32,
+             epilogue(side=jw) if jw is not None else None, stream_ptr())  # (carries the wgrad's slab sum)
         if ctx.ho is not None and ctx.ho.drop is not None:  # the last block's fc2 dropout, fused
             dx, dnw, dnb = ctx.ho.fuse(dxn, x2d, m, r, nw, None, ctx.zs)
         else:
@@ -1355,12 +1382,15 @@ class SkipFn(torch.autograd.Function):
         dev = r.device
         s = stream_ptr()
         dy = cast(dy, dt)
-        dw, db = _linear_wgrad_bias_maybe_side(ctx, dt, dy, r, M, Cd, Ce)
+        dw, db, jw = _linear_wgrad_bias_maybe_side(ctx, dt, dy, r, M, Cd, Ce)
         dw = dw.view(wshape)
         de = None
+        if jw is not None and not ctx.needs_input_grad[0]:  # no launch follows to carry the slab sum
+            call("hvit_sum_slabs_strided", jw.job.src, jw.job.splits, jw.job.stride, jw.job.n, jw.job.dst, s)
         if ctx.needs_input_grad[0]:
             dr = _empty((N, Ho, Wo, Ce), dt, dev)
-            call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, Cd, Ce, dr.data_ptr(), dt, None, s)
+            call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, Cd, Ce, dr.data_ptr(), dt,
+                 epilogue(side=jw) if jw is not None else None, s)  # (carries the wgrad's slab sum)
             if ctx.sg is not None and ctx.sg.offer(dr, (N, Ho, Wo, Ce, He, We, dt)):
                 return None, dw, db, None, None, None, None  # the encoder output's other consumer adds it
             if (He, We) != (Ho, Wo):

@@ -216,6 +216,37 @@ def test_linear_wgrad_deferred_side_job(env, cfg, N, K):
     assert torch.equal(dw1, want) and torch.equal(dw2, want)
 
 
+@pytest.mark.parametrize("M,N,K", [(8192, 256, 512), (32768, 128, 128), (131072, 64, 64), (1000, 64, 128)])
+def test_linear_wgrad_bias_deferred_side_job(env, M, N, K):
+    """hvit_linear_wgrad_bias_defer (the head and skip projections' weight and
+    bias gradients): the tall-skinny kernel's [dw | db] slabs summed by the next
+    data-gradient launch's epilogue side job (HeadFn / SkipFn backward), and
+    that launch's own output unchanged; dw and db element-wise at the
+    accumulation-order bar (the slab sum's order differs from the two-launch
+    hvit_linear_wgrad's), and bit-identical to the same job run by
+    hvit_sum_slabs_strided (splits 4 / 32 / 128 / 512: both epi_side forms)."""
+    L, HF = env
+    torch.manual_seed(6)
+    dy, x = rb(M, N), rb(M, K)
+    g, w = rb(M, N), rb(N, K, scale=N ** -0.5)
+    out_ref = torch.empty(M, K, device=DEV, dtype=torch.float32)
+    L.call("hvit_linear_dgrad", L.BF16, g.data_ptr(), w.data_ptr(), M, N, K, out_ref.data_ptr(), L.F32, None, s())
+    dw, db, job = HF.linear_wgrad_bias_deferred(L.BF16, dy, x, M, N, K)
+    assert job is not None and job.job.n == N * K + N
+    out = torch.empty_like(out_ref)
+    L.call("hvit_linear_dgrad", L.BF16, g.data_ptr(), w.data_ptr(), M, N, K, out.data_ptr(), L.F32,
+           HF.epilogue(side=job), s())
+    # the job run as a launch of its own (side-stream form): the carried order, bit for bit
+    dw2, db2, job2 = HF.linear_wgrad_bias_deferred(L.BF16, dy, x, M, N, K)
+    j = job2.job
+    L.call("hvit_sum_slabs_strided", j.src, j.splits, j.stride, j.n, j.dst, s())
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_ref)
+    check_f32(dw, dy.float().t() @ x.float(), what=f"deferred small wgrad {M}x{N}x{K}")
+    check_f32(db, dy.float().sum(0), what=f"deferred small wgrad bias {M}x{N}x{K}")
+    assert torch.equal(dw2, dw) and torch.equal(db2, db)
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 256, 512), (8192, 256, 256), (32768, 128, 128), (131072, 64, 64),
                                    (1000, 64, 128)])
 def test_linear_wgrad_small_with_bias_exact(env, M, N, K):
