@@ -149,7 +149,9 @@ int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, in
  * gemm_ring.h); what 1 = the fused first block's matrix-core kernels (1 on, 0:
  * the VALU kernels); what 2 = workgroup target of the linear weight gradients'
  * split-K choice for the calls that follow (0: default 256; also sizes
- * hvit_wgrad_workspace).  Returns the previous value (-1 for an unknown knob). */
+ * hvit_wgrad_workspace); what 3 = the persistent epilogue-overlapped kernels of the
+ * K = 512 linears (gemm_pp.hip: -1 automatic, 0 off, 1 = 256x128 tiles, 2 =
+ * 128x128 tiles).  Returns the previous value (-1 for an unknown knob). */
 int hvit_gemm_tune(int what, int value);
 /* dw[N,K] = dy^T x; db[N] = colsum(dy) (nullable; fused when db == dw + N*K) */
 int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
@@ -223,9 +225,12 @@ int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void* dout, cons
 /* The same with the attention-dropout decisions kept: the forward writes one
  * bit per (query, key) to keep_bits (hvit_mhsa_keep_bits_elems(B, N, H) 32-bit
  * words, 16-byte aligned) and the backward reads them instead of regenerating
- * the mask (bf16, head_dim 64, N <= 256, N % 4 == 0; other shapes and p = 0
- * ignore keep_bits).  Results equal hvit_mhsa_fwd / hvit_mhsa_bwd. */
+ * the mask (bf16, head_dim 64, N <= 512, N % 4 == 0; other shapes and p = 0
+ * ignore keep_bits).  Results equal hvit_mhsa_fwd / hvit_mhsa_bwd.
+ * hvit_mhsa_keep_bits_used: 1 when the (dt, N, hd) kernels use keep bits (the
+ * caller allocates none otherwise). */
 long long hvit_mhsa_keep_bits_elems(int B, int N, int H);
+int hvit_mhsa_keep_bits_used(int dt, int N, int hd);
 int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float scale, const hvit_dropout_t* dropout,
                      void* o, float* lse, unsigned* keep_bits, void* stream);
 int hvit_mhsa_bwd_kb(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N, int H,
@@ -423,6 +428,13 @@ int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_norm, float*
 int hvit_scale_tensors(int count, const hvit_tensor_t* tensors, const float* coef, void* stream);
 int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp, const float* coef,
                void* stream);
+/* hvit_adamw with the hyper-parameters read on the device when hyper_dev (f32[5]
+ * = lr, beta1, beta2, eps, weight_decay) is non-NULL: a captured optimizer step
+ * (hipGraph) then replays the values the caller last wrote there (an LR
+ * scheduler's), not the ones of capture time; hp's bc1 / bc2 still serve items
+ * without a device step counter. */
+int hvit_adamw_dev(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp, const float* coef,
+                   const float* hyper_dev, void* stream);
 /* Device-resident training counters, advanced on the stream (so a captured train
  * step, hipGraph, replays with fresh values): hvit_rng_advance steps the dropout
  * state {base, counter} and writes the next forward's seed to *seed_out (what

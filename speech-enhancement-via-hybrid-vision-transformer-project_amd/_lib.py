@@ -106,6 +106,7 @@ _SIGS = {
     "hvit_mhsa_fwd_fp8_kb": ([vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_bwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp], i32),
     "hvit_mhsa_keep_bits_elems": ([i32, i32, i32], i64),
+    "hvit_mhsa_keep_bits_used": ([i32, i32, i32], i32),
     "hvit_mhsa_fwd_kb": ([i32, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_bwd_kb": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp], i32),
     "hvit_mhsa_bwd_db": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, P(Dropout), vp, vp, vp, vp, vp], i32),
@@ -146,6 +147,7 @@ _SIGS = {
     "hvit_clip_coef": ([i32, P(TensorRef), f32, vp, i64, vp, vp], i32),
     "hvit_scale_tensors": ([i32, P(TensorRef), vp, vp], i32),
     "hvit_adamw": ([i32, P(AdamWItem), P(AdamWHyper), vp, vp], i32),
+    "hvit_adamw_dev": ([i32, P(AdamWItem), P(AdamWHyper), vp, vp, vp], i32),
     "hvit_rng_advance": ([vp, vp, vp], i32),
     "hvit_gemm_tune": ([i32, i32], i32),
     "hvit_step_bump": ([vp, i32, f32, vp], i32),

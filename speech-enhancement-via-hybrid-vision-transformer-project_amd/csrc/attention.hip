@@ -1210,6 +1210,9 @@ extern "C" int hvit_mhsa_bwd(int dt, const void* qkv, const void* o, const void*
 extern "C" long long hvit_mhsa_keep_bits_elems(int B, int N, int H) {
   return (B > 0 && N > 0 && H > 0) ? (long long)B * H * N * 8 * cdiv(N, 256) : 0;
 }
+// 1 when the kernels for (dt, N, hd) store / read keep bits (else a keep-bit
+// buffer would be allocated for nothing: callers skip it)
+extern "C" int hvit_mhsa_keep_bits_used(int dt, int N, int hd) { return v2_ok(dt, hd, N) ? 1 : 0; }
 
 extern "C" int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
                                 const hvit_dropout_t* dropout, void* o, float* lse, unsigned* keep_bits,

@@ -2,6 +2,11 @@
 #include "gemm_host.h"
 #include "gemm_ring.h"
 
+// persistent epilogue-overlapped kernels (gemm_pp.hip)
+bool hvit_pp_fwd(const void* x, const void* w, int M, int N, int K, const hvit::Epi& ep, hipStream_t st, int* rc);
+bool hvit_pp_dgrad(const void* dy, const void* w, int M, int N, int K, const hvit::Epi& ep, hipStream_t st, int* rc);
+int hvit_pp_tune(int value);
+
 extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int M, int N, int K,
                                void* y, int y_dt, const hvit_epilogue_t* epi, void* stream) {
   HVIT_CHECK(x && w && y, "hvit_linear_fwd: null pointer");
@@ -15,6 +20,7 @@ extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float
   if (M == 0) return HVIT_OK;
   if (dt == HVIT_BF16) {
     int rc = 0;
+    if (hvit_pp_fwd(x, w, M, N, K, ep, (hipStream_t)stream, &rc)) return rc;
     if (try_ring(dense<bf16_t, true>(x, K, M, K), dense<bf16_t, true>(w, K, N, K), M, N, K, 1, ep,
                  (hipStream_t)stream, &rc))
       return rc;
@@ -38,6 +44,7 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
   if (M == 0) return HVIT_OK;
   if (dt == HVIT_BF16 && N % 8 == 0) {
     int rc = 0;
+    if (hvit_pp_dgrad(dy, w, M, N, K, ep, (hipStream_t)stream, &rc)) return rc;
     if (try_ring(dense<bf16_t, true>(dy, N, M, N), dense<bf16_t, false>(w, K, K, N), M, K, N, 1, ep,
                  (hipStream_t)stream, &rc))
       return rc;
@@ -242,6 +249,7 @@ int hvit_c1_tune(int value);  // c1block.hip
 
 extern "C" int hvit_gemm_tune(int what, int value) {
   if (what == 1) return hvit_c1_tune(value);
+  if (what == 3) return hvit_pp_tune(value);  // persistent kernels: -1 auto, 0 off, 1 / 2 forced tile
   if (what == 2) {  // workgroup target of the linear weight gradients' split-K (0: default)
     const int old = (int)wg_target;
     wg_target = value > 0 ? value : 0;

@@ -299,8 +299,16 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 // iteration left the kernel at ~4.2 TB/s).  Per-element arithmetic unchanged.
 constexpr int AD_UPT = 2, AD_TILE = 256 * AD_UPT;
 
-__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a, AdamHyper h0, const float* __restrict__ coef) {
+__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a, AdamHyper h0, const float* __restrict__ coef,
+                                                    const float* __restrict__ hdev) {
   const float c = coef ? coef[1] : 1.f;
+  if (hdev) {  // device hyper-parameters (a captured step replays the CURRENT lr / betas / eps / wd)
+    h0.lr = hdev[0];
+    h0.beta1 = hdev[1];
+    h0.beta2 = hdev[2];
+    h0.eps = hdev[3];
+    h0.wd = hdev[4];
+  }
   const long tiles = a.start[a.count];  // start[] holds tile prefix sums
   int j = 0, jh = -1;
   AdamHyper h = h0;
@@ -493,8 +501,16 @@ extern "C" int hvit_scale_tensors(int count, const hvit_tensor_t* tensors, const
   return HVIT_OK;
 }
 
+extern "C" int hvit_adamw_dev(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp,
+                              const float* coef, const float* hyper_dev, void* stream);
 extern "C" int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp,
                           const float* coef, void* stream) {
+  return hvit_adamw_dev(count, items, hp, coef, nullptr, stream);
+}
+
+extern "C" int hvit_adamw_dev(int count, const hvit_adamw_item_t* items, const hvit_adamw_hyper_t* hp,
+                              const float* coef, const float* hyper_dev, void* stream) {
+  HVIT_CHECK(!hyper_dev || ((uintptr_t)hyper_dev & 3) == 0, "hvit_adamw_dev: hyper_dev alignment");
   HVIT_CHECK(count >= 0 && (count == 0 || items) && hp, "hvit_adamw: bad args");
   bool host_bc = false;
   for (int k = 0; k < count; ++k) host_bc = host_bc || !items[k].step;
@@ -523,7 +539,7 @@ extern "C" int hvit_adamw(int count, const hvit_adamw_item_t* items, const hvit_
     }
     if (a.start[a.count] == 0) continue;
     hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)std::min<long>(a.start[a.count], 2048)), dim3(256), 0,
-                       (hipStream_t)stream, a, h, coef);
+                       (hipStream_t)stream, a, h, coef, hyper_dev);
     HVIT_LAUNCH_CHECK();
   }
   return HVIT_OK;

@@ -64,6 +64,22 @@ import torch.distributed as dist
 from . import functional as HF
 
 
+_GLOO_GROUPS: Dict[tuple, object] = {}
+
+
+def _gloo_group(group):
+    """A gloo group over ``group``'s ranks, created once per (default group,
+    ranks) and reused (set_rows() rebuilds the reducer).  Created with local
+    synchronization, so only the member ranks take part: a reducer built on a
+    subgroup by that subgroup's ranks alone does not wait for the others."""
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
+    key = (id(dist.group.WORLD), ranks)
+    g = _GLOO_GROUPS.get(key)
+    if g is None:
+        g = _GLOO_GROUPS[key] = dist.new_group(ranks=list(ranks), backend="gloo", use_local_synchronization=True)
+    return g
+
+
 class GradAllReducer:
     def __init__(self, model: torch.nn.Module, bucket_mb: float = 25.0, group=None,
                  sliced: Optional[Dict[str, int]] = None, broadcast_buffers: bool = True):
@@ -121,8 +137,7 @@ class GradAllReducer:
         self._agree = bool(self.sliced) and self.world > 1
         self._host_group = self.group
         if self._agree and dist.get_backend(self.group) != "gloo":
-            self._host_group = dist.new_group(ranks=dist.get_process_group_ranks(self.group)
-                                              if self.group is not None else None, backend="gloo")
+            self._host_group = _gloo_group(self.group)
         self.reset()
         self._publish()
 

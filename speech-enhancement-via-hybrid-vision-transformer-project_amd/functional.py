@@ -1118,13 +1118,14 @@ class ViTBlockFn(torch.autograd.Function):
             # the dropout decisions the fp8 forward kept (same keep-bit layout)
             if dt != BF16:
                 raise ValueError("hvit: the fp8 attention path runs inside the bf16 model (precision='bf16')")
-            if d_attn.p > 0 and KEEPBITS and Nt % 4 == 0:
+            if d_attn.p > 0 and KEEPBITS and L.lib().hvit_mhsa_keep_bits_used(dt, Nt, hd):
                 kbits = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, Nt, H), dtype=torch.int32, device=dev)
             with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
                 call("hvit_mhsa_fwd_fp8_kb", qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),
                      lse.data_ptr(), ptr(kbits), s)
-        elif probs is None and d_attn.p > 0 and KEEPBITS:
+        elif probs is None and d_attn.p > 0 and KEEPBITS and L.lib().hvit_mhsa_keep_bits_used(dt, Nt, hd):
             # the dropout decisions are kept (1 bit per score) so the backward does not re-hash them
+            # (only for the shapes whose kernels use them: the buffer grows as N^2)
             kbits = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, Nt, H), dtype=torch.int32, device=dev)
             with timed("attn_fwd", 4.0 * B * H * Nt * Nt * hd):
                 call("hvit_mhsa_fwd_kb", dt, qkv.data_ptr(), B, Nt, H, hd, scale, d_attn.c(), o.data_ptr(),

@@ -95,6 +95,36 @@ class FusedAdamW(torch.optim.Optimizer):
         # with the right step count; otherwise CPU counters as torch's default
         self.capturable = capturable
         self._step_bufs: Dict[int, torch.Tensor] = {}
+        # capturable: each group's [lr, beta1, beta2, eps, weight_decay] also live
+        # on the device and the kernel reads them there, so a captured step
+        # replays the values of the latest sync_hyper() (an LR scheduler's), not
+        # the ones it was captured with (GraphedTrainStep syncs before a replay)
+        self._hyper_bufs: Dict[int, torch.Tensor] = {}
+        self._hyper_vals: Dict[int, tuple] = {}
+
+    @staticmethod
+    def _hyper_of(group) -> tuple:
+        b1, b2 = group["betas"]
+        return (float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]))
+
+    def sync_hyper(self) -> None:
+        """Write every group's current hyper-parameters to its device buffer
+        (stream-ordered; only when they changed).  Not during stream capture:
+        a captured copy would replay the capture-time values."""
+        if not self.capturable or torch.cuda.is_current_stream_capturing():
+            return
+        for gi, group in enumerate(self.param_groups):
+            ps = [p for p in group["params"] if p.requires_grad]
+            if not ps or not ps[0].is_cuda:
+                continue
+            vals = self._hyper_of(group)
+            buf = self._hyper_bufs.get(gi)
+            if buf is None or buf.device != ps[0].device:
+                buf = self._hyper_bufs[gi] = torch.empty(5, dtype=torch.float32, device=ps[0].device)
+                self._hyper_vals.pop(gi, None)
+            if self._hyper_vals.get(gi) != vals:
+                buf.copy_(torch.tensor(vals, dtype=torch.float32).pin_memory(), non_blocking=True)
+                self._hyper_vals[gi] = vals
 
     def _device_steps(self, gi: int, ps: list) -> torch.Tensor:
         """The group's device step buffer, state["step"] of every parameter a
@@ -151,6 +181,8 @@ class FusedAdamW(torch.optim.Optimizer):
             coef = _clip_coef([p.grad for p in live], self.max_grad_norm)
             self.last_grad_norm = coef[0]
         stream = L.stream_ptr(live[0].device)
+        if self.capturable:
+            self.sync_hyper()
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             by_step: Dict[float, list] = {}
@@ -196,8 +228,12 @@ class FusedAdamW(torch.optim.Optimizer):
                 # read p, g, m, v f32, write p, m, v f32 (+ the bf16 shadow)
                 nbytes = (float(sum(p.numel() * (28 + (2 if HF.shadow_of(p) is not None else 0)) for p in ps))
                           if HF.OP_TIMES is not None else 0.0)
+                hbuf = self._hyper_bufs.get(gi) if self.capturable else None
+                if self.capturable and hbuf is None:
+                    raise RuntimeError("hvit FusedAdamW(capturable=True): run one eager step before capturing")
                 with HF.timed("adamw", nbytes):
-                    L.call("hvit_adamw", len(ps), items, hp, coef.data_ptr() if coef is not None else None, stream)
+                    L.call("hvit_adamw_dev", len(ps), items, hp, coef.data_ptr() if coef is not None else None,
+                           hbuf.data_ptr() if hbuf is not None else None, stream)
                 for p in ps:
                     if _bump is not None:
                         _bump(p)  # the kernel wrote p in place: keep version counters honest

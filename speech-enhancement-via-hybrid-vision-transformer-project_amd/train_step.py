@@ -20,7 +20,14 @@ shape (LRU-capped):
   counters on the device, so a replayed step equals the eager step it stands
   for (the train step is deterministic: bit for bit, tests/test_gpu_graph_cache.py);
 * each graph has its own memory pool; evicting the least recently used graph
-  (``max_graphs``) frees its pool.
+  (``max_graphs``) frees its pool;
+* the optimizer's hyper-parameters are read on the device
+  (``FusedAdamW.sync_hyper`` before every call), so a replay uses the current
+  learning rate of an LR scheduler (trainer.py:304-309), not the captured one;
+* under data parallelism with a sliced ``GradAllReducer`` (whose eager steps
+  agree the token bound over a gloo group), every call first agrees over that
+  group whether any rank must run an eager step; then all ranks do, so no rank
+  waits in a host collective that a replaying rank never enters.
 
 ``step(noisy, clean)`` returns the loss as a device tensor (the graph's static
 output for replays: read it before the next call with the same shape).
@@ -60,6 +67,7 @@ class GraphedTrainStep:
         self.cache: "OrderedDict[tuple, _Entry]" = OrderedDict()
         self.captures = 0
         self.replays = 0
+        self.eager_steps = 0
         self._side: Optional[torch.cuda.Stream] = None
 
     def _eager(self, x, t):
@@ -75,6 +83,22 @@ class GraphedTrainStep:
     def _key(x, t):
         return (tuple(x.shape), x.dtype, tuple(t.shape), t.dtype, x.device)
 
+    def _every_rank(self, flag: bool) -> bool:
+        """True when ``flag`` holds on every rank of the reducer's group.  Only
+        a reducer whose ``finish()`` runs a host (gloo) agreement in eager steps
+        needs this: if one rank ran such an eager step while another replayed a
+        graph (which runs no host collective), the eager rank would wait forever.
+        So every call agrees first -- one gloo all-reduce of a flag, outside any
+        graph -- and all ranks run eager when any of them must."""
+        r = self.reducer
+        if r is None or not getattr(r, "_agree", False):
+            return flag
+        import torch.distributed as dist
+
+        t = torch.tensor([1 if flag else 0], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=r._host_group)
+        return bool(t[0])
+
     def __call__(self, noisy: torch.Tensor, clean: torch.Tensor) -> torch.Tensor:
         key = self._key(noisy, clean)
         e = self.cache.get(key)
@@ -83,16 +107,25 @@ class GraphedTrainStep:
             while len(self.cache) > self.max_graphs:
                 self.cache.popitem(last=False)  # the graph and its pool go with the entry
         self.cache.move_to_end(key)
-        if e.graph is not None:
+        # the optimizer's device hyper-parameters follow param_groups (an LR
+        # scheduler may have changed them since the graph was captured)
+        sync = getattr(self.opt, "sync_hyper", None)
+        if sync is not None:
+            sync()
+        mode = "replay" if e.graph is not None else ("eager" if e.seen < self.warmup else "capture")
+        if not self._every_rank(mode != "eager"):
+            mode = "eager"
+        if mode == "replay":
             e.x.copy_(noisy)
             e.t.copy_(clean)
             e.graph.replay()
             self.replays += 1
             return e.loss
-        if e.seen < self.warmup:
+        if mode == "eager":
             # eager steps of a new shape (on a side stream, as capture warm-ups must be,
             # so the allocations they leave are not tied to the capture stream)
-            e.seen += 1
+            if e.graph is None:
+                e.seen += 1
             if self._side is None:
                 self._side = torch.cuda.Stream(device=noisy.device)
             side = self._side
@@ -100,6 +133,7 @@ class GraphedTrainStep:
             with torch.cuda.stream(side):
                 loss = self._eager(noisy, clean)
             torch.cuda.current_stream(noisy.device).wait_stream(side)
+            self.eager_steps += 1
             return loss
         # capture (executes nothing), then replay it as this call's step
         e.x = noisy.detach().clone()

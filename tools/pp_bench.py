@@ -1,0 +1,175 @@
+"""A/B of the persistent epilogue-overlapped GEMM (csrc/gemm_pp.hip) against the
+ring / gemm.h kernels on the B=32 ViT shapes it serves: qkv forward (+bias),
+fc1 forward (+bias, GELU, dropout: stores gelu'(h) and a), fc2 data gradient
+(dropout x gelu'(h) backward, fc1 bias-grad column sums, a carried split-K
+slab-sum side job).  hvit_gemm_tune(3, mode): 0 = the previous kernels, 1 =
+256x128 tiles (8 waves), 2 = 128x128 (4 waves, two workgroups per CU).
+
+Every mode's outputs are compared with mode 0's (same bf16 operands: the
+accumulation order is the same k order, so they should agree bit for bit) and
+with a torch fp32 reference of the same op; HIP-event timing with the modes
+interleaved round by round in one process.
+
+    python tools/pp_bench.py [modes=0,1,2] [rounds=5] [M=8192]
+"""
+
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import hvit_amd_loader  # noqa: E402
+
+hv = hvit_amd_loader.load()
+L = hv._lib
+HF = sys.modules["hvit_amd.functional"]
+DEV = "cuda"
+BF = torch.bfloat16
+KEEP = []
+
+
+def s():
+    return L.stream_ptr()
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def r(*shape, scale=0.5):
+    t = (torch.randn(*shape, device=DEV) * scale).to(BF)
+    KEEP.append(t)
+    return t
+
+
+def gelu_ref(h):
+    return 0.5 * h * (1.0 + torch.erf(h * 0.7071067811865476))
+
+
+def gelu_grad_ref(h):
+    cdf = 0.5 * (1.0 + torch.erf(h * 0.7071067811865476))
+    return cdf + h * 0.3989422804014327 * torch.exp(-0.5 * h * h)
+
+
+def cases(M, D=512, HID=2048):
+    out = []
+    # qkv forward: y = x W^T + b (bf16)
+    x, wq, bq = r(M, D), r(3 * D, D, scale=0.05), torch.randn(3 * D, device=DEV)
+    KEEP.append(bq)
+    yq = torch.empty(M, 3 * D, device=DEV, dtype=BF)
+
+    def ref_q():
+        return [(x.float() @ wq.float().t() + bq)]
+    out.append(("fwd qkv", 2 * M * 3 * D * D,
+                lambda: L.call("hvit_linear_fwd", L.BF16, x.data_ptr(), wq.data_ptr(), bq.data_ptr(), M, 3 * D, D,
+                               yq.data_ptr(), L.BF16, None, s()), [yq], ref_q))
+    # fc1 forward: gelu'(h) and a = dropout(gelu(h)) (no dropout in the torch check: p = 0 variant below)
+    w1, b1 = r(HID, D, scale=0.05), torch.randn(HID, device=DEV) * 0.5
+    KEEP.append(b1)
+    gh = torch.empty(M, HID, device=DEV, dtype=BF)
+    a = torch.empty(M, HID, device=DEV, dtype=BF)
+    ep_1 = HF.epilogue(act=L.ACT_GELU_DUAL_D, out2=a, drop=L.dropout(0.1, 78, 302))
+    out.append(("fwd fc1+gelu p.1", 2 * M * HID * D,
+                lambda: L.call("hvit_linear_fwd", L.BF16, x.data_ptr(), w1.data_ptr(), b1.data_ptr(), M, HID, D,
+                               gh.data_ptr(), L.BF16, ep_1, s()), [gh, a], None))
+    gh0 = torch.empty(M, HID, device=DEV, dtype=BF)
+    a0 = torch.empty(M, HID, device=DEV, dtype=BF)
+    ep_10 = HF.epilogue(act=L.ACT_GELU_DUAL_D, out2=a0)
+
+    def ref_1():
+        h = x.float() @ w1.float().t() + b1
+        return [gelu_grad_ref(h), gelu_ref(h)]
+    out.append(("fwd fc1+gelu p0", 2 * M * HID * D,
+                lambda: L.call("hvit_linear_fwd", L.BF16, x.data_ptr(), w1.data_ptr(), b1.data_ptr(), M, HID, D,
+                               gh0.data_ptr(), L.BF16, ep_10, s()), [gh0, a0], ref_1))
+    # fc2 data gradient: dh = (g2 W2) * keep * gelu'(h), colsum partial rows
+    g2, w2 = r(M, D), r(D, HID, scale=0.05)
+    dh = torch.empty(M, HID, device=DEV, dtype=BF)
+    cs = torch.zeros((M // 64, HID), device=DEV)
+    KEEP.extend([cs, gh, a, gh0])
+    ep_g = HF.epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=L.dropout(0.1, 78, 302), colsum=cs)
+    out.append(("dgrad fc2+geluB p.1", 2 * M * D * HID,
+                lambda: L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh.data_ptr(),
+                               L.BF16, ep_g, s()), [dh, cs], None))
+    dh0 = torch.empty(M, HID, device=DEV, dtype=BF)
+    cs0 = torch.zeros((M // 64, HID), device=DEV)
+    KEEP.extend([dh0, cs0])
+    ep_g0 = HF.epilogue(act=L.ACT_MUL_AUX, aux=gh0, colsum=cs0)
+
+    def ref_2():
+        d = (g2.float() @ w2.float()) * gh0.float()
+        return [d, d.view(M // 64, 64, HID).sum(1)]
+    out.append(("dgrad fc2+geluB p0", 2 * M * D * HID,
+                lambda: L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh0.data_ptr(),
+                               L.BF16, ep_g0, s()), [dh0, cs0], ref_2))
+    return out
+
+
+def rel(a_, b_):
+    d = (a_.float() - b_.float()).abs().max().item()
+    return d / (b_.float().abs().max().item() + 1e-12)
+
+
+def main():
+    args = dict(a.split("=") for a in sys.argv[1:])
+    modes = [int(c) for c in args.get("modes", "0,1,2").split(",")]
+    rounds = int(args.get("rounds", "5"))
+    M = int(args.get("M", "8192"))
+    cs = cases(M)
+    ref = {}
+    times = {(n, c): [] for n, *_ in cs for c in modes}
+    bad = 0
+    for rd in range(rounds):
+        for c in modes:
+            L.lib().hvit_gemm_tune(3, c)
+            for name, fl, fn, outs, tref in cs:
+                if rd == 0:
+                    for t in outs:
+                        t.fill_(float("nan")) if t.is_floating_point() else None
+                    fn()
+                    torch.cuda.synchronize()
+                    got = [t.clone() for t in outs]
+                    if c == modes[0]:
+                        ref[name] = got
+                    eq = [torch.equal(a_, b_) for a_, b_ in zip(got, ref[name])]
+                    e_mode = max(rel(a_, b_) for a_, b_ in zip(got, ref[name]))
+                    msg = f"check mode {c} {name:22s} vs mode {modes[0]}: bitwise {all(eq)} max|d|/max = {e_mode:.2e}"
+                    if tref is not None:
+                        rs = tref()
+                        e_t = max(rel(a_, b_) for a_, b_ in zip(got, rs))
+                        msg += f"   vs torch fp32: {e_t:.2e}"
+                        if e_t > 2e-2:
+                            bad += 1
+                    finite = all(torch.isfinite(t).all().item() for t in got)
+                    if not finite:
+                        msg += "   NON-FINITE"
+                        bad += 1
+                    print(msg, flush=True)
+                times[(name, c)].append(timeit(fn))
+    print()
+    hdr = "".join(f"   mode{c:d} us   TF/s" for c in modes)
+    print(f"{'gemm':22s}{hdr}")
+    for name, fl, *_ in cs:
+        row = ""
+        for c in modes:
+            t = sorted(times[(name, c)])[len(times[(name, c)]) // 2]
+            row += f"  {t:9.1f} {fl / t / 1e6:6.0f}"
+        print(f"{name:22s}{row}", flush=True)
+    L.lib().hvit_gemm_tune(3, -1)
+    if bad:
+        print(f"FAILED checks: {bad}")
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
