@@ -91,8 +91,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// rows per workgroup for the backward (4 waves x 4 rows)
-constexpr int LNB_ROWS = 16;
+// rows per workgroup for the backward: 4 waves x RPW rows, every row of a wave
+// in registers before any is reduced.  RPW = 4 (16 rows) up to D = 512; wider
+// rows take RPW = 2 (8 rows): at D = 768 four rows of x / dy / resid are 144
+// VGPRs, which left one wave per SIMD -- and at BASELINE config 5's M = 4096
+// only 256 workgroups, one per CU (17.6 % of HBM, round 4).
+__host__ __device__ constexpr int lnb_rpw(int D) { return D <= 512 ? 4 : 2; }
+static inline int lnb_rows(int D) { return 4 * lnb_rpw(D); }
 
 template <typename TD>
 __device__ __forceinline__ f32x4 load_row4(const TD* p) {
@@ -125,7 +130,7 @@ struct LnDrop {
 // dgamma/dbeta partials per workgroup: written to the slab ws[blk][2][D]
 // (SLAB; [blk][3][D] with DROP's column sums) and summed by a column
 // reduction, else added atomically.
-template <typename TD, int MAXV, bool SLAB, bool DROP = false>
+template <typename TD, int MAXV, bool SLAB, bool DROP = false, int RPW = 4>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, const float* __restrict__ x,
                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                                     const float* __restrict__ g, const float* __restrict__ resid,
@@ -151,8 +156,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
   }
   // all of the wave's rows are loaded before any is reduced: RPW rows x
   // (x, dy, resid) in flight per wave hide the HBM latency at this occupancy
-  constexpr int RPW = LNB_ROWS / 4;
-  const int row0 = blockIdx.x * LNB_ROWS + w * RPW;
+  const int row0 = blockIdx.x * (4 * RPW) + w * RPW;
   f32x4 xv[RPW][MAXV], dv[RPW][MAXV], rv[RPW][MAXV];
   float mu[RPW], rs[RPW], rsc[RPW];
 #pragma unroll
@@ -395,15 +399,18 @@ extern "C" int hvit_layernorm_fwd(const float* x, const float* gamma, const floa
   hipStream_t st = (hipStream_t)stream;
   dim3 g(cdiv(M, 4));
 #define LNF(TY, V) hipLaunchKernelGGL((ln_fwd_kernel<TY, V>), g, dim3(256), 0, st, x, gamma, beta, (TY*)y, mean, rstd, M, D, eps)
-  if (y_dt == HVIT_F32) { if (D <= 256) LNF(float, 1); else if (D <= 512) LNF(float, 2); else LNF(float, 4); }
-  else { if (D <= 256) LNF(bf16_t, 1); else if (D <= 512) LNF(bf16_t, 2); else LNF(bf16_t, 4); }
+  if (y_dt == HVIT_F32) {
+    if (D <= 256) LNF(float, 1); else if (D <= 512) LNF(float, 2); else if (D <= 768) LNF(float, 3); else LNF(float, 4);
+  } else {
+    if (D <= 256) LNF(bf16_t, 1); else if (D <= 512) LNF(bf16_t, 2); else if (D <= 768) LNF(bf16_t, 3); else LNF(bf16_t, 4);
+  }
 #undef LNF
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }
 
 extern "C" long long hvit_layernorm_bwd_ws_elems(int M, int D) {
-  return M > 0 ? (long long)cdiv(M, LNB_ROWS) * 2 * D : 0;
+  return M > 0 ? (long long)cdiv(M, lnb_rows(D)) * 2 * D : 0;
 }
 
 extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, const float* mean,
@@ -415,7 +422,7 @@ extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, con
   HVIT_CHECK(aligned16(x) && aligned16(dx) && aligned16(gamma) && aligned16(dy) && (!resid || aligned16(resid)),
              "hvit_layernorm_bwd: alignment");
   hipStream_t st = (hipStream_t)stream;
-  const int nblk = cdiv(M, LNB_ROWS);
+  const int nblk = cdiv(M, lnb_rows(D));
   const bool slab = M > 0 && ws && ws_elems >= hvit_layernorm_bwd_ws_elems(M, D);
   if (!slab && !(flags & HVIT_ACC_ZEROED)) {
     (void)hipMemsetAsync(dgamma, 0, sizeof(float) * D, st);
@@ -425,15 +432,19 @@ extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, con
   dim3 g(nblk);
 #define LNB(TD, V)                                                                                                \
   do {                                                                                                            \
+    constexpr int R_ = lnb_rpw(V * 256);                                                                          \
     if (slab)                                                                                                     \
-      hipLaunchKernelGGL((ln_bwd_kernel<TD, V, true>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma,  \
-                         resid, dx, dgamma, dbeta, ws, M, D);                                                     \
+      hipLaunchKernelGGL((ln_bwd_kernel<TD, V, true, false, R_>), g, dim3(256), 0, st, (const TD*)dy, x, mean,    \
+                         rstd, gamma, resid, dx, dgamma, dbeta, ws, M, D, LnDrop());                              \
     else                                                                                                          \
-      hipLaunchKernelGGL((ln_bwd_kernel<TD, V, false>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma, \
-                         resid, dx, dgamma, dbeta, ws, M, D);                                                     \
+      hipLaunchKernelGGL((ln_bwd_kernel<TD, V, false, false, R_>), g, dim3(256), 0, st, (const TD*)dy, x, mean,   \
+                         rstd, gamma, resid, dx, dgamma, dbeta, ws, M, D, LnDrop());                              \
   } while (0)
-  if (dy_dt == HVIT_F32) { if (D <= 256) LNB(float, 1); else if (D <= 512) LNB(float, 2); else LNB(float, 4); }
-  else { if (D <= 256) LNB(bf16_t, 1); else if (D <= 512) LNB(bf16_t, 2); else LNB(bf16_t, 4); }
+  if (dy_dt == HVIT_F32) {
+    if (D <= 256) LNB(float, 1); else if (D <= 512) LNB(float, 2); else if (D <= 768) LNB(float, 3); else LNB(float, 4);
+  } else {
+    if (D <= 256) LNB(bf16_t, 1); else if (D <= 512) LNB(bf16_t, 2); else if (D <= 768) LNB(bf16_t, 3); else LNB(bf16_t, 4);
+  }
 #undef LNB
   HVIT_LAUNCH_CHECK();
   if (slab) {
@@ -446,7 +457,7 @@ extern "C" int hvit_layernorm_bwd(const void* dy, int dy_dt, const float* x, con
 }
 
 extern "C" long long hvit_layernorm_bwd_drop_ws_elems(int M, int D) {
-  return M > 0 ? (long long)cdiv(M, LNB_ROWS) * 3 * D : 0;
+  return M > 0 ? (long long)cdiv(M, lnb_rows(D)) * 3 * D : 0;
 }
 
 // hvit_layernorm_bwd + the dropout / DropPath scaling of its output (see LnDrop)
@@ -465,7 +476,7 @@ extern "C" int hvit_layernorm_bwd_drop(const void* dy, int dy_dt, const float* x
   HVIT_CHECK(g_dt == HVIT_BF16 || g_dt == HVIT_F32, "hvit_layernorm_bwd_drop: g dtype");
   hipStream_t st = (hipStream_t)stream;
   if (M <= 0) return HVIT_OK;
-  const int nblk = cdiv(M, LNB_ROWS);
+  const int nblk = cdiv(M, lnb_rows(D));
   LnDrop d;
   d.thr = dropout ? drop_threshold(dropout->p) : 0;
   d.ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
@@ -476,11 +487,14 @@ extern "C" int hvit_layernorm_bwd_drop(const void* dy, int dy_dt, const float* x
   d.g = g_out;
   d.g_bf16 = g_dt == HVIT_BF16;
   dim3 g(nblk);
-#define LNBD(TD, V)                                                                                             \
-  hipLaunchKernelGGL((ln_bwd_kernel<TD, V, true, true>), g, dim3(256), 0, st, (const TD*)dy, x, mean, rstd, gamma, \
-                     resid, dx, acc3, acc3 + D, ws, M, D, d)
-  if (dy_dt == HVIT_F32) { if (D <= 256) LNBD(float, 1); else if (D <= 512) LNBD(float, 2); else LNBD(float, 4); }
-  else { if (D <= 256) LNBD(bf16_t, 1); else if (D <= 512) LNBD(bf16_t, 2); else LNBD(bf16_t, 4); }
+#define LNBD(TD, V)                                                                                              \
+  hipLaunchKernelGGL((ln_bwd_kernel<TD, V, true, true, lnb_rpw(V * 256)>), g, dim3(256), 0, st, (const TD*)dy, x,   \
+                     mean, rstd, gamma, resid, dx, acc3, acc3 + D, ws, M, D, d)
+  if (dy_dt == HVIT_F32) {
+    if (D <= 256) LNBD(float, 1); else if (D <= 512) LNBD(float, 2); else if (D <= 768) LNBD(float, 3); else LNBD(float, 4);
+  } else {
+    if (D <= 256) LNBD(bf16_t, 1); else if (D <= 512) LNBD(bf16_t, 2); else if (D <= 768) LNBD(bf16_t, 3); else LNBD(bf16_t, 4);
+  }
 #undef LNBD
   HVIT_LAUNCH_CHECK();
   if (flags & HVIT_ACC_DEFER) return HVIT_OK;  // the caller sums the partial rows (a later launch's side job)
