@@ -244,3 +244,66 @@ def test_grad_accumulation(mode):
     for rank, err, raised in out:
         assert err < 1e-6, (mode, rank, err)
         assert raised
+
+
+def _worker_subgroup(rank, world, port, q):
+    """A GradAllReducer on a subgroup, built by that subgroup's ranks only: its
+    host (gloo) group for the token-bound agreement is created with local
+    synchronization (a plain new_group would wait for the ranks outside it);
+    and GraphedTrainStep's per-call agreement takes the MIN of the ranks' flags."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import importlib
+        import types
+
+        import hvit_amd_loader
+
+        hvit_amd_loader.load()
+        dp = importlib.import_module("hvit_amd.dp")
+        ts = importlib.import_module("hvit_amd.train_step")
+        sub = dist.new_group([0, 1])  # (every rank takes part in creating the subgroup itself)
+        ok_sub = True
+        if rank < 2:
+            real = dist.get_backend
+            dist.get_backend = lambda g=None: "nccl"  # the reducer's data group as RCCL: it needs a gloo host group
+            try:
+                torch.manual_seed(3)
+                model = Toy()
+                red = dp.GradAllReducer(model, bucket_mb=0.0005, group=sub, sliced={"pos_embed": 16})
+                red2 = dp.GradAllReducer(model, bucket_mb=0.0005, group=sub, sliced={"pos_embed": 16})
+                ok_sub = red._host_group is red2._host_group and red._host_group is not sub
+            finally:
+                dist.get_backend = real
+            red2.remove()
+            model.zero_grad(set_to_none=True)
+            model(torch.randn(4, 12, 8) * (rank + 1)).backward()
+            red.finish()  # the token agreement runs on the locally created gloo group
+            ok_sub = ok_sub and model.fc1.weight.grad is not None
+            red.remove()
+        # GraphedTrainStep's path agreement (gloo MIN over the reducer's host group)
+        fake = types.SimpleNamespace(_agree=True, _host_group=None)
+        g = ts.GraphedTrainStep(None, None, types.SimpleNamespace(capturable=True), reducer=fake)
+        agree = (g._every_rank(rank != 1), g._every_rank(True), g._every_rank(False))
+        dist.barrier()
+        q.put((rank, ok_sub, agree))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_subgroup_host_group_and_path_agreement():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_subgroup, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_sub, agree in out:
+        assert ok_sub, rank
+        assert agree == (False, True, False), (rank, agree)
