@@ -166,6 +166,22 @@ def test_rccl_world1_dp_graph_matches_eager():
     assert out["exact"], out["rel"]
 
 
+def test_rccl_world1_graph_cache_matches_eager():
+    """Verdict r4 item 8: GraphedTrainStep WITH a GradAllReducer over RCCL (world
+    1) on three input shapes, bit-identical to an eager DP copy after every step
+    (tests/dp_graph_cache_worker.py)."""
+    import json
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dp_graph_cache_worker.py"), str(_free_port())],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["bad"] == [], out
+    assert out["dropout_state_equal"]
+    assert out["captures"] >= 4 and out["replays"] >= 6 and out["cached"] <= 2, out
+
+
 def _worker_accum(rank, world, port, q):
     """Two micro-batches per optimizer step with the hooks live on both and
     zero_grad(set_to_none=True) (trainer.py:164-183 under DP): the ViT and conv
