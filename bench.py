@@ -316,6 +316,12 @@ def main():
         # that poll during the capture invalidates it (hipErrorStreamCaptureUnsupported)
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             static_loss = step()
+        # keep the replays' loss buffer but not the captured autograd graph: its
+        # AccumulateGrad nodes (created on the capture stream) would otherwise stay
+        # alive and be reused by the eager repeats below on another stream (torch's
+        # "AccumulateGrad node's stream does not match" warning, and a cross-stream
+        # sync in those eager steps; the captured graph itself is unaffected)
+        static_loss = static_loss.detach()
 
         def step():
             graph.replay()

@@ -145,6 +145,10 @@ class GraphedTrainStep:
         # would count as an illegal call and abort on
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             e.loss = self._eager(e.x, e.t)
+        # the replays' loss buffer without the captured autograd graph (whose
+        # AccumulateGrad nodes would outlive the capture and meet later eager
+        # steps on another stream)
+        e.loss = e.loss.detach()
         e.graph = g
         self.captures += 1
         g.replay()
