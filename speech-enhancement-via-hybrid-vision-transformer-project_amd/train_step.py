@@ -77,7 +77,9 @@ class GraphedTrainStep:
             self.reducer.finish()
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
-        return loss
+        # the step is done: hand back the value only, so a caller holding it does not
+        # keep this step's AccumulateGrad nodes (side stream) alive into a capture
+        return loss.detach()
 
     @staticmethod
     def _key(x, t):

