@@ -1044,6 +1044,326 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_dkv_v2(const bf16_t* __restri
   }
 }
 
+// ----------------------------------------------------------------------------
+// Single-pass backward for N <= 256 (one 8-wave workgroup per (b, h)): P and
+// dP are formed once per score tile instead of once in the dQ kernel and again
+// in the dK/dV kernel, and Q, dO, K, V are staged once.
+//
+// Wave w owns keys 32w .. 32w+31 (their K and V rows in registers, dK and dV
+// accumulated in registers, the dK/dV kernel's S[q][key] form).  The queries
+// go by in pairs of 16-row tiles; at step s wave w takes pair (w + s) mod 8,
+// so in every step the 8 waves hold 8 different pairs.  dQ^T += K^T dS^T of
+// the wave's 32 keys then goes into the pair's f32 dQ rows in LDS
+// (read -> MFMA C operand -> write) without conflicts, a barrier hands the
+// rows to the next owner, and every dQ row takes its 8 contributions in the
+// fixed order w = p, p - 1, ... (mod 8): deterministic, no atomics.  dS^T for
+// that MFMA is the dK MFMA's dS transposed through a per-wave 2 KiB LDS image
+// (8-byte writes, ds_read_b64_tr_b16 reads), and K^T comes from a K image
+// staged once into the dQ rows' space before they are zeroed.
+//
+// LDS: Q and dO images 2 x 32 KiB, dQ rows 64 KiB (256 x 64 f32, 16-byte
+// chunks XOR-swizzled by row & 15), lse / delta 2 KiB, transposed keep bits
+// 8.5 KiB, dS^T images 8 x 2 KiB (also the bias column-sum scratch at the end).
+// ----------------------------------------------------------------------------
+constexpr int FB_WAVES = 8;
+constexpr int FB_KBP = 256 + 16;
+constexpr int FB_DS = 256 * V2_ROWB, FB_ACC = 2 * FB_DS, FB_LS = FB_ACC + 256 * 256, FB_DL = FB_LS + 1024,
+              FB_KB = FB_DL + 1024, FB_SCR = FB_KB + 8 * FB_KBP * 4, FB_SMEM = FB_SCR + FB_WAVES * 2048;
+static_assert(FB_SMEM <= 160 * 1024, "mhsa_bwd_fused: LDS");
+
+// f32 dQ row q, 16-byte chunk c (columns 4c .. 4c + 3)
+__device__ __forceinline__ int fb_acc(int q, int c) { return q * 256 + ((c ^ (q & 15)) << 4); }
+// dS^T image of one wave: [32 keys][32 queries] bf16, 64-byte rows, 8-byte
+// units XOR-swizzled by row & 7
+__device__ __forceinline__ int fb_scr(int row, int unit) { return row * 64 + ((unit ^ (row & 7)) << 3); }
+
+__global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int N, int H, float scale,
+    uint32_t thr, float dscale, DSeed seed_, uint32_t site, const uint32_t* __restrict__ kbits,
+    float* __restrict__ dbias) {
+  const unsigned long long seed = seed_;
+  __shared__ __attribute__((aligned(16))) char smem[FB_SMEM];
+  char* Qs = smem;
+  char* Ds = smem + FB_DS;
+  char* Acc = smem + FB_ACC;
+  float* Ls = (float*)(smem + FB_LS);
+  float* Dl = (float*)(smem + FB_DL);
+  uint32_t* Kb = (uint32_t*)(smem + FB_KB);
+  const int D = H * 64;
+  const long pitch = 3L * D;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+  char* Scr = smem + FB_SCR + w * 2048;
+  const V2Lane LN(lane);
+  const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
+  const bf16_t* dob = dout + (long)b * N * D + h * 64;
+  const int nqt = (N + 15) >> 4;
+  const int N32 = (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite copies)
+  const uint64_t bh = (uint64_t)b * H + h;
+  // Q, dO and (into the dQ rows' space) K images of all rows
+  v2_stage_glds<FB_WAVES>(Qs, base, pitch, N, N32);
+  v2_stage_glds<FB_WAVES>(Ds, dob, D, N, N32);
+  // this wave's keys (two 16-key tiles): K and V rows as MFMA B operands
+  u32x4 kf[2][2], vf[2][2];
+  bool kv[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = 32 * w + 16 * kt + frow;
+    kv[kt] = key < N;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      kf[kt][s2] = kv[kt] ? *(const u32x4*)(base + D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+      vf[kt][s2] =
+          kv[kt] ? *(const u32x4*)(base + 2 * D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+  // delta = rowsum(dO * O) (two threads per query), lse in log2 units
+  {
+    const int qd = threadIdx.x >> 1, hf = threadIdx.x & 1;
+    float dl = 0.f;
+    if (qd < N) {
+      const bf16_t* dp = dob + (long)qd * D + 32 * hf;
+      const bf16_t* op = o + ((long)b * N + qd) * D + h * 64 + 32 * hf;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const u32x4 x = *(const u32x4*)(dp + 8 * c), y = *(const u32x4*)(op + 8 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          dl += __uint_as_float(x[e] << 16) * __uint_as_float(y[e] << 16) +
+                __uint_as_float(x[e] & 0xffff0000u) * __uint_as_float(y[e] & 0xffff0000u);
+      }
+    }
+    dl += __shfl_xor(dl, 1, 64);
+    if (hf == 0) {
+      Dl[qd] = qd < N ? dl : 0.f;
+      Ls[qd] = qd < N ? lse[bh * N + qd] * 1.4426950408889634f : 0.f;
+      if (qd < N) delta[bh * N + qd] = dl;
+    }
+  }
+  // the forward's keep bits of this (b, h), transposed: Kb[word][query] (mhsa_dkv_v2's layout)
+  const bool use_kb = kbits && thr;
+  if (use_kb)
+    for (int i = threadIdx.x; i < N * 2; i += FB_WAVES * 64) {
+      const u32x4 v = ((const u32x4*)(kbits + bh * N * 8))[i];
+      const int q = i >> 1, w0 = 4 * (i & 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Kb[(w0 + e) * FB_KBP + q] = v[e];
+    }
+  int kword[2], kshift[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kl = 32 * w + 16 * kt + frow;
+    const int kbit = 8 * (kl >> 5) + 4 * ((kl >> 4) & 1) + (kl & 3);
+    kword[kt] = ((kl >> 2) & 3) * 2 + (kbit >> 5);
+    kshift[kt] = kbit & 31;
+  }
+  __syncthreads();
+  // K^T of this wave's 32 keys as the A operand of dQ^T = K^T dS^T (keys 4g + e, 16 + 4g + e):
+  // its K rows written from registers into a 4 KiB image (in the dQ rows' space, before they
+  // are zeroed) and read back transposed
+  u32x4 kT[4];
+  {
+    char* Ki = Acc + w * 4096;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) *(u32x4*)(Ki + v2_off(16 * kt + frow, 4 * s2 + fq)) = kf[kt][s2];
+    lds_fence();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kT[t] = v2_trj2(Ki, LN, 0, t);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256 * 16; i += FB_WAVES * 64) ((f32x4*)Acc)[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  const float c2 = scale * 1.4426950408889634f;
+  const uint32_t rk = rng_key(seed, site);
+  const bool wact = 32 * w < N;
+  f32x4 dkt[4][2], dvt[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) dkt[t][kt] = dvt[t][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < FB_WAVES; ++s) {
+    const int j0 = 2 * ((w + s) & (FB_WAVES - 1));  // first query tile of this step's pair
+    if (wact && j0 < nqt) {                         // wave-uniform
+      f32x4 pd[2][2], dsv[2][2];                    // [query tile][key tile]
+#pragma unroll
+      for (int bq = 0; bq < 2; ++bq) {
+        const int j = j0 + bq;
+        if (j < nqt) {
+          const u32x4 qa0 = v2_fragj(Qs, LN, j, 0), qa1 = v2_fragj(Qs, LN, j, 1);
+          const u32x4 da0 = v2_fragj(Ds, LN, j, 0), da1 = v2_fragj(Ds, LN, j, 1);
+          const f32x4 l4 = *(const f32x4*)(Ls + 16 * j + 4 * fq);
+          const f32x4 d4 = *(const f32x4*)(Dl + 16 * j + 4 * fq);
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            // S[q][key], dP[q][key]: rows = queries 16j + 4fq + r, column = this lane's key
+            f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
+            sv = v2_mma32(qa0, kf[kt][0], sv);
+            sv = v2_mma32(qa1, kf[kt][1], sv);
+            dp = v2_mma32(da0, vf[kt][0], dp);
+            dp = v2_mma32(da1, vf[kt][1], dp);
+            const int key = 32 * w + 16 * kt + frow;
+            uint32_t hlo = 0u, hhi = 0u;
+            if (thr && !use_kb) {  // re-hash (mhsa_dkv_v2's quad exchange)
+              const int qc = 16 * j + 4 * fq + (frow & 3);
+              const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
+              hlo = rng_pair(rk, idx);
+              hhi = rng_pair(rk, idx + 2);
+            }
+            u32x4 kw4 = {0u, 0u, 0u, 0u};
+            if (use_kb) kw4 = *(const u32x4*)(Kb + kword[kt] * FB_KBP + 16 * j + 4 * fq);
+            f32x4 p;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) p[r] = kv[kt] ? __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -l4[r])) : 0.f;
+            if (16 * j + 16 > N) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (16 * j + 4 * fq + r >= N) p[r] = 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float kp = 1.f;
+              if (use_kb) {
+                kp = ((kw4[r] >> kshift[kt]) & 1u) ? dscale : 0.f;
+              } else if (thr) {
+                const int src = (lane & ~3) | r;
+                const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
+                const uint32_t word = (key & 2) ? hi : lo;
+                const uint32_t u16 = (key & 1) ? (word >> 16) : (word & 0xffffu);
+                kp = u16 >= thr ? dscale : 0.f;
+              }
+              pd[bq][kt][r] = p[r] * kp;
+              dsv[bq][kt][r] = p[r] * fmaf(dp[r], kp, -d4[r]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) pd[bq][kt] = dsv[bq][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      // dV^T[d][key] += dO^T[d][q] P~[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]  (the pair's 32 queries)
+      u32x4 pb[2], sb[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        pb[kt] = v2_cat(v2_pack(pd[0][kt]), v2_pack(pd[1][kt]));
+        sb[kt] = v2_cat(v2_pack(dsv[0][kt]), v2_pack(dsv[1][kt]));
+        // dS^T image: row = key (16kt + frow), queries 16bq + 4fq .. +3
+#pragma unroll
+        for (int bq = 0; bq < 2; ++bq)
+          *(v4s_t*)(Scr + fb_scr(16 * kt + frow, 4 * bq + fq)) = v2_pack(dsv[bq][kt]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const u32x4 doT = v2_trj2(Ds, LN, j0, t), qT = v2_trj2(Qs, LN, j0, t);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          dvt[t][kt] = v2_mma32(doT, pb[kt], dvt[t][kt]);
+          dkt[t][kt] = v2_mma32(qT, sb[kt], dkt[t][kt]);
+        }
+      }
+      lds_fence();  // this wave's dS^T image written before its transposed reads
+      // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q] into the pair's f32 rows (this step's owner)
+#pragma unroll
+      for (int bq = 0; bq < 2; ++bq) {
+        if (j0 + bq < nqt) {
+          const int g = lane >> 4, li = lane & 15;
+          v4s_t lo, hi;
+          {
+            const int row = 4 * g + (li >> 2), unit = 4 * bq + (li & 3);
+            lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(Scr + fb_scr(row, unit)));
+            hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(Scr + fb_scr(row + 16, unit)));
+          }
+          const u32x4 bfr = v2_cat(lo, hi);
+          const int q = 16 * (j0 + bq) + frow;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            f32x4* a = (f32x4*)(Acc + fb_acc(q, 4 * t + fq));
+            *a = v2_mma32(kT[t], bfr, *a);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // dQ (bf16, x scale): two threads per query row
+  {
+    const int qd = threadIdx.x >> 1, hf = threadIdx.x & 1;
+    if (qd < N) {
+      bf16_t* dst = dqkv + ((long)b * N + qd) * pitch + h * 64 + 32 * hf;
+#pragma unroll
+      for (int c = 0; c < 8; c += 2) {
+        const f32x4 x = *(const f32x4*)(Acc + fb_acc(qd, 8 * hf + c));
+        const f32x4 y = *(const f32x4*)(Acc + fb_acc(qd, 8 * hf + c + 1));
+        u32x4 u;
+        u[0] = f2bf2(x[0] * scale, x[1] * scale);
+        u[1] = f2bf2(x[2] * scale, x[3] * scale);
+        u[2] = f2bf2(y[0] * scale, y[1] * scale);
+        u[3] = f2bf2(y[2] * scale, y[3] * scale);
+        *(u32x4*)(dst + 4 * c) = u;
+      }
+    }
+  }
+  // q part of the qkv bias gradient's partial row: column sums of the f32 dQ rows (rows >= N are 0)
+  float* red = (float*)(smem + FB_SCR);
+  if (dbias) {
+    const int c = threadIdx.x & 63, g8 = threadIdx.x >> 6;
+    float sum = 0.f;
+    for (int r = 32 * g8; r < 32 * g8 + 32; ++r) sum += ((const float*)(Acc + fb_acc(r, c >> 2)))[c & 3];
+    red[g8 * 64 + c] = sum * scale;
+  }
+  __syncthreads();  // the dQ rows are read: their space takes the dK / dV rows
+  // dK (x scale) and dV rows of this wave's keys through LDS ([32 keys][dK 64 | dV 64] bf16,
+  // 16-byte chunks XOR-swizzled by row & 15), then stored as whole 128-byte row segments
+  {
+    char* Rw = Acc + w * 8192;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int row = 16 * kt + frow;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        uint2 u;
+        u.x = f2bf2(dkt[t][kt][0] * scale, dkt[t][kt][1] * scale);
+        u.y = f2bf2(dkt[t][kt][2] * scale, dkt[t][kt][3] * scale);
+        *(uint2*)(Rw + row * 256 + (((2 * t + (fq >> 1)) ^ (row & 15)) << 4) + 8 * (fq & 1)) = u;
+        u.x = f2bf2(dvt[t][kt][0], dvt[t][kt][1]);
+        u.y = f2bf2(dvt[t][kt][2], dvt[t][kt][3]);
+        *(uint2*)(Rw + row * 256 + (((8 + 2 * t + (fq >> 1)) ^ (row & 15)) << 4) + 8 * (fq & 1)) = u;
+      }
+    }
+    lds_fence();
+    const int c = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 4 * i + (lane >> 4);
+      const int key = 32 * w + row;
+      const u32x4 v = *(const u32x4*)(Rw + row * 256 + ((c ^ (row & 15)) << 4));
+      if (key < N) *(u32x4*)(dqkv + ((long)b * N + key) * pitch + (c < 8 ? D : 2 * D - 64) + h * 64 + 8 * c) = v;
+    }
+  }
+  // k / v parts of the bias partial row from the register accumulators (keys >= N hold 0)
+  if (dbias) {
+    float* prow = dbias + (long)b * 3 * D;
+    f32x4 sk[4], sv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sk[t] = dkt[t][0] + dkt[t][1];
+      sv[t] = dvt[t][0] + dvt[t][1];
+    }
+    v2_colsum64<FB_WAVES>(sk, scale, red + 2 * FB_WAVES * 64, prow + D + h * 64);
+    v2_colsum64<FB_WAVES>(sv, 1.f, red + 4 * FB_WAVES * 64, prow + 2 * D + h * 64);
+    if (threadIdx.x < 64) {
+      float sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FB_WAVES; ++i) sq += red[i * 64 + threadIdx.x];
+      prow[h * 64 + threadIdx.x] = sq;
+    }
+  }
+}
+
 static bool v2_ok(int dt, int hd, int N) { return dt == HVIT_BF16 && hd == 64 && N <= V2_KMAX && N % 4 == 0; }
 static bool v2_big(int N) { return N > 256; }  // the KMAX = 512 instantiations
 // waves per v2 workgroup: 16 = all queries (keys) of a (b, h) in one
@@ -1055,6 +1375,13 @@ static bool v2_big(int N) { return N > 256; }  // the KMAX = 512 instantiations
 // to 4, the template the launches fall back to) cannot size the rows apart
 // from the grid.
 // (N > 256 takes the KMAX = 512 kernels, instantiated for 16 waves only)
+// the single-pass backward (mhsa_bwd_fused) for N <= 256; HVIT_ATTN_FUSED=0 or
+// hvit_gemm_tune(4, 0) selects the dQ + dK/dV kernel pair (A/B, tests)
+int& attn_fused_ref() {
+  static int v = getenv("HVIT_ATTN_FUSED") ? atoi(getenv("HVIT_ATTN_FUSED")) : 1;
+  return v;
+}
+static bool v2_fused(int N) { return attn_fused_ref() != 0 && !v2_big(N); }
 static int v2_waves(int N) {
   static const int w = [] {
     const int e = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
@@ -1150,7 +1477,7 @@ static int mhsa_fwd_impl(int dt, const void* qkv, int B, int N, int H, int hd, f
 // partial rows of the fused bias gradient per sample: one per v2 workgroup
 // along the token axis; one per sample otherwise
 static long long mhsa_bias_rows_per_sample(int dt, int hd, int N) {
-  return v2_ok(dt, hd, N) ? cdiv(N, 16 * v2_waves(N)) : 1;
+  return v2_ok(dt, hd, N) ? (v2_fused(N) ? 1 : cdiv(N, 16 * v2_waves(N))) : 1;
 }
 
 static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dout, const float* lse, int B, int N,
@@ -1175,6 +1502,13 @@ static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dou
       hipLaunchKernelGGL(dkvk, g, dim3(64 * waves), 0, st, (const bf16_t*)qkv, (const bf16_t*)dout, lse,
                          (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits, dbias);
     };
+    if (v2_fused(N)) {
+      hipLaunchKernelGGL(mhsa_bwd_fused, dim3(1, H, B), dim3(FB_WAVES * 64), 0, st, (const bf16_t*)qkv,
+                         (const bf16_t*)o, (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds,
+                         seed, site, keep_bits, dbias);
+      HVIT_LAUNCH_CHECK();
+      return HVIT_OK;
+    }
     const int wv = v2_waves(N);
     if (v2_big(N)) go(mhsa_dq_v2<16, 512>, mhsa_dkv_v2<16, 512>, 16);
     else if (wv == 16) go(mhsa_dq_v2<16, 256>, mhsa_dkv_v2<16, 256>, 16);
@@ -1213,6 +1547,12 @@ extern "C" long long hvit_mhsa_keep_bits_elems(int B, int N, int H) {
 // 1 when the kernels for (dt, N, hd) store / read keep bits (else a keep-bit
 // buffer would be allocated for nothing: callers skip it)
 extern "C" int hvit_mhsa_keep_bits_used(int dt, int N, int hd) { return v2_ok(dt, hd, N) ? 1 : 0; }
+
+int hvit_attn_tune(int value) {
+  const int old = hvit::attn_fused_ref();
+  hvit::attn_fused_ref() = value;
+  return old;
+}
 
 extern "C" int hvit_mhsa_fwd_kb(int dt, const void* qkv, int B, int N, int H, int hd, float scale,
                                 const hvit_dropout_t* dropout, void* o, float* lse, unsigned* keep_bits,

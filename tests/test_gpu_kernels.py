@@ -442,6 +442,62 @@ def test_mhsa_v2_deterministic(hv, N):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,N,H,p,kb", [(4, 256, 8, 0.1, True), (2, 240, 8, 0.1, False), (3, 100, 2, 0.0, False),
+                                        (2, 228, 4, 0.3, True), (2, 16, 2, 0.1, True), (1, 36, 3, 0.0, False)])
+def test_mhsa_bwd_single_pass_matches_pair(hv, B, N, H, p, kb):
+    """The single-pass backward (mhsa_bwd_fused, N <= 256, hvit_gemm_tune(4, 1))
+    against the dQ + dK/dV kernel pair (hvit_gemm_tune(4, 0)) and the torch fp32
+    gradient of the same forward: dqkv within bf16 rounding of the pair (they sum
+    in different orders), both within the usual bar of the reference; the qkv
+    bias partial rows summed equal the column sums of the same dqkv; repeated
+    calls bit-identical (the dQ rows take their contributions in a fixed order)."""
+    l = L(hv)
+    hd, D = 64, H * 64
+    torch.manual_seed(N + H)
+    qkv = (torch.randn(B * N, 3 * D, device=DEV) * 0.7).to(torch.bfloat16)
+    go = torch.randn(B * N, D, device=DEV).to(torch.bfloat16)
+    dr = l.dropout(p, 77, 23) if p > 0 else None
+    o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    bits = torch.zeros(l.lib().hvit_mhsa_keep_bits_elems(B, N, H), dtype=torch.int32, device=DEV)
+    l.call("hvit_mhsa_fwd_kb", l.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+           bits.data_ptr() if kb else None, s())
+    outs = {}
+    old = l.lib().hvit_gemm_tune(4, 1)
+    try:
+        for mode in (0, 1, 1):
+            l.lib().hvit_gemm_tune(4, mode)
+            rows = l.lib().hvit_mhsa_bias_rows(l.BF16, B, N, H, hd)
+            parts = torch.full((rows, 3 * D), float("nan"), device=DEV)
+            dq = torch.full_like(qkv, float("nan"))
+            delta = torch.empty(B, H, N, device=DEV)
+            l.call("hvit_mhsa_bwd_db", l.BF16, qkv.data_ptr(), o.data_ptr(), go.data_ptr(), lse.data_ptr(), B, N, H,
+                   hd, hd ** -0.5, dr, bits.data_ptr() if kb else None, dq.data_ptr(), delta.data_ptr(),
+                   parts.data_ptr(), s())
+            torch.cuda.synchronize()
+            outs.setdefault(mode, []).append((dq, parts.sum(0), delta))
+    finally:
+        l.lib().hvit_gemm_tune(4, old)
+    (pair, pair_db, pair_delta), = outs[0]
+    (one, one_db, one_delta), (again, again_db, _) = outs[1]
+    assert torch.isfinite(one.float()).all()
+    assert torch.equal(one, again) and torch.equal(one_db, again_db)
+    assert torch.allclose(one_delta, pair_delta, rtol=1e-5, atol=1e-5)
+    mask = None
+    if p > 0:
+        mask = torch.as_tensor(keep_mask(77, 23, B * H * N * N, p).reshape(B, H, N, N), device=DEV).float()
+    xr = qkv.float().requires_grad_(True)
+    o_ref, _ = attn_ref(xr, B, N, H, hd, p, mask)
+    o_ref.backward(go.float())
+    g1, g0, r = one.float().view(B * N, 3, D), pair.float().view(B * N, 3, D), xr.grad.view(B * N, 3, D)
+    for i in range(3):
+        assert rel(g1[:, i], g0[:, i]) < 1e-2, ("qkv"[i], rel(g1[:, i], g0[:, i]))
+        assert rel(g1[:, i], r[:, i]) < 4e-2, ("qkv"[i], rel(g1[:, i], r[:, i]))
+    want = one.float().sum(0)
+    bar = one.float().abs().sum(0) * 2.0 ** -8 + 1e-5
+    assert ((one_db - want).abs() <= bar).all(), float(((one_db - want).abs() / bar).max())
+
+
 @pytest.mark.parametrize("B,N,H,p,kb", [(4, 256, 8, 0.1, True), (3, 100, 2, 0.0, False), (2, 300, 2, 0.1, False),
                                         (2, 496, 8, 0.1, True), (2, 520, 2, 0.1, False)])
 def test_mhsa_bwd_fused_qkv_bias(hv, B, N, H, p, kb):
