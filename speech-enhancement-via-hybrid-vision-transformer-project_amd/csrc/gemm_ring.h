@@ -192,6 +192,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the acc -> LDS rows below branch per wave
   const int wm = wid / WN, wn = wid % WN;
   const TileId t3 = tile_of(ep.xcd_remap);
+  GEMM_STAMP(0);
   const int m0 = t3.mt * BM, n0 = t3.nt * BN;
   const int kbeg = t3.z * kps;
   const int kend = min(K, kbeg + kps);
@@ -204,6 +205,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   C::run(la, lb, smem, m0, n0, kbeg, kend, acc, ep);
+  GEMM_STAMP(1);
 
   // ------------------------------------------------------------ epilogue ---
   const uint32_t dkey = epi_key(ep);
@@ -393,6 +395,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
       }
     }
   }
+  GEMM_STAMP(2);
 }
 
 // ---------------------------------------------------------------- host -----

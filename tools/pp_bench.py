@@ -10,7 +10,11 @@ accumulation order is the same k order, so they should agree bit for bit) and
 with a torch fp32 reference of the same op; HIP-event timing with the modes
 interleaved round by round in one process.
 
-    python tools/pp_bench.py [modes=0,1,2] [rounds=5] [M=8192]
+    python tools/pp_bench.py [modes=0,1,2] [rounds=5] [M=8192] [what=3]
+
+what=W A/Bs the values `modes` of another hvit_gemm_tune knob W instead (the
+persistent kernels off); the weight-gradient rows time the ring / gemm.h
+weight-gradient kernels with their slab sums.
 """
 
 import os
@@ -112,6 +116,18 @@ def cases(M, D=512, HID=2048):
     out.append(("dgrad fc2+geluB p0", 2 * M * D * HID,
                 lambda: L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh0.data_ptr(),
                                L.BF16, ep_g0, s()), [dh0, cs0], ref_2))
+    # weight gradients (both operands k-major: the ring kernels' 128x128 / 128x64 forms + slab sums)
+    for nm, n_, k_ in (("wgrad qkv", 3 * D, D), ("wgrad fc1", HID, D), ("wgrad fc2", D, HID), ("wgrad proj", D, D)):
+        dy_, x_ = r(M, n_), r(M, k_)
+        dw_ = torch.empty(n_, k_, device=DEV)
+        KEEP.append(dw_)
+
+        def fw(dy_=dy_, x_=x_, n_=n_, k_=k_, dw_=dw_):
+            HF.linear_wgrad_now(L.BF16, dy_, x_, M, n_, k_, dest=dw_)
+
+        def rw(dy_=dy_, x_=x_):
+            return [dy_.float().t() @ x_.float()]
+        out.append((nm, 2 * M * n_ * k_, fw, [dw_], rw))
     return out
 
 
@@ -133,13 +149,17 @@ def main():
     modes = [int(c) for c in args.get("modes", "0,1,2").split(",")]
     rounds = int(args.get("rounds", "5"))
     M = int(args.get("M", "8192"))
+    what = int(args.get("what", "3"))  # the hvit_gemm_tune knob the modes set
+    if what != 3:
+        L.lib().hvit_gemm_tune(3, 0)
+    old = L.lib().hvit_gemm_tune(what, modes[0])
     cs = cases(M)
     ref = {}
     times = {(n, c): [] for n, *_ in cs for c in modes}
     bad = 0
     for rd in range(rounds):
         for c in modes:
-            L.lib().hvit_gemm_tune(3, c)
+            L.lib().hvit_gemm_tune(what, c)
             for name, fl, fn, outs, tref in cs:
                 if rd == 0:
                     for t in outs:
@@ -174,7 +194,7 @@ def main():
             t = sorted(times[(name, c)])[len(times[(name, c)]) // 2]
             row += f"  {t:9.1f} {fl / t / 1e6:6.0f}"
         print(f"{name:22s}{row}", flush=True)
-    L.lib().hvit_gemm_tune(3, -1)
+    L.lib().hvit_gemm_tune(what, old)
     if bad:
         print(f"FAILED checks: {bad}")
         sys.exit(1)
