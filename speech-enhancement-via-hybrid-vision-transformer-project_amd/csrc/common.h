@@ -178,6 +178,34 @@ __device__ __forceinline__ GeluGG gelu_gg(float x) {
   return {x * cdf, cdf + x * (0.39894228040143268f * e)};
 }
 
+// The same for 4 values, the arithmetic on packed f32 pairs (v_pk_fma_f32 /
+// v_pk_mul_f32: two lanes' worth per issue; rcp / exp stay per element): the
+// fc1 forward epilogue evaluates one per output, ~40 % fewer VALU issues than
+// four gelu_gg calls.  Same operation sequence per element as gelu_gg.
+__device__ __forceinline__ void gelu_gg4(const f32x4& v, f32x4& g, f32x4& d) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x2_t x = {v[2 * h], v[2 * h + 1]};
+    const f32x2_t z = x * 0.70710678118654752f;
+    const f32x2_t az = {fabsf(z.x), fabsf(z.y)};
+    const f32x2_t den = 1.f + 0.3275911f * az;
+    const f32x2_t t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    const f32x2_t q = az * az;
+    const f32x2_t e = {__expf(-q.x), __expf(-q.y)};
+    const f32x2_t poly =
+        t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+    const f32x2_t r = 1.f - poly * e;
+    const f32x2_t er = {copysignf(r.x, z.x), copysignf(r.y, z.y)};
+    const f32x2_t cdf = 0.5f * (1.f + er);
+    const f32x2_t gg = x * cdf;
+    const f32x2_t dd = cdf + x * (0.39894228040143268f * e);
+    g[2 * h] = gg.x;
+    g[2 * h + 1] = gg.y;
+    d[2 * h] = dd.x;
+    d[2 * h + 1] = dd.y;
+  }
+}
+
 // ---------------------------------------------------------- wave reductions --
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

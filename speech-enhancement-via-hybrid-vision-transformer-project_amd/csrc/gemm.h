@@ -600,8 +600,9 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
   }
   if (ep.act == ACT_GELU_DUAL) {
     f32x4 g, d;
+    gelu_gg4(v, g, d);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { const GeluGG t_ = gelu_gg(v[e]); g[e] = t_.g * keep[e]; d[e] = t_.d; }
+    for (int e = 0; e < 4; ++e) g[e] *= keep[e];
     if (ep.out) store4v<FAST>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, nv, ep.out_dt);
     store4v<FAST>(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
     return;
@@ -1416,11 +1417,10 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
             kb = keep4(ep, dkey, m, n8 + 4, N);
           }
           f32x4 ga, gb, da, db;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            { const GeluGG t_ = gelu_gg(va[e]); ga[e] = t_.g * ka[e]; da[e] = t_.d; }
-            { const GeluGG t_ = gelu_gg(vb[e]); gb[e] = t_.g * kb[e]; db[e] = t_.d; }
-          }
+          gelu_gg4(va, ga, da);
+          gelu_gg4(vb, gb, db);
+          ga *= ka;
+          gb *= kb;
           // (no out: the inference form, HVIT_ACT_GELU -- only gelu(v) is stored)
           if (ep.out) *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? wide8(da, db) : wide8(va, vb);
           *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = wide8(ga, gb);
@@ -1607,8 +1607,8 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           const f32x4 v = *(const f32x4*)(Cs + row * CP + c4 * 4) + bias4;
           const f32x4 k = ep.drop_thr ? keep4(ep, dkey, m, n, N) : (f32x4){1.f, 1.f, 1.f, 1.f};
           f32x4 g, d;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { const GeluGG t_ = gelu_gg(v[e]); g[e] = t_.g * k[e]; d[e] = t_.d; }
+          gelu_gg4(v, g, d);
+          g *= k;
           if (ep.out) store4v<true>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, 4, ep.out_dt);
           store4v<true>(ep.out2, (long)m * ep.ldo2 + n, g, 4, ep.out2_dt);
         }

@@ -255,11 +255,10 @@ __device__ __forceinline__ static void run(const LdDense<bf16_t, true>& la, cons
         kb = keep4_at(dkey, i0 + 4, ep.drop_thr, ep.drop_scale);
       }
       f32x4 ga, gb, dda, ddb;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        { const GeluGG t_ = gelu_gg(va8[e]); ga[e] = t_.g * ka[e]; dda[e] = t_.d; }
-        { const GeluGG t_ = gelu_gg(vb8[e]); gb[e] = t_.g * kb[e]; ddb[e] = t_.d; }
-      }
+      gelu_gg4(va8, ga, dda);
+      gelu_gg4(vb8, gb, ddb);
+      ga *= ka;
+      gb *= kb;
       st16(ep.gd ? pack8(dda, ddb) : pack8(va8, vb8), rout, (unsigned)(((long)m * ep.ldo + n) * 2) | kill);
       st16(pack8(ga, gb), rout2, (unsigned)(((long)m * ep.ldo2 + n) * 2) | kill);
     } else {  // K_GELU_BWD: v *= keep * gelu'(h)  (aux = gelu'(h) when gd, else h)

@@ -280,11 +280,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
           kb = keep4(ep, dkey, m, n8 + 4, N);
         }
         f32x4 ga, gb, da, db;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          { const GeluGG t_ = gelu_gg(va[e]); ga[e] = t_.g * ka[e]; da[e] = t_.d; }
-          { const GeluGG t_ = gelu_gg(vb[e]); gb[e] = t_.g * kb[e]; db[e] = t_.d; }
-        }
+        gelu_gg4(va, ga, da);
+        gelu_gg4(vb, gb, db);
+        ga *= ka;
+        gb *= kb;
         // (no out: the inference form, HVIT_ACT_GELU -- only gelu(v) is stored)
         if (ep.out) *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? pack8(da, db) : pack8(va, vb);
         *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = pack8(ga, gb);
