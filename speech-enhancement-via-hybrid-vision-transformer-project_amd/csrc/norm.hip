@@ -92,11 +92,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 }
 
 // rows per workgroup for the backward: 4 waves x RPW rows, every row of a wave
-// in registers before any is reduced.  RPW = 4 (16 rows) up to D = 512; wider
-// rows take RPW = 2 (8 rows): at D = 768 four rows of x / dy / resid are 144
-// VGPRs, which left one wave per SIMD -- and at BASELINE config 5's M = 4096
-// only 256 workgroups, one per CU (17.6 % of HBM, round 4).
-__host__ __device__ constexpr int lnb_rpw(int D) { return D <= 512 ? 4 : 2; }
+// in registers before any is reduced.  RPW = 2 (8 rows): at D = 768 four rows
+// of x / dy / resid were 144 VGPRs, which left one wave per SIMD -- and at
+// BASELINE config 5's M = 4096 only 256 workgroups, one per CU (17.6 % of HBM,
+// round 4; 39.7 -> 17.9 us per launch with two); at D = 512 two rows per wave
+// measured 22.1 -> 20.6 us per launch in-step (round 5, same-box A/B).
+__host__ __device__ constexpr int lnb_rpw(int) { return 2; }
 static inline int lnb_rows(int D) { return 4 * lnb_rpw(D); }
 
 template <typename TD>
