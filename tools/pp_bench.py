@@ -116,6 +116,28 @@ def cases(M, D=512, HID=2048):
     out.append(("dgrad fc2+geluB p0", 2 * M * D * HID,
                 lambda: L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh0.data_ptr(),
                                L.BF16, ep_g0, s()), [dh0, cs0], ref_2))
+    # a conv-shaped dense GEMM (enc1 forward as a plain GEMM: M = 32 x 128 x 128 pixels, N = 128
+    # channels, K = 64 x 9 taps; the real conv gathers A by implicit im2col)
+    if os.environ.get("PP_CONVLIKE"):
+        Mc = 32 * 128 * 128
+        xc, wc = r(Mc, 576), r(128, 576, scale=0.05)
+        yc = torch.empty(Mc, 128, device=DEV, dtype=BF)
+        KEEP.append(yc)
+        out.append(("convlike fwd", 2 * Mc * 128 * 576,
+                    lambda: L.call("hvit_linear_fwd", L.BF16, xc.data_ptr(), wc.data_ptr(), None, Mc, 128, 576,
+                                   yc.data_ptr(), L.BF16, None, s()), [yc], None))
+    # N = 512 data gradients (dy [M, K] x W [K, 512]: qkv / proj in bf16, fc1 in f32 for the LN backward)
+    for nm, k_, odt in (("dgrad qkv->512", 3 * D, L.BF16), ("dgrad proj->512", D, L.BF16), ("dgrad fc1->512", HID, L.F32)):
+        dy_, w_ = r(M, k_), r(k_, D, scale=0.05)
+        o_ = torch.empty(M, D, device=DEV, dtype=BF if odt == L.BF16 else torch.float32)
+        KEEP.append(o_)
+
+        def fd(dy_=dy_, w_=w_, k_=k_, o_=o_, odt=odt):
+            L.call("hvit_linear_dgrad", L.BF16, dy_.data_ptr(), w_.data_ptr(), M, k_, D, o_.data_ptr(), odt, None, s())
+
+        def rd(dy_=dy_, w_=w_):
+            return [dy_.float() @ w_.float()]
+        out.append((nm, 2 * M * k_ * D, fd, [o_], rd))
     # weight gradients (both operands k-major: the ring kernels' 128x128 / 128x64 forms + slab sums)
     for nm, n_, k_ in (("wgrad qkv", 3 * D, D), ("wgrad fc1", HID, D), ("wgrad fc2", D, HID), ("wgrad proj", D, D)):
         dy_, x_ = r(M, n_), r(M, k_)
