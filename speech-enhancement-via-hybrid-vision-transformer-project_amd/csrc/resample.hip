@@ -51,6 +51,50 @@ __global__ __launch_bounds__(256) void bilinear_fwd_kernel(const void* x, int x_
   }
 }
 
+// The same with one output row per blockIdx.y and CV channels per thread
+// (bf16 CV = 8: four 16-byte loads, one 16-byte store; f32 CV = 1: the C = 1
+// final resize): the row / column index math once per CV channels and no
+// per-element division (the element-wise form above spent most of its time in
+// three integer divisions per element).  Same arithmetic per element.
+template <typename T, int CV>
+__global__ __launch_bounds__(256) void bilinear_fwd_rows_kernel(const T* __restrict__ x, T* __restrict__ y, int Hi,
+                                                               int Wi, int C, int Ho, int Wo, float sh, float sw) {
+  const int r = blockIdx.y;  // n * Ho + oy
+  const int n = r / Ho, oy = r - n * Ho;
+  const int G = C / CV;
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= Wo * G) return;
+  const int ox = item / G, cg = item - ox * G;
+  const LinIdx ly = lin_idx(oy, Hi, sh), lx = lin_idx(ox, Wi, sw);
+  const T* r0 = x + ((long)(n * Hi + ly.i0) * Wi) * C + cg * CV;
+  const T* r1 = x + ((long)(n * Hi + ly.i1) * Wi) * C + cg * CV;
+  T* out = y + ((long)r * Wo + ox) * C + cg * CV;
+  if constexpr (CV == 8) {
+    const u32x4 a = *(const u32x4*)(r0 + (long)lx.i0 * C), b = *(const u32x4*)(r0 + (long)lx.i1 * C);
+    const u32x4 c = *(const u32x4*)(r1 + (long)lx.i0 * C), d = *(const u32x4*)(r1 + (long)lx.i1 * C);
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        auto f = [&](uint32_t u) { return h ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16); };
+        const float v00 = f(a[e]), v01 = f(b[e]), v10 = f(c[e]), v11 = f(d[e]);
+        v[h] = ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11);
+      }
+      o[e] = f2bf2(v[0], v[1]);
+    }
+    *(u32x4*)out = o;
+  } else {
+#pragma unroll
+    for (int e = 0; e < CV; ++e) {
+      const float v00 = Elem<T>::to_f(r0[(long)lx.i0 * C + e]), v01 = Elem<T>::to_f(r0[(long)lx.i1 * C + e]);
+      const float v10 = Elem<T>::to_f(r1[(long)lx.i0 * C + e]), v11 = Elem<T>::to_f(r1[(long)lx.i1 * C + e]);
+      out[e] = Elem<T>::from_f(ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11));
+    }
+  }
+}
+
 // weight with which output index o samples input index i along one dim
 __device__ __forceinline__ float lin_w(int o, int i, int in, float scale) {
   LinIdx l = lin_idx(o, in, scale);
@@ -187,21 +231,25 @@ __global__ __launch_bounds__(256) void bilinear_bwd_vec_kernel(const TI* __restr
   }
 }
 
-// Row-blocked gather backward: one workgroup per input row (n, iy).  The
-// output taps of every input column of the row (and of the row itself) are
-// computed once into LDS, then threads walk (column, channel group) items.
-constexpr int RB_MAXW = 256, RB_TAPS = 12;
+// Row-blocked gather backward: one workgroup per RB input rows (n, iy .. iy +
+// RB - 1; RB > 1 only when one row has fewer (column, channel group) items
+// than threads -- the C = 1 final-output resize: 64 items per row left three
+// quarters of every workgroup idle, 0.3 TB/s).  The output taps of every input
+// column of the row (and of the rows themselves) are computed once into LDS,
+// then threads walk (row, column, channel group) items.
+constexpr int RB_MAXW = 256, RB_TAPS = 12, RB_MAXR = 8;
 template <typename TI, typename TO, int CV>
 __global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __restrict__ dy, TO* __restrict__ dx,
                                                                int Hi, int Wi, int C, int Ho, int Wo, float sh,
-                                                               float sw, int accumulate) {
+                                                               float sw, int accumulate, int RB) {
   __shared__ int xo[RB_MAXW][RB_TAPS];
   __shared__ float xw[RB_MAXW][RB_TAPS];
   __shared__ int xn[RB_MAXW];
-  __shared__ int yo[RB_TAPS];
-  __shared__ float yw[RB_TAPS];
-  __shared__ int yn;
-  const int n = blockIdx.x / Hi, iy = blockIdx.x - n * Hi;
+  __shared__ int yo[RB_MAXR][RB_TAPS];
+  __shared__ float yw[RB_MAXR][RB_TAPS];
+  __shared__ int yn[RB_MAXR];
+  const int rpn = (Hi + RB - 1) / RB;  // row blocks per sample
+  const int n = blockIdx.x / rpn, iy0 = (blockIdx.x - n * rpn) * RB;
   for (int ix = threadIdx.x; ix < Wi; ix += blockDim.x) {
     int lo, hi;
     out_range(ix, Wi, Wo, sw, lo, hi);
@@ -216,32 +264,38 @@ __global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __rest
     }
     xn[ix] = nt;
   }
-  if (threadIdx.x == 0) {
-    int lo, hi;
-    out_range(iy, Hi, Ho, sh, lo, hi);
+  if (threadIdx.x < RB) {
+    const int r = threadIdx.x, iy = iy0 + r;
     int nt = 0;
-    for (int o = lo; o <= hi && nt < RB_TAPS; ++o) {
-      const float wt = lin_w(o, iy, Hi, sh);
-      if (wt != 0.f) {
-        yo[nt] = o;
-        yw[nt] = wt;
-        ++nt;
+    if (iy < Hi) {
+      int lo, hi;
+      out_range(iy, Hi, Ho, sh, lo, hi);
+      for (int o = lo; o <= hi && nt < RB_TAPS; ++o) {
+        const float wt = lin_w(o, iy, Hi, sh);
+        if (wt != 0.f) {
+          yo[r][nt] = o;
+          yw[r][nt] = wt;
+          ++nt;
+        }
       }
     }
-    yn = nt;
+    yn[r] = nt;
   }
   __syncthreads();
   const int G = C / CV;
-  const int ny = yn;
-  for (int item = threadIdx.x; item < Wi * G; item += blockDim.x) {
-    const int ix = item / G, cg = item - ix * G;
+  const int per_row = Wi * G;
+  for (int item = threadIdx.x; item < RB * per_row; item += blockDim.x) {
+    const int r = item / per_row, rem = item - r * per_row;
+    const int iy = iy0 + r;
+    if (iy >= Hi) break;  // (items are row-major: every later item is past the last row too)
+    const int ix = rem / G, cg = rem - ix * G;
     float acc[CV];
 #pragma unroll
     for (int e = 0; e < CV; ++e) acc[e] = 0.f;
-    const int nx = xn[ix];
+    const int nx = xn[ix], ny = yn[r];
     for (int a = 0; a < ny; ++a) {
-      const TI* row = dy + ((size_t)(n * Ho + yo[a]) * Wo) * C + cg * CV;
-      const float wa = yw[a];
+      const TI* row = dy + ((size_t)(n * Ho + yo[r][a]) * Wo) * C + cg * CV;
+      const float wa = yw[r][a];
       for (int b = 0; b < nx; ++b) {
         const float w = wa * xw[ix][b];
         const TI* q = row + (size_t)xo[ix][b] * C;
@@ -304,6 +358,38 @@ __global__ __launch_bounds__(256) void up_split_bwd_kernel(const void* du, int d
   }
 }
 
+// The same for bf16 with C1 % 8 == C2 % 8 == 0: a thread sums the U x U
+// 16-byte channel groups of one output pixel (f32 accumulation in the same
+// a-major, b-minor order) and stores one 16-byte group; two integer divisions
+// per 8 channels instead of four per channel.
+__global__ __launch_bounds__(256) void up_split_bwd_vec_kernel(const bf16_t* __restrict__ du, int N, int H, int W,
+                                                              int U, int C1, int C2, bf16_t* __restrict__ dx1,
+                                                              bf16_t* __restrict__ dx2) {
+  const int Ct = C1 + C2, G8 = Ct >> 3;
+  const int total = N * H * W * G8;  // < 2^31 (checked on the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int p = i / G8;
+    const int c0 = (i - p * G8) << 3;
+    const int t = p / W;  // n * H + y
+    const int x = p - t * W;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < U; ++a)
+      for (int b = 0; b < U; ++b) {
+        const u32x4 u = *(const u32x4*)(du + ((long)(t * U + a) * (W * U) + x * U + b) * Ct + c0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[2 * e] += __uint_as_float(u[e] << 16);
+          s[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf2(s[2 * e], s[2 * e + 1]);
+    if (c0 < C1) *(u32x4*)(dx1 + (long)p * C1 + c0) = o;
+    else *(u32x4*)(dx2 + (long)p * C2 + (c0 - C1)) = o;
+  }
+}
+
 static int grid_for(long n) {
   long g = (n + 255) / 256;
   if (g > 16384) g = 16384;
@@ -323,6 +409,20 @@ extern "C" int hvit_bilinear_fwd(const void* x, int x_dt, int N, int Hi, int Wi,
   if (total <= 0) return HVIT_OK;
   HVIT_CHECK(total < (1L << 31) && (long)N * Hi * Wi * C < (1L << 31), "resample: tensor too large");
   float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
+  if (x_dt == y_dt && (long)N * Ho < 65536) {
+    if (x_dt == HVIT_BF16 && C % 8 == 0 && aligned16(x) && aligned16(y)) {
+      hipLaunchKernelGGL((bilinear_fwd_rows_kernel<bf16_t, 8>), dim3(cdiv((long)Wo * (C / 8), 256), N * Ho), dim3(256),
+                         0, (hipStream_t)stream, (const bf16_t*)x, (bf16_t*)y, Hi, Wi, C, Ho, Wo, sh, sw);
+      HVIT_LAUNCH_CHECK();
+      return HVIT_OK;
+    }
+    if (x_dt == HVIT_F32 && C == 1) {
+      hipLaunchKernelGGL((bilinear_fwd_rows_kernel<float, 1>), dim3(cdiv(Wo, 256), N * Ho), dim3(256), 0,
+                         (hipStream_t)stream, (const float*)x, (float*)y, Hi, Wi, C, Ho, Wo, sh, sw);
+      HVIT_LAUNCH_CHECK();
+      return HVIT_OK;
+    }
+  }
   hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, x_dt,
                      y, y_dt, N, Hi, Wi, C, Ho, Wo, sh, sw);
   HVIT_LAUNCH_CHECK();
@@ -341,15 +441,24 @@ extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int W
   const bool taps_ok = (float)Ho / (float)Hi <= 6.f && (float)Wo / (float)Wi <= 6.f;
   const bool rows_ok = (float)Ho / (float)Hi <= 4.f && (float)Wo / (float)Wi <= 4.f && Wi <= RB_MAXW &&
                        (long)N * Hi < (1L << 31) && dy_dt == dx_dt;
+  // input rows per workgroup: enough (column, channel group) items for the 256 threads
+  auto rows_per_wg = [&](int cv) {
+    const long items = (long)Wi * (C / cv);
+    int rb = 1;
+    while (rb < RB_MAXR && items * rb * 2 <= 256) rb *= 2;
+    return rb;
+  };
   if (rows_ok && C % 8 == 0 && dy_dt == HVIT_BF16 && aligned16(dy) && aligned16(dx)) {
-    hipLaunchKernelGGL((bilinear_bwd_rows_kernel<bf16_t, bf16_t, 8>), dim3(N * Hi), dim3(256), 0,
-                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
+    const int rb = rows_per_wg(8);
+    hipLaunchKernelGGL((bilinear_bwd_rows_kernel<bf16_t, bf16_t, 8>), dim3(N * cdiv(Hi, rb)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, Hi, Wi, C, Ho, Wo, sh, sw, accumulate, rb);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
   if (rows_ok && C == 1 && dy_dt == HVIT_F32) {
-    hipLaunchKernelGGL((bilinear_bwd_rows_kernel<float, float, 1>), dim3(N * Hi), dim3(256), 0,
-                       (hipStream_t)stream, (const float*)dy, (float*)dx, Hi, Wi, C, Ho, Wo, sh, sw, accumulate);
+    const int rb = rows_per_wg(1);
+    hipLaunchKernelGGL((bilinear_bwd_rows_kernel<float, float, 1>), dim3(N * cdiv(Hi, rb)), dim3(256), 0,
+                       (hipStream_t)stream, (const float*)dy, (float*)dx, Hi, Wi, C, Ho, Wo, sh, sw, accumulate, rb);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }
@@ -380,6 +489,13 @@ extern "C" int hvit_upsample_split_bwd(const void* du, int du_dt, int N, int H, 
   long total = (long)N * H * W * (C1 + C2);
   if (total <= 0) return HVIT_OK;
   HVIT_CHECK(total * U * U < (1L << 31), "resample: tensor too large");
+  if (du_dt == HVIT_BF16 && dx1_dt == HVIT_BF16 && (C2 == 0 || dx2_dt == HVIT_BF16) && C1 % 8 == 0 && C2 % 8 == 0 &&
+      aligned16(du) && aligned16(dx1) && (C2 == 0 || aligned16(dx2))) {
+    hipLaunchKernelGGL(up_split_bwd_vec_kernel, dim3(grid_for(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)du, N, H, W, U, C1, C2, (bf16_t*)dx1, (bf16_t*)dx2);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   hipLaunchKernelGGL(up_split_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, du, du_dt,
                      N, H, W, U, C1, C2, dx1, dx1_dt, dx2, dx2_dt);
   HVIT_LAUNCH_CHECK();

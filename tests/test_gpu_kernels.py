@@ -647,8 +647,33 @@ def test_bn_act(hv, dt, N, H, W, C, pool, p):
     assert rel(sums[C:2 * C], gamma.grad) < 1e-4
 
 
+@pytest.mark.parametrize("N,H,W,U,C1,C2", [(4, 64, 64, 2, 128, 128), (2, 32, 32, 2, 256, 0), (3, 7, 9, 3, 8, 24)])
+def test_upsample_split_bwd_vector_path(hv, N, H, W, U, C1, C2):
+    """The bf16 16-byte-group form of hvit_upsample_split_bwd (all-bf16 tensors,
+    C1 and C2 multiples of 8) equals the element-wise form (f32 outputs, then
+    rounded to bf16) bit for bit: same U x U summation order, one rounding."""
+    l = L(hv)
+    torch.manual_seed(N * H + C1)
+    du = torch.randn(N, H * U, W * U, C1 + C2, device=DEV).to(torch.bfloat16)
+    outs = []
+    for odt in (torch.bfloat16, torch.float32):
+        dx1 = torch.full((N, H, W, C1), float("nan"), device=DEV, dtype=odt)
+        dx2 = torch.full((N, H, W, max(C2, 1)), float("nan"), device=DEV, dtype=odt)
+        l.call("hvit_upsample_split_bwd", du.data_ptr(), l.BF16, N, H, W, U, C1, C2, dx1.data_ptr(),
+               l.BF16 if odt == torch.bfloat16 else l.F32, dx2.data_ptr() if C2 else None,
+               l.BF16 if odt == torch.bfloat16 else l.F32, s())
+        outs.append((dx1, dx2))
+    torch.cuda.synchronize()
+    (v1, v2), (r1, r2) = outs
+    assert torch.equal(v1, r1.to(torch.bfloat16))
+    if C2:
+        assert torch.equal(v2, r2.to(torch.bfloat16))
+    ref = du.float().view(N, H, U, W, U, C1 + C2).sum((2, 4))
+    assert rel(r1, ref[..., :C1]) < 1e-5
+
+
 # -------------------------------------------------------------- bilinear ---
-@pytest.mark.parametrize("N,Hi,Wi,C,Ho,Wo", [(2, 64, 64, 256, 16, 16), (2, 64, 64, 1, 256, 256),
+@pytest.mark.parametrize("N,Hi,Wi,C,Ho,Wo", [(2, 64, 64, 256, 16, 16), (2, 64, 64, 1, 256, 256), (3, 30, 20, 1, 100, 77),
                                              (1, 8, 8, 1, 33, 47), (2, 16, 23, 8, 4, 4), (1, 64, 60, 1, 257, 251),
                                              (1, 128, 125, 64, 32, 30)])
 def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
@@ -666,6 +691,11 @@ def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
     l.call("hvit_bilinear_bwd", ga.data_ptr(), l.F32, N, Ho, Wo, C, Hi, Wi, dx.data_ptr(), l.F32, 0, s())
     assert rel(nchw(dx), x.grad) < 1e-5
     if C % 8 == 0:  # bf16 (the skip-connection path), incl. accumulate
+        xb = xa.to(torch.bfloat16)
+        yb = torch.empty(N, Ho, Wo, C, device=DEV, dtype=torch.bfloat16)
+        l.call("hvit_bilinear_fwd", xb.data_ptr(), l.BF16, N, Hi, Wi, C, Ho, Wo, yb.data_ptr(), l.BF16, s())
+        yr = F.interpolate(nchw(xb.float()), size=(Ho, Wo), mode="bilinear", align_corners=False)
+        assert (nchw(yb.float()) - yr).abs().max() <= 2.0 ** -8 * yr.abs().max() + 1e-6  # bf16 rounding of y only
         gb = ga.to(torch.bfloat16)
         dxb = torch.empty(N, Hi, Wi, C, device=DEV, dtype=torch.bfloat16)
         l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, dxb.data_ptr(), l.BF16, 0, s())
