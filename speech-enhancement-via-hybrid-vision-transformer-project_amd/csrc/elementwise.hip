@@ -321,6 +321,7 @@ struct WPrepItem {
   const float *gamma, *beta, *rmean, *rvar;
   float* bias;
   float eps;
+  int ci_shift;  // log2(ci) when ci is a power of two, else -1
 };
 struct WPrepArgs {
   int count;
@@ -351,12 +352,21 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = 4 * l4 + e;
-      const int kx = i % w.ks;
-      int t = i / w.ks;
-      const int ky = t % w.ks;
-      t /= w.ks;
-      const int ci = t % w.ci;
-      const int co = t / w.ci;
+      int kx, ky, t;
+      if (w.ks == 3) {  // the 3x3 convs: divisions by constants (multiply-shift), not the runtime-divisor loop
+        t = i / 9;
+        const int r9 = i - 9 * t;
+        ky = r9 / 3;
+        kx = r9 - 3 * ky;
+      } else {
+        kx = i % w.ks;
+        t = i / w.ks;
+        ky = t % w.ks;
+        t /= w.ks;
+      }
+      // Cin a power of two (every HybridViT conv but Cin = 1 / 3): shift and mask
+      const int ci = w.ci_shift >= 0 ? (t & (w.ci - 1)) : t % w.ci;
+      const int co = w.ci_shift >= 0 ? (t >> w.ci_shift) : t / w.ci;
       const long o = w.kind != 2 ? (((long)co * w.ks + ky) * w.ks + kx) * w.ci + ci
                                  : (((long)ci * w.ks + (w.ks - 1 - ky)) * w.ks + (w.ks - 1 - kx)) * w.co + co;
       float x = v[e];
@@ -691,8 +701,9 @@ extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void*
                  "hvit_weight_prep: item %d: conv shape", base + k);
       HVIT_CHECK(aligned16(it.src) && (it.kind != 0 || aligned16(it.dst)), "hvit_weight_prep: item %d: alignment",
                  base + k);
+      const int cis = (it.cin > 0 && (it.cin & (it.cin - 1)) == 0) ? __builtin_ctz((unsigned)it.cin) : -1;
       a.it[k] = WPrepItem{it.src,   it.dst,  (int)(it.numel / 4), it.kind, it.dt,   it.cout, it.cin,
-                          it.ks,    it.gamma, it.beta,             it.rmean, it.rvar, it.bias, it.eps};
+                          it.ks,    it.gamma, it.beta,             it.rmean, it.rvar, it.bias, it.eps, cis};
       a.start[k + 1] = a.start[k] + (int)(it.numel / 4);
     }
     const int total = a.start[a.count];

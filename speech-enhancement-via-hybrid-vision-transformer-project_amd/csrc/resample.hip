@@ -290,8 +290,25 @@ __global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __rest
     if (iy >= Hi) break;  // (items are row-major: every later item is past the last row too)
     const int ix = rem / G, cg = rem - ix * G;
     float acc[CV];
+    TO* d = dx + ((size_t)(n * Hi + iy) * Wi + ix) * C + cg * CV;
+    // the accumulated-into gradient first: its load is independent of the taps
+    // (issued after the tap loop it waited behind the previous item's store)
+    if constexpr (CV == 8 && sizeof(TO) == 2) {
+      if (accumulate) {
+        const u32x4 u = *(const u32x4*)d;
 #pragma unroll
-    for (int e = 0; e < CV; ++e) acc[e] = 0.f;
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] = __uint_as_float(u[e] << 16);
+          acc[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < CV; ++e) acc[e] = 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < CV; ++e) acc[e] = accumulate ? Elem<TO>::to_f(d[e]) : 0.f;
+    }
     const int nx = xn[ix], ny = yn[r];
     for (int a = 0; a < ny; ++a) {
       const TI* row = dy + ((size_t)(n * Ho + yo[r][a]) * Wo) * C + cg * CV;
@@ -312,26 +329,14 @@ __global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __rest
         }
       }
     }
-    TO* d = dx + ((size_t)(n * Hi + iy) * Wi + ix) * C + cg * CV;
     if constexpr (CV == 8 && sizeof(TO) == 2) {
-      if (accumulate) {
-        const u32x4 u = *(const u32x4*)d;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[2 * e] += __uint_as_float(u[e] << 16);
-          acc[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
-        }
-      }
       u32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = f2bf2(acc[2 * e], acc[2 * e + 1]);
       *(u32x4*)d = o;
     } else {
 #pragma unroll
-      for (int e = 0; e < CV; ++e) {
-        const float v = acc[e] + (accumulate ? Elem<TO>::to_f(d[e]) : 0.f);
-        d[e] = Elem<TO>::from_f(v);
-      }
+      for (int e = 0; e < CV; ++e) d[e] = Elem<TO>::from_f(acc[e]);
     }
   }
 }

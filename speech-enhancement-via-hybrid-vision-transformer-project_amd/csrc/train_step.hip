@@ -179,14 +179,16 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
 }
 
 // ------------------------------------------------------- clip + AdamW ------
-constexpr int MT_MAX = 40;      // tensors per launch (kernel arguments by value)
+constexpr int MT_MAX = 40;      // tensors per AdamW launch (kernel arguments by value: 64 B per tensor)
+constexpr int SQ_MT_MAX = 128;  // tensors per sum-of-squares / scale launch (24 B per tensor: the whole
+                                // HybridViT in one launch; three launches of a third each were tail-bound)
 constexpr int SUMSQ_GRID = 1024; // partials per sum-of-squares launch
 
 struct SumsqArgs {
   int count;
-  long start[MT_MAX + 1];  // prefix sums of 4-element units (sum of squares: of SQ_TILE-unit tiles)
-  long n[MT_MAX];
-  const float* g[MT_MAX];
+  long start[SQ_MT_MAX + 1];  // prefix sums of 4-element units (sum of squares: of SQ_TILE-unit tiles)
+  long n[SQ_MT_MAX];
+  const float* g[SQ_MT_MAX];
 };
 
 // a unit = 4 consecutive elements of one tensor (the last unit of a tensor
@@ -454,7 +456,7 @@ extern "C" int hvit_loss_bwd(const float* pred, const float* tgt, int B, long lo
 }
 
 extern "C" long long hvit_clip_ws_elems(int count) {
-  return count <= 0 ? 0 : (long long)cdiv(count, MT_MAX) * SUMSQ_GRID;
+  return count <= 0 ? 0 : (long long)cdiv(count, SQ_MT_MAX) * SUMSQ_GRID;
 }
 
 static int fill_sumsq(SumsqArgs& a, const hvit_tensor_t* t, int base, int count, long per = 1) {
@@ -477,9 +479,9 @@ extern "C" int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_n
   HVIT_CHECK(count == 0 || (ws && ws_elems >= hvit_clip_ws_elems(count)), "hvit_clip_coef: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   int nparts = 0;
-  for (int base = 0; base < count; base += MT_MAX) {
+  for (int base = 0; base < count; base += SQ_MT_MAX) {
     SumsqArgs a;
-    if (int rc = fill_sumsq(a, grads, base, std::min(MT_MAX, count - base), SQ_TILE)) return rc;
+    if (int rc = fill_sumsq(a, grads, base, std::min(SQ_MT_MAX, count - base), SQ_TILE)) return rc;
     hipLaunchKernelGGL(sumsq_kernel, dim3(SUMSQ_GRID), dim3(256), 0, st, a, ws + nparts);
     HVIT_LAUNCH_CHECK();
     nparts += SUMSQ_GRID;
@@ -491,9 +493,9 @@ extern "C" int hvit_clip_coef(int count, const hvit_tensor_t* grads, float max_n
 
 extern "C" int hvit_scale_tensors(int count, const hvit_tensor_t* tensors, const float* coef, void* stream) {
   HVIT_CHECK(count >= 0 && (count == 0 || tensors) && coef, "hvit_scale_tensors: bad args");
-  for (int base = 0; base < count; base += MT_MAX) {
+  for (int base = 0; base < count; base += SQ_MT_MAX) {
     SumsqArgs a;
-    if (int rc = fill_sumsq(a, tensors, base, std::min(MT_MAX, count - base))) return rc;
+    if (int rc = fill_sumsq(a, tensors, base, std::min(SQ_MT_MAX, count - base))) return rc;
     hipLaunchKernelGGL(scale_kernel, dim3(grid_for_units(a.start[a.count], 2048)), dim3(256), 0,
                        (hipStream_t)stream, a, coef);
     HVIT_LAUNCH_CHECK();

@@ -136,7 +136,9 @@ def test_rccl_world1_bench_dp_branch():
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--steps", "3",
            "--warmup", "1", "--batch", "4", "--no-cpu-baseline"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-4000:]
+    # (the first error lines name the failing call; the tail holds the launcher's report)
+    errs = [ln for ln in r.stderr.splitlines() if "rror" in ln or "what()" in ln or "fault" in ln.lower()][:20]
+    assert r.returncode == 0, "\n".join(errs) + "\n...\n" + r.stderr[-2500:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     out = json.loads(line)
     assert out["config"]["dist_backend"] == "nccl"
