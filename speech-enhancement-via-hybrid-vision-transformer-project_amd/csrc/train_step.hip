@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const float* __restrict__
 }
 
 // ------------------------------------------------------- clip + AdamW ------
-constexpr int MT_MAX = 40;      // tensors per AdamW launch (kernel arguments by value: 64 B per tensor)
+constexpr int MT_MAX = 60;      // tensors per AdamW launch (kernel arguments by value: 64 B per tensor)
 constexpr int SQ_MT_MAX = 128;  // tensors per sum-of-squares / scale launch (24 B per tensor: the whole
                                 // HybridViT in one launch; three launches of a third each were tail-bound)
 constexpr int SUMSQ_GRID = 1024; // partials per sum-of-squares launch
@@ -277,6 +277,8 @@ struct AdamArgs {
   bf16_t* shadow[MT_MAX];
   const float* step[MT_MAX];  // device step counters (nullable: the host bias corrections)
 };
+
+static_assert(sizeof(AdamArgs) + 64 <= 4096, "adamw_kernel: kernel argument size");
 
 struct AdamHyper {
   float lr, beta1, beta2, eps, wd, bc1, bc2_sqrt;
@@ -519,9 +521,11 @@ extern "C" int hvit_adamw_dev(int count, const hvit_adamw_item_t* items, const h
   HVIT_CHECK(!host_bc || (hp->bc1 > 0.f && hp->bc2 > 0.f), "hvit_adamw: bias corrections must be positive");
   const AdamHyper h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, host_bc ? hp->bc1 : 1.f,
                     host_bc ? sqrtf(hp->bc2) : 1.f};
-  for (int base = 0; base < count; base += MT_MAX) {
+  // launches of equal tensor counts (104 HybridViT tensors: 52 + 52, not 60 + 44)
+  const int per = count > 0 ? cdiv(count, cdiv(count, MT_MAX)) : MT_MAX;
+  for (int base = 0; base < count; base += per) {
     AdamArgs a;
-    a.count = std::min(MT_MAX, count - base);
+    a.count = std::min(per, count - base);
     a.start[0] = 0;
     for (int k = 0; k < a.count; ++k) {
       const hvit_adamw_item_t& it = items[base + k];

@@ -10,8 +10,8 @@ betas, eps, weight_decay, amsgrad)`` in ``create_optimizer``
   one multi-tensor sum-of-squares launch + one finalize block + one scale
   launch, no host sync; returns the total norm as a 0-dim device tensor.
 * ``FusedAdamW`` -- torch.optim.AdamW's update rule (decoupled weight decay,
-  bias corrections, per-parameter ``step``) as one multi-tensor launch per 40
-  tensors.  With ``max_grad_norm`` the clip is fused: the update multiplies
+  bias corrections, per-parameter ``step``) as multi-tensor launches of at
+  most 60 tensors each, balanced (HybridViT's 104: two of 52).  With ``max_grad_norm`` the clip is fused: the update multiplies
   each gradient by the clip coefficient as it reads it (gradients are not
   rewritten; ``last_grad_norm`` holds the norm).  It also writes the bf16 copy
   of each updated linear weight that the next bf16 forward's GEMMs read
