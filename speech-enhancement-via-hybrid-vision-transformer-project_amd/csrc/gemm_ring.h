@@ -118,7 +118,13 @@ struct RingCore {
     for (int t = 0; t < NB - 1; ++t) issue(t);
     // a side job (epi_side) while the prologue stages are in flight
     epi_side(ep);
+#ifdef HVIT_GEMM_STAMPS
+    unsigned long long wait_cyc = 0, t_w0 = 0;
+#endif
     for (int t = 0; t < nk; ++t) {
+#ifdef HVIT_GEMM_STAMPS
+      t_w0 = __builtin_amdgcn_s_memtime();
+#endif
       // stage t landed for this wave (NB-2 younger stages stay in flight) ...
       __builtin_amdgcn_s_waitcnt(vm_imm((NB - 2) * INFL));
       asm volatile("" ::: "memory");
@@ -127,6 +133,9 @@ struct RingCore {
       // (t-1) % NB = (t+NB-1) % NB may be refilled: one barrier per stage
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#ifdef HVIT_GEMM_STAMPS
+      wait_cyc += __builtin_amdgcn_s_memtime() - t_w0;
+#endif
       const char* at = smem + (t % NB) * STAGE;
       const char* bt = at + IA::BYTES;
       u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
@@ -150,6 +159,12 @@ struct RingCore {
       lds_pin(fb1);
       mma(fa1, fb1);
     }
+#ifdef HVIT_GEMM_STAMPS
+    {  // wave 0's cycles spent in the per-stage wait + barrier (shader clock), slot 3
+      const unsigned bid_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+      if (threadIdx.x == 0 && bid_ < 65536) g_gemm_stamps[bid_ * 4 + 3] = wait_cyc;
+    }
+#endif
     // drain the trailing (never used) DMA and let every wave finish reading
     // before the epilogue reuses the ring
     __builtin_amdgcn_s_waitcnt(vm_imm(0));

@@ -31,6 +31,11 @@ def report(name, fn, nblk):
     end = (s[:, 2] - t0) * TICK_US
     q = lambda a: "min %5.1f med %5.1f max %5.1f" % (a.min(), np.median(a), a.max())  # noqa: E731
     print(f"{name:22s} start {q(st)} | K loop {q(k)} | epilogue {q(e)} | end {q(end)}", flush=True)
+    # slot 3: wave 0's shader cycles in the per-stage vmcnt wait + barrier (diagnostic build);
+    # as a share of the K loop via the in-kernel clock (cycles / wall of the same K loop)
+    w = s[:, 3]
+    print(f"{'':22s} K-loop wait+barrier: median {np.median(w):9.0f} cycles "
+          f"(~{np.median(w) / np.median(k) / 1e3:4.2f} GHz-us of a {np.median(k):4.1f} us K loop)", flush=True)
 
 
 def main():
