@@ -169,10 +169,19 @@ def _zs(ctx, n):
     return zslot(n) if any(ctx.needs_input_grad) else None
 
 
-# Per-forward cache of prepared weights, filled by prep_weights() with one
-# multi-tensor launch: (id(param), kind, dt) -> (param._version, tensor).  A
-# hit requires the parameter to be unmodified since preparation.
+# Cache of prepared weights, filled by prep_weights() with one multi-tensor
+# launch: (id(param), kind, dt) -> (param._version, tensor, param, BN
+# versions).  A lookup requires the parameter to be unmodified since
+# preparation.  Entries survive from one forward to the next only for
+# inference forwards (prep_weights(reuse=True): eval + no_grad, the caller
+# drops the cache on every train()/eval() switch) -- a captured training step
+# updates parameters without bumping their version counters, so training
+# forwards always re-prepare.
 _PREP = {}
+
+
+def prep_cache_clear() -> None:
+    _PREP.clear()
 
 
 def _prep_get(t, kind, dt):
@@ -180,6 +189,10 @@ def _prep_get(t, kind, dt):
     if hit is not None and hit[0] == t._version and hit[2] is t:
         return hit[1]
     return None
+
+
+def _bn_versions(bn):
+    return tuple(x._version for x in bn[:4]) + tuple(id(x) for x in bn[:4])
 
 
 # Persistent bf16 copies of linear weights ("shadows"): id(param) ->
@@ -202,16 +215,24 @@ def shadow_mark(p):
         e[2] = p._version
 
 
-def prep_weights(items, dev):
+def prep_weights(items, dev, reuse: bool = False):
     """items: [(param, kind, dt)] or, kind 3, [(param, 3, dt, (gamma, beta,
     running_mean, running_var, eps))]; kind 0 = cast, 1/2 = conv pack mode 0/1,
     3 = mode-0 pack with eval BatchNorm folded in (prepared value: (packed
     weight, f32 bias)).  Replaces the cache with freshly prepared copies (one
     kernel launch); bf16 casts whose shadow is current are reused without a
-    launch."""
+    launch, and with ``reuse`` (inference forwards) so is every entry still
+    current from the previous forward."""
+    old = dict(_PREP) if reuse else {}
     _PREP.clear()
     todo = []
     for w, kind, dt, *bn in items:
+        key = (id(w), kind, dt)
+        hit = old.get(key)
+        if (hit is not None and hit[2] is w and hit[0] == w._version and
+                (kind != 3 or hit[3] == _bn_versions(bn[0]))):
+            _PREP[key] = hit  # unchanged since it was prepared (repeated inference forwards)
+            continue
         if kind == 3:
             out = (_empty((w.numel(),), dt, dev), torch.empty(w.shape[0], dtype=torch.float32, device=dev))
             todo.append((w, kind, dt, out, bn[0]))
@@ -223,7 +244,7 @@ def prep_weights(items, dev):
             if e is None or e[0]() is not w or e[1].shape != w.shape:
                 e = _SHADOW[id(w)] = [weakref.ref(w), _empty(w.shape, dt, dev), None]
             if e[2] == w._version:
-                _PREP[(id(w), kind, dt)] = (w._version, e[1], w)
+                _PREP[(id(w), kind, dt)] = (w._version, e[1], w, None)
                 continue
             todo.append((w, kind, dt, e[1], None))
             continue
@@ -241,8 +262,8 @@ def prep_weights(items, dev):
         else:
             arr[i] = L.WPrepItem(w.data_ptr(), out.data_ptr(), w.numel(), kind, dt, co, ci, ks)
     call("hvit_weight_prep", len(todo), arr, stream_ptr())
-    for w, kind, dt, out, _ in todo:
-        _PREP[(id(w), kind, dt)] = (w._version, out, w)
+    for w, kind, dt, out, bn in todo:
+        _PREP[(id(w), kind, dt)] = (w._version, out, w, _bn_versions(bn) if kind == 3 else None)
         if kind == 0 and dt == BF16:
             shadow_mark(w)
 

@@ -375,6 +375,12 @@ class HybridViT(nn.Module):
         st = self.__dict__.get("_rng_state")
         return None if st is None else st.clone()
 
+    def train(self, mode: bool = True):
+        """nn.Module.train / eval; also drops the prepared-weight cache (inference
+        forwards reuse packed / BN-folded weights only within one eval period)."""
+        HF.prep_cache_clear()
+        return super().train(mode)
+
     def _prep_weights(self, dt: int, dev) -> None:
         """Cast / pack every weight this forward (and its backward) will use
         in one multi-tensor launch instead of one launch per weight."""
@@ -412,7 +418,7 @@ class HybridViT(nn.Module):
                 items.append((blk.conv.weight, 1, dt))
             if grads:
                 items.append((blk.conv.weight, 2, dt))
-        HF.prep_weights(items, dev)
+        HF.prep_weights(items, dev, reuse=fold)
 
     @staticmethod
     def _nhwc(t: torch.Tensor) -> torch.Tensor:

@@ -204,6 +204,40 @@ def test_inference_fusions_match_training_graph_path(hv):
     assert rel(y_fused.cpu(), y_plain.cpu()) < 5e-2
 
 
+def test_inference_reuses_prepared_weights_until_they_change(hv):
+    """Repeated inference forwards reuse the packed / BN-folded conv weights
+    (no weight-preparation launch after the first), bit-identical outputs; an
+    in-place change of a conv weight or of a BatchNorm running statistic is
+    seen by the next forward (it equals a fresh model's); a training step in
+    between (train() then eval()) drops the cache."""
+    import importlib
+
+    HF = importlib.import_module("hvit_amd.functional")
+    m = build(hv, {}, "bf16", False).eval()
+    g = golden("default_256")
+    x = torch.as_tensor(g["x"]).cuda()
+    with torch.no_grad():
+        y0 = m(x)
+        prepared = {k: v[1] for k, v in HF._PREP.items()}
+        y1 = m(x)
+        assert all(HF._PREP[k][1] is t for k, t in prepared.items())  # reused, not re-prepared
+        assert torch.equal(y0, y1)
+        m.encoder[1].conv.weight.mul_(1.25)
+        m.decoder[0].bn.running_var.mul_(2.0)
+        y2 = m(x)
+    fresh = build(hv, {}, "bf16", False).eval()
+    fresh.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        y3 = fresh(x)
+    assert not torch.equal(y2, y1)
+    assert torch.equal(y2, y3)
+    m.train()
+    assert not HF._PREP
+    m.eval()
+    with torch.no_grad():
+        assert torch.equal(m(x), y2)
+
+
 def test_autocast_selects_bf16(hv):
     m = build(hv, O.TINY, "auto", False).eval()
     x = torch.as_tensor(CF.spectrogram((2, 1, 64, 64), 5)).cuda()
