@@ -240,10 +240,282 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_kernel(const bf16_t* 
   }
 }
 
+// ============================================================================
+// Round-5 form (mhsa_fwd_fp8_v2): the same arithmetic -- the same e4m3
+// roundings, scales, mask and normaliser, so the emulation tests pin both --
+// with the bf16 v2 kernel's economy:
+//  * staging in units of 4 keys x 16 bytes: a thread converts its unit and
+//    writes K as 8-byte rows and V^T as one dword per d (a 4x4 byte transpose
+//    in registers by v_perm) instead of 16 single-byte LDS writes;
+//  * the d (k) order of the S^T MFMAs is per-lane contiguous (lane group g
+//    supplies d = 16g .. 16g + 15 to both MFMAs: any order both operands agree
+//    on sums the same), so a K fragment pair is one 16-byte LDS read;
+//  * the key order of the P V MFMA is the P registers' own (lane group g,
+//    register m, byte r <-> key 128kb + 16m + 4g + r): V^T is stored in that
+//    permuted key order, so a lane's 32 bytes of V^T are two 16-byte reads
+//    (row pitch 272 B: 16 lanes of a read phase hit disjoint banks);
+//  * 256 P comes out of the exponent (exp2(s c2 - max + 8)), the e4m3
+//    conversion needs no clamp (256 P <= 256 < 448), the block scale of P is
+//    2^0 and the normaliser is the sum of the 256 P values;
+//  * the dropout mask as selects from one hash per key pair.
+// ============================================================================
+constexpr int F8V_KP = 80;   // K image row pitch (64 e4m3 + 16 pad)
+constexpr int F8V_VP = 272;  // V^T image row pitch (256 keys + 16 pad)
+
+// position of key k in a V^T row (see above)
+__device__ __forceinline__ int f8v_pos(int k) {
+  return (k & ~127) + 32 * ((k >> 2) & 3) + 4 * ((k >> 4) & 7) + (k & 3);
+}
+// 4x4 byte transpose: o[e] = {w0.b_e, w1.b_e, w2.b_e, w3.b_e}
+__device__ __forceinline__ void bt4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t (&o)[4]) {
+  const uint32_t t0 = __builtin_amdgcn_perm(w1, w0, 0x05010400u), t1 = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
+  const uint32_t t2 = __builtin_amdgcn_perm(w3, w2, 0x05010400u), t3 = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+  o[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+  o[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+  o[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+  o[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+// 4 non-negative floats <= 448 -> 4 e4m3 bytes
+__device__ __forceinline__ int f8x4_pos(f32x4 p) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], w, true);
+}
+// |x| maximum of 8 bf16 as bf16 bits in both 16-bit halves' maximum: the sign
+// bits cleared, the magnitudes compared as unsigned integers two at a time
+// (v_pk_max_u16; finite non-negative bf16 order like their bit patterns)
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2_t amax_pk(u16x2_t m, const u32x4& u) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2_t, u[e] & 0x7fff7fffu));
+  return m;
+}
+__device__ __forceinline__ float amax_f(u16x2_t m) {
+  return __uint_as_float((uint32_t)(m.x > m.y ? m.x : m.y) << 16);
+}
+// 8 bf16 * 2^e -> 8 e4m3 bytes by the scaled conversion (v_cvt_scalef32_pk_fp8_bf16
+// divides by its scale operand -- measured, tools/probes/cvt_probe.hip -- and
+// rounds to nearest even like the emulation's float8_e4m3fn cast): inv = 2^-e
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t f8w(uint32_t a, uint32_t b, float inv) {
+  s16x2_t r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16((s16x2_t){0, 0}, __builtin_bit_cast(bf16x2v_t, a), inv, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2v_t, b), inv, true);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint2 f8_bf(const u32x4& u, float inv) {
+  return make_uint2(f8w(u[0], u[1], inv), f8w(u[2], u[3], inv));
+}
+// MFMA result -> VALU read distance on a taken branch edge (attention.hip v2_settle)
+__device__ __forceinline__ void f8_settle(f32x4& a) { asm volatile("s_nop 7\n\ts_nop 3" : "+v"(a)); }
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                             float* __restrict__ lse, int N, int H, float scale,
+                                                             uint32_t thr, float dscale, DSeed seed_, uint32_t site,
+                                                             uint32_t* __restrict__ kbits) {
+  const unsigned long long seed = seed_;
+  constexpr int NT = WAVES * 64;
+  constexpr int UPT = 1024 / NT;  // staging units (4 keys x 8 d of K or V) per thread
+  __shared__ __attribute__((aligned(16))) char Ks[F8_KMAX * F8V_KP];
+  __shared__ __attribute__((aligned(16))) char Vt[64 * F8V_VP];
+  __shared__ float red[2][WAVES];
+  const int D = H * 64;
+  const long pitch = 3L * D;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int frow = lane & 15, fq = lane >> 4;
+  const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
+  const uint64_t bh = (uint64_t)b * H + h;
+
+  // ---- this lane's query row: d = 16 fq .. 16 fq + 15 (both S^T MFMAs)
+  const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;
+  u32x4 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    qb[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 16 * fq + 8 * s2) : (u32x4){0u, 0u, 0u, 0u};
+  // ---- K / V units -> registers, per-tensor absmax
+  u32x4 ur[UPT][4];
+  float mk = 0.f, mv = 0.f;
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int u = tid + i * NT, tv = u >> 9, a = (u >> 3) & 63, dc = u & 7;
+    const bf16_t* src = base + (tv + 1) * D + dc * 8;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 4 * a + r;
+      ur[i][r] = key < N ? *(const u32x4*)(src + (long)key * pitch) : (u32x4){0u, 0u, 0u, 0u};
+    }
+    u16x2_t m2 = {0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m2 = amax_pk(m2, ur[i][r]);
+    const float m = amax_f(m2);
+    if (tv) mv = fmaxf(mv, m);
+    else mk = fmaxf(mk, m);
+  }
+  float mq = amax_f(amax_pk(amax_pk((u16x2_t){0, 0}, qb[0]), qb[1]));
+  mq = fmaxf(mq, __shfl_xor(mq, 16, 64));
+  mq = fmaxf(mq, __shfl_xor(mq, 32, 64));
+  mk = wave_max(mk);
+  mv = wave_max(mv);
+  if (lane == 0) {
+    red[0][w] = mk;
+    red[1][w] = mv;
+  }
+  __syncthreads();
+  mk = mv = 0.f;
+#pragma unroll
+  for (int i = 0; i < WAVES; ++i) {
+    mk = fmaxf(mk, red[0][i]);
+    mv = fmaxf(mv, red[1][i]);
+  }
+  const int ek = pow2_exp(mk), ev = pow2_exp(mv), eq = pow2_exp(mq);
+  const float sk = exp2i(ek), sq = exp2i(eq);
+  // ---- e4m3 images (values * 2^e stay <= 448: no saturation)
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int u = tid + i * NT, tv = u >> 9, a = (u >> 3) & 63, dc = u & 7;
+    if (!tv) {
+      const float ik = exp2i(-ek);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) *(uint2*)(Ks + (4 * a + r) * F8V_KP + dc * 8) = f8_bf(ur[i][r], ik);
+    } else {
+      const float iv = exp2i(-ev);
+      uint2 c[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) c[r] = f8_bf(ur[i][r], iv);
+      uint32_t lo[4], hi[4];
+      bt4(c[0].x, c[1].x, c[2].x, c[3].x, lo);  // d = 8 dc + 0..3
+      bt4(c[0].y, c[1].y, c[2].y, c[3].y, hi);  // d = 8 dc + 4..7
+      char* vcol = Vt + f8v_pos(4 * a);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        *(uint32_t*)(vcol + (8 * dc + e) * F8V_VP) = lo[e];
+        *(uint32_t*)(vcol + (8 * dc + 4 + e) * F8V_VP) = hi[e];
+      }
+    }
+  }
+  long q8[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) q8[s2] = __builtin_bit_cast(long, f8_bf(qb[s2], exp2i(-eq)));
+  __syncthreads();
+
+  const int nkt = (N + 15) >> 4;
+  const float c2 = scale * 1.4426950408889634f / (sq * sk);
+  // S^T tiles: st[j][r] = raw score(key 16j + 4fq + r, query q)
+  f32x4 st[F8_KMAX / 16];
+  float mx = -INFINITY;
+  const char* krow = Ks + frow * F8V_KP + 16 * fq;
+#pragma unroll
+  for (int j = 0; j < F8_KMAX / 16; ++j) {
+    if (j < nkt) {
+      const u32x4 kf = *(const u32x4*)(krow + 16 * j * F8V_KP);
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      a = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(__builtin_bit_cast(long, (uint2){kf[0], kf[1]}), q8[0], a, 0,
+                                                     0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(__builtin_bit_cast(long, (uint2){kf[2], kf[3]}), q8[1], a, 0,
+                                                     0, 0);
+      f8_settle(a);
+      if (16 * j + 16 > N) {  // wave-uniform: only a partial last tile
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, a[r]);
+      st[j] = a;
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float mxs = mx * c2;  // c2 > 0: the max commutes with the scale
+  const float off = 8.f - mxs;
+  float sum = 0.f;  // of 256 P (unrounded, undropped)
+#pragma unroll
+  for (int j = 0; j < F8_KMAX / 16; ++j) {
+    if (j < nkt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[j][r], c2, off));
+        st[j][r] = p;
+        sum += p;
+      }
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  f32x4 ot[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const uint32_t rk = rng_key(seed, site);
+  const uint64_t qrow = (bh * N + (q < N ? q : 0)) * (uint64_t)N;
+  unsigned long long kw = 0ull;  // bit 4j + r = keep(q, key 16j + 4fq + r)
+  const char* vrow = Vt + frow * F8V_VP + 32 * fq;
+#pragma unroll
+  for (int kb = 0; kb < F8_KMAX / 128; ++kb) {
+    if (128 * kb < N) {
+      i32x8 pb;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int j = 8 * kb + m;
+        f32x4 p = (j < nkt) ? st[j] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (thr && j < nkt) {
+          const uint64_t i0 = qrow + 16 * j + 4 * fq;
+          const uint32_t h0 = rng_pair(rk, i0), h1 = rng_pair(rk, i0 + 2);
+          const bool k0 = (h0 & 0xffffu) >= thr, k1 = (h0 >> 16) >= thr;
+          const bool k2 = (h1 & 0xffffu) >= thr, k3 = (h1 >> 16) >= thr;
+          p[0] = k0 ? p[0] : 0.f;
+          p[1] = k1 ? p[1] : 0.f;
+          p[2] = k2 ? p[2] : 0.f;
+          p[3] = k3 ? p[3] : 0.f;
+          kw |= (unsigned long long)((uint32_t)k0 | ((uint32_t)k1 << 1) | ((uint32_t)k2 << 2) | ((uint32_t)k3 << 3))
+                << (4 * j);
+        }
+        pb[m] = f8x4_pos(p);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const char* vr = vrow + 16 * t * F8V_VP + 128 * kb;
+        const u32x4 v0 = *(const u32x4*)vr, v1 = *(const u32x4*)(vr + 16);
+        const i32x8 va = {(int)v0[0], (int)v0[1], (int)v0[2], (int)v0[3],
+                          (int)v1[0], (int)v1[1], (int)v1[2], (int)v1[3]};
+        // scale_a = 2^-ev (undo V's scale), scale_b = 2^0 (the normaliser is the sum of 256 P)
+        ot[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(va, pb, ot[t], 0, 0, 0, 127 - ev, 0, 127);
+      }
+    }
+  }
+  if (q < N) {
+    bf16_t* op = o + ((long)b * N + q) * D + h * 64;
+    const float inv = 1.f / sum;
+    const float oinv = thr ? inv * dscale : inv;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint2 u;
+      u.x = f2bf2(ot[t][0] * oinv, ot[t][1] * oinv);
+      u.y = f2bf2(ot[t][2] * oinv, ot[t][3] * oinv);
+      *(uint2*)(op + 16 * t + 4 * fq) = u;
+    }
+    if (fq == 0) lse[bh * N + q] = (mxs - 8.f + log2f(sum)) * 0.6931471805599453f;
+    if (kbits && thr) *(uint2*)(kbits + ((bh * N + q) * 4 + fq) * 2) = make_uint2((uint32_t)kw, (uint32_t)(kw >> 32));
+  }
+}
+
+// 0: the round-4 kernel, 1: v2 with one 16-wave workgroup per (b, h), 2: v2 with
+// two 8-wave workgroups per (b, h) (hvit_gemm_tune(5, v) for A/B)
+int& fp8_form_ref() {
+  static int v = getenv("HVIT_FP8_FORM") ? atoi(getenv("HVIT_FP8_FORM")) : 1;
+  return v;
+}
+
 }  // namespace
 }  // namespace hvit
 
 using namespace hvit;
+
+int hvit_fp8_tune(int value) {
+  const int old = fp8_form_ref();
+  fp8_form_ref() = value;
+  return old;
+}
 
 extern "C" int hvit_mhsa_fwd_fp8_kb(const void* qkv, int B, int N, int H, int hd, float scale,
                                     const hvit_dropout_t* dropout, void* o, float* lse, unsigned* keep_bits,
@@ -259,12 +531,22 @@ extern "C" int hvit_mhsa_fwd_fp8_kb(const void* qkv, int B, int N, int H, int hd
   // the normaliser: no saturation for any dropout p
   const uint32_t thr = dropout ? drop_threshold(dropout->p) : 0;
   const float ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
-  // one 16-wave workgroup per (b, h) (measured faster than two 8-wave ones at
-  // config 5's B*H = 192: 24.4 vs 26.4 us per layer)
-  constexpr int WAVES = 16;
-  hipLaunchKernelGGL(mhsa_fwd_fp8_kernel<WAVES>, dim3(cdiv(N, 16 * WAVES), H, B), dim3(64 * WAVES), 0,
-                     (hipStream_t)stream, (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds,
-                     dseed(dropout), dropout ? dropout->site : 0u, keep_bits);
+  const int form = fp8_form_ref();
+  const uint32_t site = dropout ? dropout->site : 0u;
+  if (form == 2) {
+    hipLaunchKernelGGL(mhsa_fwd_fp8_v2<8>, dim3(cdiv(N, 128), H, B), dim3(512), 0, (hipStream_t)stream,
+                       (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dropout), site, keep_bits);
+  } else if (form == 1) {
+    hipLaunchKernelGGL(mhsa_fwd_fp8_v2<16>, dim3(cdiv(N, 256), H, B), dim3(1024), 0, (hipStream_t)stream,
+                       (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dropout), site, keep_bits);
+  } else {
+    // round 4: one 16-wave workgroup per (b, h) (measured faster than two 8-wave
+    // ones at config 5's B*H = 192: 24.4 vs 26.4 us per layer)
+    constexpr int WAVES = 16;
+    hipLaunchKernelGGL(mhsa_fwd_fp8_kernel<WAVES>, dim3(cdiv(N, 16 * WAVES), H, B), dim3(64 * WAVES), 0,
+                       (hipStream_t)stream, (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds,
+                       dseed(dropout), site, keep_bits);
+  }
   HVIT_LAUNCH_CHECK();
   return HVIT_OK;
 }

@@ -7,6 +7,7 @@ bool hvit_pp_fwd(const void* x, const void* w, int M, int N, int K, const hvit::
 bool hvit_pp_dgrad(const void* dy, const void* w, int M, int N, int K, const hvit::Epi& ep, hipStream_t st, int* rc);
 int hvit_pp_tune(int value);
 int hvit_attn_tune(int value);
+int hvit_fp8_tune(int value);  // attention_fp8.hip
 
 extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float* bias, int M, int N, int K,
                                void* y, int y_dt, const hvit_epilogue_t* epi, void* stream) {
@@ -252,6 +253,7 @@ extern "C" int hvit_gemm_tune(int what, int value) {
   if (what == 1) return hvit_c1_tune(value);
   if (what == 3) return hvit_pp_tune(value);  // persistent kernels: -1 auto, 0 off, 1 / 2 forced tile
   if (what == 4) return hvit_attn_tune(value);  // attention backward for N <= 256: 1 single pass, 0 two kernels
+  if (what == 5) return hvit_fp8_tune(value);  // fp8 attention forward: 0 round-4 kernel, 1 v2 16 waves, 2 v2 8 waves
   if (what == 2) {  // workgroup target of the linear weight gradients' split-K (0: default)
     const int old = (int)wg_target;
     wg_target = value > 0 ? value : 0;

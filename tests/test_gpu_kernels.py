@@ -961,6 +961,52 @@ def test_mhsa_fwd_fp8_keep_bits(hv, N, p):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("N,p", [(256, 0.1), (100, 0.0), (240, 0.3)])
+def test_mhsa_fwd_fp8_forms(hv, N, p):
+    """The fp8 forward's kernel forms (hvit_gemm_tune(5, form)): the v2 kernel
+    as one 16-wave and as two 8-wave workgroups per (b, h) bitwise equal (the
+    same per-query arithmetic), and v2 against the round-4 kernel (form 0) and
+    the e4m3 emulation: the same roundings in another summation order, so equal
+    to bf16-output rounding; keep bits identical across all three."""
+    l = L(hv)
+    torch.manual_seed(N + 1)
+    B, H, hd = 2, 12, 64
+    D = H * hd
+    qkv = torch.randn(B * N, 3 * D, device=DEV).to(torch.bfloat16)
+    dr = l.dropout(p, 55, 9)
+    nkb = l.lib().hvit_mhsa_keep_bits_elems(B, N, H)
+    res = {}
+    old = l.lib().hvit_gemm_tune(5, 1)
+    try:
+        for form in (0, 1, 2):
+            l.lib().hvit_gemm_tune(5, form)
+            o = torch.empty(B * N, D, device=DEV, dtype=torch.bfloat16)
+            lse = torch.empty(B, H, N, device=DEV)
+            kb = torch.full((nkb,), -1, dtype=torch.int32, device=DEV)
+            l.call("hvit_mhsa_fwd_fp8_kb", qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr, o.data_ptr(), lse.data_ptr(),
+                   kb.data_ptr(), s())
+            res[form] = (o, lse, kb)
+    finally:
+        l.lib().hvit_gemm_tune(5, old)
+    torch.cuda.synchronize()
+    assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][1], res[2][1])
+    if p > 0:
+        assert torch.equal(res[0][2], res[1][2]) and torch.equal(res[1][2], res[2][2])
+    t = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    keep = None
+    ds = 1.0
+    if p > 0:
+        ds = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+        keep = torch.as_tensor(keep_mask(55, 9, B * H * N * N, p).reshape(B, H, N, N), device=DEV).float()
+    emu = _attn_fp8_emulated(t[0], t[1], t[2], hd ** -0.5, keep, ds)
+    for form in (0, 1):
+        got = res[form][0].float().view(B, N, H, hd).permute(0, 2, 1, 3)
+        assert ((got - emu).norm() / emu.norm()).item() < 8e-3, form
+    d = (res[0][0].float() - res[1][0].float()).norm() / res[0][0].float().norm()
+    assert d.item() < 8e-3
+    assert (res[0][1] - res[1][1]).abs().max().item() < 1e-4
+
+
 def test_mhsa_fp8_forward_gradient_bound(hv):
     """The fp8 path's gradient (e4m3 forward, bf16 backward recomputing P from
     the fp8 forward's lse -- whose recomputed rows need not sum to exactly 1)

@@ -3,6 +3,8 @@ vectors recorded from the reference (tests/golden, via tools/gen_golden.py) and
 against the CPU oracle.  North-star bar: fp32 forward within 1e-3 relative of
 the reference; bf16 path within bf16 tolerances."""
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -12,6 +14,7 @@ from oracle import closed_form as CF
 from oracle import hvit_oracle as O
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 FP32_TOL = 1e-3      # north_star: forward within 1e-3 rel (fp32)
 BF16_TOL = 5e-2
@@ -490,6 +493,105 @@ def test_vit_backward_isolated(hv, kw):
         assert relnorm(got, r) < 1e-4, k
         n += 1
     assert n == 12 * cfg.num_layers + 5
+
+
+def _f8(x):
+    """round to OCP e4m3 (float8_e4m3fn) and back"""
+    return x.to(torch.float8_e4m3fn).to(x.dtype)
+
+
+def _pow2(amax):
+    """the fp8 kernel's power-of-two scale 2^floor(log2(448 / amax))"""
+    amax = amax.detach().float()
+    r = torch.where(amax > 0, 448.0 / amax.clamp_min(1e-30), torch.ones_like(amax))
+    return torch.exp2(torch.floor(torch.log2(r)))
+
+
+def _mhsa_fp8_emulated(sd, pfx, x, H, p_attn, p, training, want_attn=False):
+    """O.mhsa with the fp8 attention forward's roundings (attention_fp8.hip:
+    per-(b,h) K / V and per-query Q power-of-two scales, e4m3 q, k, v and
+    256 exp(s - max), normaliser from the unrounded sum) as straight-through
+    values: the backward sees the unrounded operands, as the bf16 backward of
+    the fp8 path does.  Dropout off (the test's configuration)."""
+    import torch.nn.functional as F
+    B, N, C = x.shape
+    hd = C // H
+    qkv = F.linear(x, sd[f"{pfx}.qkv.weight"], sd[f"{pfx}.qkv.bias"])
+    qkv = qkv.reshape(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    st = lambda t, r: t + (r - t).detach()  # noqa: E731
+    sq = _pow2(q.abs().amax(dim=3, keepdim=True)).to(q.dtype)
+    sk = _pow2(k.abs().amax(dim=(2, 3), keepdim=True)).to(k.dtype)
+    sv = _pow2(v.abs().amax(dim=(2, 3), keepdim=True)).to(v.dtype)
+    q8, k8, v8 = st(q, _f8(q * sq) / sq), st(k, _f8(k * sk) / sk), st(v, _f8(v * sv) / sv)
+    s = (q8 @ k8.transpose(-2, -1)).float() * (hd ** -0.5)
+    u = torch.exp(s - s.amax(-1, keepdim=True).detach())
+    o = (st(u, _f8(u * 256.0) / 256.0) @ v8.float()) / u.sum(-1, keepdim=True)
+    o = o.to(x.dtype).transpose(1, 2).reshape(B, N, C)
+    o = F.linear(o, sd[f"{pfx}.proj.weight"], sd[f"{pfx}.proj.bias"])
+    return o, None
+
+
+def test_large_config_fp8_train_step_grads(hv, monkeypatch):
+    """BASELINE config 5 train step (D=768 / 12 heads / 12 layers, bf16, dropout
+    off, B=4) with the fp8 attention forward: the loss and EVERY parameter
+    gradient per tensor (relative L2) against the fp32 CPU oracle.  Bars
+    calibrated as the bf16 B=32 test's: torch bf16 autocast of the oracle gives
+    the bf16 error e_tb, and the same with the attention core replaced by an
+    emulation of the fp8 forward's roundings (straight-through, bf16 backward)
+    gives the fp8 error e_t8; our bf16 path must stay within 2 e_tb + 1e-2 and
+    our fp8 path within 2 e_t8 + 1e-2 per tensor.  The per-group table goes to
+    gpurun_out/fp8_grad_calibration.json when HVIT_RECORD is set."""
+    import json
+    cfg = O.HViTConfig(**LARGE)
+    cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
+    shapes = O.state_dict_shapes(cfg)
+    W = CF.weights(shapes)
+    x = torch.as_tensor(CF.spectrogram((4, 1, 256, 256), 80))
+    t = torch.as_tensor(CF.spectrogram((4, 1, 256, 256), 81))
+    sd = O.make_state(shapes, W, requires_grad=True)
+    lo_t = O.combined_loss(O.forward(sd, x, cfg, training=True), t)
+    lo_t.backward()
+    lo = lo_t.item()
+    tgrads = {}
+    for name in ("bf16", "fp8"):
+        sdg = {k: v.detach().cuda().requires_grad_(v.requires_grad) for k, v in sd.items()}
+        with monkeypatch.context() as mp:
+            if name == "fp8":
+                mp.setattr(O, "mhsa", _mhsa_fp8_emulated)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                yb = O.forward(sdg, x.cuda(), cfg, training=True)
+            O.combined_loss(yb.float(), t.cuda()).backward()
+        tgrads[name] = {k: v.grad.detach().float().cpu() for k, v in sdg.items() if v.grad is not None}
+    table, bad = {}, []
+    for name in ("bf16", "fp8"):
+        m = hv.HybridViT(**cfg.as_kwargs(), precision="bf16",
+                        attention_precision="fp8" if name == "fp8" else None).cuda().train()
+        m.load_state_dict({k: torch.as_tensor(v) for k, v in W.items()}, strict=True)
+        loss = hv.CombinedLoss()(m(x.cuda()), t.cuda())
+        loss.backward()
+        torch.cuda.synchronize()
+        assert abs(loss.item() - lo) < 2e-2 * abs(lo), (name, loss.item(), lo)
+        for k, p in m.named_parameters():
+            assert p.grad is not None and torch.isfinite(p.grad).all(), (name, k)
+            got, ref, tb = p.grad.detach().cpu(), sd[k].grad, tgrads[name][k]
+            if k == "pos_encoding.pos_embed":
+                got, ref, tb = got[:, :256], ref[:, :256], tb[:, :256]
+            e, et = relnorm(got, ref), relnorm(tb, ref)
+            grp = k.split(".")[0] if not k.startswith("transformer.blocks") else "transformer." + k.split(".")[3]
+            cur = table.setdefault(name, {}).get(grp)
+            if cur is None or e > cur[0]:
+                table[name][grp] = (e, et, k)
+            if e > 2 * et + 1e-2:
+                bad.append((name, k, round(e, 4), round(et, 4)))
+    out = {n: {g: {"ours": v[0], "torch_emulation": v[1], "worst_tensor": v[2]} for g, v in d.items()}
+           for n, d in table.items()}
+    print("config 5 B=4 step, worst rel-L2 per group:", json.dumps(out, indent=1))
+    if os.environ.get("HVIT_RECORD"):
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "fp8_grad_calibration.json"), "w") as f:
+            json.dump({"loss_oracle": lo, "groups": out, "violations": bad}, f, indent=1)
+    assert not bad, bad
 
 
 def test_large_config_fp8_attention(hv):

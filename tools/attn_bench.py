@@ -56,6 +56,39 @@ def main(p=0.1):
         print(f"mhsa bwd_kb+bias p={p}: {us:7.1f} us  {2 * fl / us / 1e6:6.1f} TF/s", flush=True)
 
 
+def fp8_main(p=0.1):
+    """config 5's attention (B=16, N=256, H=12, hd=64): the bf16 forward against
+    the fp8 forms (hvit_gemm_tune(5, form): 0 round-4 kernel, 1 v2 16 waves,
+    2 v2 8 waves), keep-bit entry points (the training path)."""
+    B, N, H, hd = 16, 256, 12, 64
+    D = H * hd
+    qkv = (torch.randn(B * N, 3 * D, device="cuda") * 0.7).to(torch.bfloat16)
+    o = torch.empty(B * N, D, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device="cuda")
+    dr = L.dropout(p, 1, 2)
+    kb = torch.empty(L.lib().hvit_mhsa_keep_bits_elems(B, N, H), dtype=torch.int32, device="cuda")
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    fl = 4 * B * H * N * N * hd
+    fb = lambda: L.call("hvit_mhsa_fwd_kb", L.BF16, qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr,  # noqa
+                        o.data_ptr(), lse.data_ptr(), kb.data_ptr(), st())
+    us = timeit(fb)
+    print(f"config5 bf16 fwd_kb p={p}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s", flush=True)
+    f8 = lambda: L.call("hvit_mhsa_fwd_fp8_kb", qkv.data_ptr(), B, N, H, hd, hd ** -0.5, dr,  # noqa
+                        o.data_ptr(), lse.data_ptr(), kb.data_ptr(), st())
+    old = L.lib().hvit_gemm_tune(5, 1)
+    try:
+        for form in (0, 1, 2):
+            L.lib().hvit_gemm_tune(5, form)
+            us = timeit(f8)
+            print(f"config5 fp8 form {form} fwd_kb p={p}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s", flush=True)
+    finally:
+        L.lib().hvit_gemm_tune(5, old)
+
+
 if __name__ == "__main__":
-    main(0.1)
-    main(0.0)
+    if "--fp8" in sys.argv:
+        fp8_main(0.1)
+        fp8_main(0.0)
+    else:
+        main(0.1)
+        main(0.0)
