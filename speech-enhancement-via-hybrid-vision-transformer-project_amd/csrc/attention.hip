@@ -583,7 +583,9 @@ __device__ __forceinline__ f32x4 v2_keep(uint64_t bh, int N, int qi, int kj, uin
 // (running max and sum, the output rescaled when the max grows); for N <= 256
 // the one chunk gives exactly the single-pass arithmetic.  The KMAX = 512 form
 // runs 8-wave workgroups (at 16 waves the 128-VGPR budget spilled).
-template <int WAVES, int KMAX>
+// FULL: N == KMAX == 256 (the model's 16x16 token grid), every key tile whole
+// and every query in range: no partial-tile masks or tile-count tests.
+template <int WAVES, int KMAX, bool FULL = false>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int N, int H, float scale,
                                                          uint32_t thr, float dscale, DSeed seed_,
@@ -602,10 +604,11 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
   const int NK32 = (N + 31) & ~31;  // staged rows: whole tile pairs
   const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;  // this lane's query
+  const bool qin = FULL || q < N;
   u32x4 qf[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
-    qf[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
+    qf[s2] = qin ? *(const u32x4*)(base + (long)q * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
   v2_stage_glds<WAVES>(Ks, base + D, pitch, N, NK32);
   v2_stage_glds<WAVES>(Vs, base + 2 * D, pitch, N, NK32);
   __syncthreads();
@@ -613,7 +616,8 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   const uint64_t bh = (uint64_t)b * H + h;
   const uint64_t BHN = (uint64_t)gridDim.z * H * N;  // keep-bit chunk stride (queries)
   const uint32_t rk = rng_key(seed, site);
-  const uint64_t qrow = (bh * N + (q < N ? q : 0)) * (uint64_t)N;
+  const uint64_t qrow = (bh * N + (qin ? q : 0)) * (uint64_t)N;
+  const uint32_t hq = (uint32_t)(qrow >> 1) + 2u * (uint32_t)fq;  // dropout-hash pair index of key 0
   // O^T[d][q] += V^T[d][keys] P^T[keys][q]   (4 d-blocks of 16)
   f32x4 ot[4];
 #pragma unroll
@@ -623,7 +627,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
   // softmax update, P V; its keep bits
   auto chunk = [&](auto c0c) {
     constexpr int c0 = decltype(c0c)::value;
-    const int nkt = (min(N - c0, CH) + 15) >> 4;  // key tiles of this chunk
+    const int nkt = FULL ? CH / 16 : (min(N - c0, CH) + 15) >> 4;  // key tiles of this chunk
     const char* Kc = Ks + c0 * V2_ROWB;
     const char* Vc = Vs + c0 * V2_ROWB;
     // S^T tiles: st[j][r] = raw score(key c0 + 16j + 4fq + r, query q)
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
         a = v2_mma32(v2_fragj(Kc, LN, j, 0), qf[0], a);
         a = v2_mma32(v2_fragj(Kc, LN, j, 1), qf[1], a);
         v2_settle(a);
-        if (c0 + 16 * j + 16 > N) {  // wave-uniform: only a partial last tile
+        if (!FULL && c0 + 16 * j + 16 > N) {  // wave-uniform: only a partial last tile
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (c0 + 16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
@@ -695,8 +699,10 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             if (2 * jp + e < nkt) {
-              const uint64_t i0 = qrow + c0 + 32 * jp + 16 * e + 4 * fq;
-              const uint32_t h0 = rng_pair(rk, i0), h1 = rng_pair(rk, i0 + 2);
+              // rng_pair(rk, qrow + c0 + 32jp + 16e + 4fq) and (.. + 2) in 32 bits:
+              // qrow and the offset are even, so (qrow + off) >> 1 = qrow / 2 + off / 2
+              const uint32_t x0 = hq + (uint32_t)(c0 / 2 + 16 * jp + 8 * e);
+              const uint32_t h0 = hash32(rk ^ x0), h1 = hash32(rk ^ (x0 + 1u));
               const bool k0 = (h0 & 0xffffu) >= thr, k1 = (h0 >> 16) >= thr;
               const bool k2 = (h1 & 0xffffu) >= thr, k3 = (h1 >> 16) >= thr;
               f32x4& pp = e ? p1 : p0;
@@ -714,14 +720,14 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_v2(const bf16_t* __restri
         for (int t = 0; t < 4; ++t) ot[t] = v2_mma32(v2_trj2(Vc, LN, 2 * jp, t), pb, ot[t]);
       }
     }
-    if (q < N && kbits && thr)
+    if (qin && kbits && thr)
       *(uint2*)(kbits + (((uint64_t)(c0 / CH) * BHN + bh * N + q) * 4 + fq) * 2) = make_uint2(kb[0], kb[1]);
   };
   chunk(std::integral_constant<int, 0>());
   if constexpr (KMAX > CH) {
     if (N > CH) chunk(std::integral_constant<int, CH>());
   }
-  if (q < N) {
+  if (qin) {
     const float inv = 1.f / sum;
     const float os = thr ? inv * dscale : inv;
     bf16_t* op = o + ((long)b * N + q) * D + h * 64;
@@ -1465,6 +1471,7 @@ static int mhsa_fwd_impl(int dt, const void* qkv, int B, int N, int H, int hd, f
                          (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dr), dr ? dr->site : 0u, keep_bits);
     };
     if (v2_big(N)) go(mhsa_fwd_v2<8, 512>, 8);
+    else if (wv == 16 && N == 256) go(mhsa_fwd_v2<16, 256, true>, 16);
     else if (wv == 16) go(mhsa_fwd_v2<16, 256>, 16);
     else if (wv == 8) go(mhsa_fwd_v2<8, 256>, 8);
     else go(mhsa_fwd_v2<4, 256>, 4);

@@ -308,7 +308,8 @@ __device__ __forceinline__ uint2 f8_bf(const u32x4& u, float inv) {
 // MFMA result -> VALU read distance on a taken branch edge (attention.hip v2_settle)
 __device__ __forceinline__ void f8_settle(f32x4& a) { asm volatile("s_nop 7\n\ts_nop 3" : "+v"(a)); }
 
-template <int WAVES>
+// FULL: N == 256 (every key tile whole, every query in range)
+template <int WAVES, bool FULL>
 __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                              float* __restrict__ lse, int N, int H, float scale,
                                                              uint32_t thr, float dscale, DSeed seed_, uint32_t site,
@@ -329,10 +330,11 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
 
   // ---- this lane's query row: d = 16 fq .. 16 fq + 15 (both S^T MFMAs)
   const int q = blockIdx.x * WAVES * 16 + w * 16 + frow;
+  const bool qin = FULL || q < N;
   u32x4 qb[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
-    qb[s2] = q < N ? *(const u32x4*)(base + (long)q * pitch + 16 * fq + 8 * s2) : (u32x4){0u, 0u, 0u, 0u};
+    qb[s2] = qin ? *(const u32x4*)(base + (long)q * pitch + 16 * fq + 8 * s2) : (u32x4){0u, 0u, 0u, 0u};
   // ---- K / V units -> registers, per-tensor absmax
   u32x4 ur[UPT][4];
   float mk = 0.f, mv = 0.f;
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = 4 * a + r;
-      ur[i][r] = key < N ? *(const u32x4*)(src + (long)key * pitch) : (u32x4){0u, 0u, 0u, 0u};
+      ur[i][r] = FULL || key < N ? *(const u32x4*)(src + (long)key * pitch) : (u32x4){0u, 0u, 0u, 0u};
     }
     u16x2_t m2 = {0, 0};
 #pragma unroll
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
   for (int s2 = 0; s2 < 2; ++s2) q8[s2] = __builtin_bit_cast(long, f8_bf(qb[s2], exp2i(-eq)));
   __syncthreads();
 
-  const int nkt = (N + 15) >> 4;
+  const int nkt = FULL ? 16 : (N + 15) >> 4;
   const float c2 = scale * 1.4426950408889634f / (sq * sk);
   // S^T tiles: st[j][r] = raw score(key 16j + 4fq + r, query q)
   f32x4 st[F8_KMAX / 16];
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
       a = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(__builtin_bit_cast(long, (uint2){kf[2], kf[3]}), q8[1], a, 0,
                                                      0, 0);
       f8_settle(a);
-      if (16 * j + 16 > N) {  // wave-uniform: only a partial last tile
+      if (!FULL && 16 * j + 16 > N) {  // wave-uniform: only a partial last tile
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (16 * j + 4 * fq + r >= N) a[r] = -INFINITY;
@@ -447,20 +449,22 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
 #pragma unroll
   for (int t = 0; t < 4; ++t) ot[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const uint32_t rk = rng_key(seed, site);
-  const uint64_t qrow = (bh * N + (q < N ? q : 0)) * (uint64_t)N;
+  const uint64_t qrow = (bh * N + (qin ? q : 0)) * (uint64_t)N;
+  const uint32_t hq = (uint32_t)(qrow >> 1) + 2u * (uint32_t)fq;
   unsigned long long kw = 0ull;  // bit 4j + r = keep(q, key 16j + 4fq + r)
   const char* vrow = Vt + frow * F8V_VP + 32 * fq;
 #pragma unroll
   for (int kb = 0; kb < F8_KMAX / 128; ++kb) {
-    if (128 * kb < N) {
+    if (FULL || 128 * kb < N) {
       i32x8 pb;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         const int j = 8 * kb + m;
         f32x4 p = (j < nkt) ? st[j] : (f32x4){0.f, 0.f, 0.f, 0.f};
         if (thr && j < nkt) {
-          const uint64_t i0 = qrow + 16 * j + 4 * fq;
-          const uint32_t h0 = rng_pair(rk, i0), h1 = rng_pair(rk, i0 + 2);
+          // rng_pair(rk, qrow + 16j + 4fq) and (.. + 2): even terms, 32-bit pair index
+          const uint32_t x0 = hq + (uint32_t)(8 * j);
+          const uint32_t h0 = hash32(rk ^ x0), h1 = hash32(rk ^ (x0 + 1u));
           const bool k0 = (h0 & 0xffffu) >= thr, k1 = (h0 >> 16) >= thr;
           const bool k2 = (h1 & 0xffffu) >= thr, k3 = (h1 >> 16) >= thr;
           p[0] = k0 ? p[0] : 0.f;
@@ -483,7 +487,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
       }
     }
   }
-  if (q < N) {
+  if (qin) {
     bf16_t* op = o + ((long)b * N + q) * D + h * 64;
     const float inv = 1.f / sum;
     const float oinv = thr ? inv * dscale : inv;
@@ -533,12 +537,13 @@ extern "C" int hvit_mhsa_fwd_fp8_kb(const void* qkv, int B, int N, int H, int hd
   const float ds = (dropout && dropout->p > 0.f) ? 1.f / (1.f - dropout->p) : 1.f;
   const int form = fp8_form_ref();
   const uint32_t site = dropout ? dropout->site : 0u;
-  if (form == 2) {
-    hipLaunchKernelGGL(mhsa_fwd_fp8_v2<8>, dim3(cdiv(N, 128), H, B), dim3(512), 0, (hipStream_t)stream,
-                       (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dropout), site, keep_bits);
-  } else if (form == 1) {
-    hipLaunchKernelGGL(mhsa_fwd_fp8_v2<16>, dim3(cdiv(N, 256), H, B), dim3(1024), 0, (hipStream_t)stream,
-                       (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dropout), site, keep_bits);
+  if (form == 1 || form == 2) {
+    auto go = [&](auto kern, int waves) {
+      hipLaunchKernelGGL(kern, dim3(cdiv(N, 16 * waves), H, B), dim3(64 * waves), 0, (hipStream_t)stream,
+                         (const bf16_t*)qkv, (bf16_t*)o, lse, N, H, scale, thr, ds, dseed(dropout), site, keep_bits);
+    };
+    if (form == 2) N == 256 ? go(mhsa_fwd_fp8_v2<8, true>, 8) : go(mhsa_fwd_fp8_v2<8, false>, 8);
+    else N == 256 ? go(mhsa_fwd_fp8_v2<16, true>, 16) : go(mhsa_fwd_fp8_v2<16, false>, 16);
   } else {
     // round 4: one 16-wave workgroup per (b, h) (measured faster than two 8-wave
     // ones at config 5's B*H = 192: 24.4 vs 26.4 us per layer)
