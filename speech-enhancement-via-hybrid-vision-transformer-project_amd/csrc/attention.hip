@@ -1083,6 +1083,9 @@ __device__ __forceinline__ int fb_acc(int q, int c) { return q * 256 + ((c ^ (q 
 // units XOR-swizzled by row & 7
 __device__ __forceinline__ int fb_scr(int row, int unit) { return row * 64 + ((unit ^ (row & 7)) << 3); }
 
+// FULL: N == 256 (no row / tile range tests).  DM: the dropout form, 0 none,
+// 1 the forward's keep bits, 2 re-hashed (mhsa_dkv_v2's quad exchange).
+template <bool FULL, int DM>
 __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int N, int H, float scale,
@@ -1105,8 +1108,8 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
   const V2Lane LN(lane);
   const bf16_t* base = qkv + (long)b * N * pitch + h * 64;
   const bf16_t* dob = dout + (long)b * N * D + h * 64;
-  const int nqt = (N + 15) >> 4;
-  const int N32 = (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite copies)
+  const int nqt = FULL ? 16 : (N + 15) >> 4;
+  const int N32 = FULL ? 256 : (N + 31) & ~31;  // staged rows: whole tile pairs (rows >= N finite copies)
   const uint64_t bh = (uint64_t)b * H + h;
   // Q, dO and (into the dQ rows' space) K images of all rows
   v2_stage_glds<FB_WAVES>(Qs, base, pitch, N, N32);
@@ -1117,7 +1120,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const int key = 32 * w + 16 * kt + frow;
-    kv[kt] = key < N;
+    kv[kt] = FULL || key < N;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       kf[kt][s2] = kv[kt] ? *(const u32x4*)(base + D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
@@ -1129,7 +1132,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
   {
     const int qd = threadIdx.x >> 1, hf = threadIdx.x & 1;
     float dl = 0.f;
-    if (qd < N) {
+    if (FULL || qd < N) {
       const bf16_t* dp = dob + (long)qd * D + 32 * hf;
       const bf16_t* op = o + ((long)b * N + qd) * D + h * 64 + 32 * hf;
 #pragma unroll
@@ -1149,7 +1152,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
     }
   }
   // the forward's keep bits of this (b, h), transposed: Kb[word][query] (mhsa_dkv_v2's layout)
-  const bool use_kb = kbits && thr;
+  constexpr bool use_kb = DM == 1;
   if (use_kb)
     for (int i = threadIdx.x; i < N * 2; i += FB_WAVES * 64) {
       const u32x4 v = ((const u32x4*)(kbits + bh * N * 8))[i];
@@ -1186,7 +1189,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
 
   const float c2 = scale * 1.4426950408889634f;
   const uint32_t rk = rng_key(seed, site);
-  const bool wact = 32 * w < N;
+  const bool wact = FULL || 32 * w < N;
   f32x4 dkt[4][2], dvt[4][2];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -1194,12 +1197,12 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
     for (int kt = 0; kt < 2; ++kt) dkt[t][kt] = dvt[t][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < FB_WAVES; ++s) {
     const int j0 = 2 * ((w + s) & (FB_WAVES - 1));  // first query tile of this step's pair
-    if (wact && j0 < nqt) {                         // wave-uniform
+    if (wact && (FULL || j0 < nqt)) {               // wave-uniform
       f32x4 pd[2][2], dsv[2][2];                    // [query tile][key tile]
 #pragma unroll
       for (int bq = 0; bq < 2; ++bq) {
         const int j = j0 + bq;
-        if (j < nqt) {
+        if (FULL || j < nqt) {
           const u32x4 qa0 = v2_fragj(Qs, LN, j, 0), qa1 = v2_fragj(Qs, LN, j, 1);
           const u32x4 da0 = v2_fragj(Ds, LN, j, 0), da1 = v2_fragj(Ds, LN, j, 1);
           const f32x4 l4 = *(const f32x4*)(Ls + 16 * j + 4 * fq);
@@ -1214,18 +1217,19 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
             dp = v2_mma32(da1, vf[kt][1], dp);
             const int key = 32 * w + 16 * kt + frow;
             uint32_t hlo = 0u, hhi = 0u;
-            if (thr && !use_kb) {  // re-hash (mhsa_dkv_v2's quad exchange)
+            if (DM == 2) {  // re-hash (mhsa_dkv_v2's quad exchange)
               const int qc = 16 * j + 4 * fq + (frow & 3);
               const uint64_t idx = (bh * N + (qc < N ? qc : 0)) * (uint64_t)N + (key & ~3);
               hlo = rng_pair(rk, idx);
               hhi = rng_pair(rk, idx + 2);
             }
             u32x4 kw4 = {0u, 0u, 0u, 0u};
-            if (use_kb) kw4 = *(const u32x4*)(Kb + kword[kt] * FB_KBP + 16 * j + 4 * fq);
+            if (DM == 1) kw4 = *(const u32x4*)(Kb + kword[kt] * FB_KBP + 16 * j + 4 * fq);
             f32x4 p;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) p[r] = kv[kt] ? __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -l4[r])) : 0.f;
-            if (16 * j + 16 > N) {
+            for (int r = 0; r < 4; ++r)
+              p[r] = (FULL || kv[kt]) ? __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -l4[r])) : 0.f;
+            if (!FULL && 16 * j + 16 > N) {
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 if (16 * j + 4 * fq + r >= N) p[r] = 0.f;
@@ -1233,17 +1237,22 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float kp = 1.f;
-              if (use_kb) {
+              if constexpr (DM == 1) {
                 kp = ((kw4[r] >> kshift[kt]) & 1u) ? dscale : 0.f;
-              } else if (thr) {
+              } else if constexpr (DM == 2) {
                 const int src = (lane & ~3) | r;
                 const uint32_t lo = __shfl(hlo, src, 64), hi = __shfl(hhi, src, 64);
                 const uint32_t word = (key & 2) ? hi : lo;
                 const uint32_t u16 = (key & 1) ? (word >> 16) : (word & 0xffffu);
                 kp = u16 >= thr ? dscale : 0.f;
               }
-              pd[bq][kt][r] = p[r] * kp;
-              dsv[bq][kt][r] = p[r] * fmaf(dp[r], kp, -d4[r]);
+              if constexpr (DM == 0) {
+                pd[bq][kt][r] = p[r];
+                dsv[bq][kt][r] = p[r] * (dp[r] - d4[r]);
+              } else {
+                pd[bq][kt][r] = p[r] * kp;
+                dsv[bq][kt][r] = p[r] * fmaf(dp[r], kp, -d4[r]);
+              }
             }
           }
         } else {
@@ -1275,7 +1284,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
       // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q] into the pair's f32 rows (this step's owner)
 #pragma unroll
       for (int bq = 0; bq < 2; ++bq) {
-        if (j0 + bq < nqt) {
+        if (FULL || j0 + bq < nqt) {
           const int g = lane >> 4, li = lane & 15;
           v4s_t lo, hi;
           {
@@ -1298,7 +1307,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
   // dQ (bf16, x scale): two threads per query row
   {
     const int qd = threadIdx.x >> 1, hf = threadIdx.x & 1;
-    if (qd < N) {
+    if (FULL || qd < N) {
       bf16_t* dst = dqkv + ((long)b * N + qd) * pitch + h * 64 + 32 * hf;
 #pragma unroll
       for (int c = 0; c < 8; c += 2) {
@@ -1347,7 +1356,7 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
       const int row = 4 * i + (lane >> 4);
       const int key = 32 * w + row;
       const u32x4 v = *(const u32x4*)(Rw + row * 256 + ((c ^ (row & 15)) << 4));
-      if (key < N) *(u32x4*)(dqkv + ((long)b * N + key) * pitch + (c < 8 ? D : 2 * D - 64) + h * 64 + 8 * c) = v;
+      if (FULL || key < N) *(u32x4*)(dqkv + ((long)b * N + key) * pitch + (c < 8 ? D : 2 * D - 64) + h * 64 + 8 * c) = v;
     }
   }
   // k / v parts of the bias partial row from the register accumulators (keys >= N hold 0)
@@ -1510,9 +1519,21 @@ static int mhsa_bwd_impl(int dt, const void* qkv, const void* o, const void* dou
                          (const float*)delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site, keep_bits, dbias);
     };
     if (v2_fused(N)) {
-      hipLaunchKernelGGL(mhsa_bwd_fused, dim3(1, H, B), dim3(FB_WAVES * 64), 0, st, (const bf16_t*)qkv,
-                         (const bf16_t*)o, (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds,
-                         seed, site, keep_bits, dbias);
+      auto fb = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(1, H, B), dim3(FB_WAVES * 64), 0, st, (const bf16_t*)qkv, (const bf16_t*)o,
+                           (const bf16_t*)dout, lse, delta_ws, (bf16_t*)dqkv, N, H, scale, thr, ds, seed, site,
+                           keep_bits, dbias);
+      };
+      const int dm = !thr ? 0 : keep_bits ? 1 : 2;
+      if (N == 256) {
+        if (dm == 0) fb(mhsa_bwd_fused<true, 0>);
+        else if (dm == 1) fb(mhsa_bwd_fused<true, 1>);
+        else fb(mhsa_bwd_fused<true, 2>);
+      } else {
+        if (dm == 0) fb(mhsa_bwd_fused<false, 0>);
+        else if (dm == 1) fb(mhsa_bwd_fused<false, 1>);
+        else fb(mhsa_bwd_fused<false, 2>);
+      }
       HVIT_LAUNCH_CHECK();
       return HVIT_OK;
     }
