@@ -341,6 +341,44 @@ __global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __rest
   }
 }
 
+// The exact 2x downsample's backward (Hi = 2 Ho, Wi = 2 Wo: every input pixel is
+// sampled by one output pixel at weight 0.5 * 0.5, the skip resizes of the
+// encoder outputs onto the decoder grid), bf16, 8-channel groups: one thread
+// per (output pixel, channel group) scatters its 0.25 dy onto its 2x2 input
+// pixels -- each input pixel is written by exactly one thread, so this is the
+// gather form's arithmetic (acc = dx; acc += 0.25 * dy) without its tap tables
+// and per-item divisions.  blockIdx.y = n * Ho + oy; G = C / 8 a power of two.
+__global__ __launch_bounds__(256) void bilinear_bwd_half_kernel(const bf16_t* __restrict__ dy,
+                                                               bf16_t* __restrict__ dx, int Wo, int C, int gshift,
+                                                               int accumulate) {
+  const int r = blockIdx.y;
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= (Wo << gshift)) return;
+  const int ox = item >> gshift, cg = item & ((1 << gshift) - 1);
+  const u32x4 g = *(const u32x4*)(dy + ((long)r * Wo + ox) * C + cg * 8);
+  const long Wi = 2L * Wo;
+  bf16_t* d[4];
+  u32x4 old[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    d[q] = dx + ((2L * r + (q >> 1)) * Wi + 2 * ox + (q & 1)) * C + cg * 8;
+    old[q] = accumulate ? *(const u32x4*)d[q] : (u32x4){0u, 0u, 0u, 0u};
+  }
+  const float w = 0.25f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float lo = __uint_as_float(old[q][e] << 16), hi = __uint_as_float(old[q][e] & 0xffff0000u);
+      lo += w * __uint_as_float(g[e] << 16);
+      hi += w * __uint_as_float(g[e] & 0xffff0000u);
+      o[e] = f2bf2(lo, hi);
+    }
+    *(u32x4*)d[q] = o;
+  }
+}
+
 // dU [N, H*U, W*U, C1+C2] -> dx1 [N, H, W, C1], dx2 [N, H, W, C2] (sum over U x U)
 __global__ __launch_bounds__(256) void up_split_bwd_kernel(const void* du, int du_dt, int N, int H, int W, int U,
                                                           int C1, int C2, void* dx1, int dx1_dt, void* dx2,
@@ -453,6 +491,16 @@ extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int W
     while (rb < RB_MAXR && items * rb * 2 <= 256) rb *= 2;
     return rb;
   };
+  const int G8 = C / 8;
+  if (Hi == 2 * Ho && Wi == 2 * Wo && C % 8 == 0 && (G8 & (G8 - 1)) == 0 && dy_dt == HVIT_BF16 &&
+      dx_dt == HVIT_BF16 && aligned16(dy) && aligned16(dx) && (long)N * Ho < 65536) {
+    int gshift = 0;
+    while ((1 << gshift) < G8) ++gshift;
+    hipLaunchKernelGGL(bilinear_bwd_half_kernel, dim3(cdiv((long)Wo * G8, 256), N * Ho), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, Wo, C, gshift, accumulate);
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   if (rows_ok && C % 8 == 0 && dy_dt == HVIT_BF16 && aligned16(dy) && aligned16(dx)) {
     const int rb = rows_per_wg(8);
     hipLaunchKernelGGL((bilinear_bwd_rows_kernel<bf16_t, bf16_t, 8>), dim3(N * cdiv(Hi, rb)), dim3(256), 0,

@@ -705,6 +705,29 @@ def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
         assert rel(dxb.float(), 2 * refb) < 2e-2
 
 
+@pytest.mark.parametrize("N,Ho,Wo,C", [(32, 64, 64, 64), (32, 32, 32, 128), (32, 16, 16, 256), (2, 5, 7, 8),
+                                       (2, 6, 4, 24)])
+def test_bilinear_bwd_exact_half(hv, N, Ho, Wo, C):
+    """The skip resizes' backward (exact 2x downsample, bf16, accumulate into the
+    encoder output's gradient): each input pixel gets 0.25 dy of its one output
+    pixel, bit for bit as the gather arithmetic (dx + 0.25 dy in f32, one bf16
+    rounding); C / 8 = 3 takes the general path, checked the same way."""
+    l = L(hv)
+    torch.manual_seed(C + Ho)
+    Hi, Wi = 2 * Ho, 2 * Wo
+    gb = torch.randn(N, Ho, Wo, C, device=DEV).to(torch.bfloat16)
+    up = gb.float().repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+    dx = torch.full((N, Hi, Wi, C), 7.0, device=DEV, dtype=torch.bfloat16)
+    l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, dx.data_ptr(), l.BF16, 0, s())
+    torch.cuda.synchronize()
+    assert torch.equal(dx, (0.25 * up).to(torch.bfloat16))
+    base = torch.randn(N, Hi, Wi, C, device=DEV).to(torch.bfloat16)
+    acc = base.clone()
+    l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, acc.data_ptr(), l.BF16, 1, s())
+    torch.cuda.synchronize()
+    assert torch.equal(acc, (base.float() + 0.25 * up).to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("g_dt", ["bf16", "f32"])
 @pytest.mark.parametrize("M,D,p,rps", [(8192, 512, 0.1, 256), (37, 64, 0.3, 5), (300, 768, 0.0, 100)])
 def test_layernorm_bwd_drop_equals_two_passes(hv, g_dt, M, D, p, rps):
