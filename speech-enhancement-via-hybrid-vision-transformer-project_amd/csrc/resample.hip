@@ -341,27 +341,34 @@ __global__ __launch_bounds__(256) void bilinear_bwd_rows_kernel(const TI* __rest
   }
 }
 
-// The exact 2x downsample's backward (Hi = 2 Ho, Wi = 2 Wo: every input pixel is
-// sampled by one output pixel at weight 0.5 * 0.5, the skip resizes of the
-// encoder outputs onto the decoder grid), bf16, 8-channel groups: one thread
-// per (output pixel, channel group) scatters its 0.25 dy onto its 2x2 input
-// pixels -- each input pixel is written by exactly one thread, so this is the
-// gather form's arithmetic (acc = dx; acc += 0.25 * dy) without its tap tables
-// and per-item divisions.  blockIdx.y = n * Ho + oy; G = C / 8 a power of two.
-__global__ __launch_bounds__(256) void bilinear_bwd_half_kernel(const bf16_t* __restrict__ dy,
+// The backward of an exact even-factor downsample (Hi = k Ho, Wi = k Wo, k even:
+// the skip resizes of the encoder outputs onto the decoder grid, k = 2 and 4).
+// With align_corners=False output pixel o samples src = k o + (k - 1) / 2, i.e.
+// input pixels k o + k/2 - 1 and k o + k/2 at weight 0.5 each: every input
+// pixel is sampled by at most one output pixel, at weight 0.5 * 0.5 or not at
+// all.  bf16, 8-channel groups: one thread per (output pixel, channel group)
+// adds 0.25 dy to its 2x2 sampled input pixels (acc = dx; acc += 0.25 * dy in
+// f32, one bf16 rounding: the gather form's arithmetic) and, when not
+// accumulating, zeroes the rest of its k x k block (accumulating, those keep
+// their value, as the gather form rewrites them unchanged) -- no tap tables,
+// no per-item divisions, and at k = 4 a quarter of the input gradient's bytes.
+// blockIdx.y = n * Ho + oy; G = C / 8 a power of two.
+__global__ __launch_bounds__(256) void bilinear_bwd_down_kernel(const bf16_t* __restrict__ dy,
                                                                bf16_t* __restrict__ dx, int Wo, int C, int gshift,
-                                                               int accumulate) {
+                                                               int k, int accumulate) {
   const int r = blockIdx.y;
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= (Wo << gshift)) return;
   const int ox = item >> gshift, cg = item & ((1 << gshift) - 1);
   const u32x4 g = *(const u32x4*)(dy + ((long)r * Wo + ox) * C + cg * 8);
-  const long Wi = 2L * Wo;
+  const long Wi = (long)k * Wo;
+  const int h = k / 2 - 1;  // first sampled row / column of the block
+  bf16_t* blk = dx + ((long)k * r * Wi + (long)k * ox) * C + cg * 8;
   bf16_t* d[4];
   u32x4 old[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    d[q] = dx + ((2L * r + (q >> 1)) * Wi + 2 * ox + (q & 1)) * C + cg * 8;
+    d[q] = blk + ((h + (q >> 1)) * Wi + h + (q & 1)) * C;
     old[q] = accumulate ? *(const u32x4*)d[q] : (u32x4){0u, 0u, 0u, 0u};
   }
   const float w = 0.25f;
@@ -377,6 +384,11 @@ __global__ __launch_bounds__(256) void bilinear_bwd_half_kernel(const bf16_t* __
     }
     *(u32x4*)d[q] = o;
   }
+  if (!accumulate && k > 2)
+    for (int yy = 0; yy < k; ++yy)
+      for (int xx = 0; xx < k; ++xx)
+        if (yy - h < 0 || yy - h > 1 || xx - h < 0 || xx - h > 1)
+          *(u32x4*)(blk + (yy * Wi + xx) * C) = (u32x4){0u, 0u, 0u, 0u};
 }
 
 // dU [N, H*U, W*U, C1+C2] -> dx1 [N, H, W, C1], dx2 [N, H, W, C2] (sum over U x U)
@@ -491,13 +503,13 @@ extern "C" int hvit_bilinear_bwd(const void* dy, int dy_dt, int N, int Ho, int W
     while (rb < RB_MAXR && items * rb * 2 <= 256) rb *= 2;
     return rb;
   };
-  const int G8 = C / 8;
-  if (Hi == 2 * Ho && Wi == 2 * Wo && C % 8 == 0 && (G8 & (G8 - 1)) == 0 && dy_dt == HVIT_BF16 &&
-      dx_dt == HVIT_BF16 && aligned16(dy) && aligned16(dx) && (long)N * Ho < 65536) {
+  const int G8 = C / 8, kd = Hi / Ho;
+  if ((kd == 2 || kd == 4) && Hi == kd * Ho && Wi == kd * Wo && C % 8 == 0 && (G8 & (G8 - 1)) == 0 &&
+      dy_dt == HVIT_BF16 && dx_dt == HVIT_BF16 && aligned16(dy) && aligned16(dx) && (long)N * Ho < 65536) {
     int gshift = 0;
     while ((1 << gshift) < G8) ++gshift;
-    hipLaunchKernelGGL(bilinear_bwd_half_kernel, dim3(cdiv((long)Wo * G8, 256), N * Ho), dim3(256), 0,
-                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, Wo, C, gshift, accumulate);
+    hipLaunchKernelGGL(bilinear_bwd_down_kernel, dim3(cdiv((long)Wo * G8, 256), N * Ho), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)dy, (bf16_t*)dx, Wo, C, gshift, kd, accumulate);
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
   }

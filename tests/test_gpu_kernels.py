@@ -705,18 +705,25 @@ def test_bilinear(hv, N, Hi, Wi, C, Ho, Wo):
         assert rel(dxb.float(), 2 * refb) < 2e-2
 
 
-@pytest.mark.parametrize("N,Ho,Wo,C", [(32, 64, 64, 64), (32, 32, 32, 128), (32, 16, 16, 256), (2, 5, 7, 8),
-                                       (2, 6, 4, 24)])
-def test_bilinear_bwd_exact_half(hv, N, Ho, Wo, C):
-    """The skip resizes' backward (exact 2x downsample, bf16, accumulate into the
-    encoder output's gradient): each input pixel gets 0.25 dy of its one output
-    pixel, bit for bit as the gather arithmetic (dx + 0.25 dy in f32, one bf16
-    rounding); C / 8 = 3 takes the general path, checked the same way."""
+@pytest.mark.parametrize("N,Ho,Wo,C,k", [(32, 64, 64, 64, 2), (32, 32, 32, 128, 2), (32, 16, 16, 256, 2),
+                                         (2, 5, 7, 8, 2), (2, 6, 4, 24, 2), (32, 32, 32, 64, 4), (32, 16, 16, 128, 4),
+                                         (2, 3, 5, 16, 4), (2, 3, 5, 24, 4)])
+def test_bilinear_bwd_exact_down(hv, N, Ho, Wo, C, k):
+    """The skip resizes' backward (exact 2x / 4x downsample, bf16, accumulate into
+    the encoder output's gradient): output pixel o samples input pixels
+    k o + k/2 - 1 and k o + k/2 at 0.5 each, so those 2 x 2 pixels of every k x k
+    block get 0.25 dy and the others nothing -- bit for bit the gather
+    arithmetic (dx + 0.25 dy in f32, one bf16 rounding; untouched pixels keep
+    their value when accumulating, 0 otherwise); C / 8 = 3 takes the general
+    path, checked the same way."""
     l = L(hv)
-    torch.manual_seed(C + Ho)
-    Hi, Wi = 2 * Ho, 2 * Wo
+    torch.manual_seed(C + Ho + k)
+    Hi, Wi = k * Ho, k * Wo
     gb = torch.randn(N, Ho, Wo, C, device=DEV).to(torch.bfloat16)
-    up = gb.float().repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+    sel = torch.zeros(k, device=DEV)
+    sel[k // 2 - 1:k // 2 + 1] = 1.0
+    mask = (sel[:, None] * sel[None, :]).repeat(Ho, Wo)[None, :, :, None]
+    up = gb.float().repeat_interleave(k, dim=1).repeat_interleave(k, dim=2) * mask
     dx = torch.full((N, Hi, Wi, C), 7.0, device=DEV, dtype=torch.bfloat16)
     l.call("hvit_bilinear_bwd", gb.data_ptr(), l.BF16, N, Ho, Wo, C, Hi, Wi, dx.data_ptr(), l.BF16, 0, s())
     torch.cuda.synchronize()
