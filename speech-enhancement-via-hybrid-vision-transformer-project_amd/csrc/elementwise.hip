@@ -302,14 +302,14 @@ __global__ void sum_slabs4_kernel(const float* ws, int splits, int n4, float* ou
   }
 }
 
-// Multi-tensor weight preparation (one launch per forward instead of one per
-// weight): f32 master parameters -> bf16/f32 copies (kind 0) or conv packings
-// (kind 1: [Cout][KS][KS][Cin], kind 2: flipped [Cin][KS][KS][Cout], kind 3:
-// kind 1 with eval BatchNorm folded in, bn_fold_kernel's arithmetic with the
-// running statistics -- inference no longer spends an eval-prep and a fold
-// launch per conv block).  The flattened index space is split into 4-element
-// units (every item's numel is a multiple of 4); a thread locates its item in
-// the prefix table.
+// Multi-tensor weight preparation (one launch per forward per form instead of
+// one per weight): f32 master parameters -> bf16/f32 copies (kind 0) or conv
+// packings (kind 1: [Cout][KS][KS][Cin], kind 2: flipped [Cin][KS][KS][Cout],
+// kind 3: kind 1 with eval BatchNorm folded in, bn_fold_kernel's arithmetic
+// with the running statistics -- inference no longer spends an eval-prep and a
+// fold launch per conv block).  Casts: the flattened index space split into
+// 4-element units (every item's numel is a multiple of 4), a thread locating its
+// item in the prefix table; packings: weight_pack_tiled_kernel below.
 constexpr int WPREP_MAX = 24;
 struct WPrepItem {
   const float* src;
@@ -322,6 +322,7 @@ struct WPrepItem {
   float* bias;
   float eps;
   int ci_shift;  // log2(ci) when ci is a power of two, else -1
+  int co_shift;  // log2(co) when co is a power of two, else -1
 };
 struct WPrepArgs {
   int count;
@@ -330,7 +331,7 @@ struct WPrepArgs {
 };
 static_assert(sizeof(WPrepArgs) <= 4096, "weight_prep: kernel argument size");
 
-__global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
+__global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {  // kind 0: casts
   const int total = a.start[a.count];
   int j = 0;
   for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
@@ -338,43 +339,62 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(WPrepArgs a) {
     const WPrepItem& w = a.it[j];
     const int l4 = u - a.start[j];
     const f32x4 v = *(const f32x4*)(w.src + 4L * l4);
-    if (w.kind == 0) {
-      if (w.dt == HVIT_F32) {
-        *(f32x4*)((float*)w.dst + 4L * l4) = v;
-      } else {
-        uint2 o;
-        o.x = f2bf2(v[0], v[1]);
-        o.y = f2bf2(v[2], v[3]);
-        *(uint2*)((bf16_t*)w.dst + 4L * l4) = o;
-      }
-      continue;
+    if (w.dt == HVIT_F32) {
+      *(f32x4*)((float*)w.dst + 4L * l4) = v;
+    } else {
+      *(uint2*)((bf16_t*)w.dst + 4L * l4) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * l4 + e;
-      int kx, ky, t;
-      if (w.ks == 3) {  // the 3x3 convs: divisions by constants (multiply-shift), not the runtime-divisor loop
-        t = i / 9;
-        const int r9 = i - 9 * t;
-        ky = r9 / 3;
-        kx = r9 - 3 * ky;
-      } else {
-        kx = i % w.ks;
-        t = i / w.ks;
-        ky = t % w.ks;
-        t /= w.ks;
-      }
-      // Cin a power of two (every HybridViT conv but Cin = 1 / 3): shift and mask
-      const int ci = w.ci_shift >= 0 ? (t & (w.ci - 1)) : t % w.ci;
-      const int co = w.ci_shift >= 0 ? (t >> w.ci_shift) : t / w.ci;
-      const long o = w.kind != 2 ? (((long)co * w.ks + ky) * w.ks + kx) * w.ci + ci
-                                 : (((long)ci * w.ks + (w.ks - 1 - ky)) * w.ks + (w.ks - 1 - kx)) * w.co + co;
-      float x = v[e];
-      if (w.kind == 3) {
-        x *= w.gamma[co] * rsqrtf(w.rvar[co] + w.eps);
-        if (i < w.co) w.bias[i] = w.beta[i] - w.rmean[i] * (w.gamma[i] * rsqrtf(w.rvar[i] + w.eps));
-      }
-      st_dt(w.dst, o, x, w.dt);
+  }
+}
+
+// The conv packings tiled through LDS: one workgroup per output channel (kinds
+// 1 / 3: destination block [KS][KS][Cin] of that channel, contiguous; its source
+// [Cin][KS][KS] block read contiguously) or per input channel (kind 2: the
+// flipped [KS][KS][Cout] block; its source rows of KS*KS floats gathered), so
+// both the reads and the stores coalesce (the flat form above gathered or
+// scattered single elements: ~30 us for the model's 4.3 M conv weights x 2
+// packings).  start[] holds prefix sums of blocks; the same arithmetic per
+// element as the flat form.
+constexpr int WPT_MAXE = 40960;  // floats per block (Cin * KS * KS or Cout * KS * KS): 160 KiB of LDS
+__global__ __launch_bounds__(256) void weight_pack_tiled_kernel(WPrepArgs a) {
+  extern __shared__ float tile[];  // the launch's largest block
+  const int blk = blockIdx.x;
+  int j = 0;
+  while (blk >= a.start[j + 1]) ++j;  // uniform per workgroup
+  const WPrepItem& w = a.it[j];
+  const int b = blk - a.start[j];
+  const int K2 = w.ks * w.ks;
+  const int tid = threadIdx.x;
+  if (w.kind != 2) {  // b = output channel
+    const int n = w.ci * K2;
+    const float* src = w.src + (long)b * n;
+    for (int i = tid; i < n; i += 256) tile[i] = src[i];
+    __syncthreads();
+    float sc = 1.f;
+    if (w.kind == 3) {
+      sc = w.gamma[b] * rsqrtf(w.rvar[b] + w.eps);
+      if (tid == 0) w.bias[b] = w.beta[b] - w.rmean[b] * (w.gamma[b] * rsqrtf(w.rvar[b] + w.eps));
+    }
+    const long o0 = (long)b * n;
+    for (int o = tid; o < n; o += 256) {
+      const int ci = w.ci_shift >= 0 ? (o & (w.ci - 1)) : o % w.ci;
+      const int t = w.ci_shift >= 0 ? (o >> w.ci_shift) : o / w.ci;  // ky * KS + kx
+      float x = tile[ci * K2 + t];
+      if (w.kind == 3) x *= sc;
+      st_dt(w.dst, o0 + o, x, w.dt);
+    }
+  } else {  // b = input channel; destination [ky'][kx'][co], ky' = KS-1-ky, kx' = KS-1-kx
+    const int n = w.co * K2;
+    for (int i = tid; i < n; i += 256) {
+      const int co = i / K2, t = i - co * K2;
+      tile[i] = w.src[((long)co * w.ci + b) * K2 + t];
+    }
+    __syncthreads();
+    const long o0 = (long)b * n;
+    for (int o = tid; o < n; o += 256) {
+      const int co = w.co_shift >= 0 ? (o & (w.co - 1)) : o % w.co;
+      const int tf = w.co_shift >= 0 ? (o >> w.co_shift) : o / w.co;
+      st_dt(w.dst, o0 + o, tile[co * K2 + (K2 - 1 - tf)], w.dt);
     }
   }
 }
@@ -686,30 +706,55 @@ extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* o
 
 extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void* stream) {
   HVIT_CHECK(count >= 0 && (count == 0 || items), "hvit_weight_prep: bad args");
-  for (int base = 0; base < count; base += WPREP_MAX) {
+  // casts (kind 0) in the flat launch, packings (kinds 1-3) in the tiled one
+  for (int pass = 0; pass < 2; ++pass) {
     WPrepArgs a;
-    a.count = std::min(WPREP_MAX, count - base);
+    a.count = 0;
     a.start[0] = 0;
-    for (int k = 0; k < a.count; ++k) {
-      const hvit_wprep_item_t& it = items[base + k];
+    long maxe = 0;  // the tiled launch's largest block (floats)
+    auto flush = [&]() -> int {
+      const int total = a.start[a.count];
+      if (total > 0) {
+        if (pass == 0)
+          hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
+        else {
+          if (maxe * (long)sizeof(float) > 65536)
+            (void)hipFuncSetAttribute((const void*)weight_pack_tiled_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(maxe * sizeof(float)));
+          hipLaunchKernelGGL(weight_pack_tiled_kernel, dim3(total), dim3(256), maxe * sizeof(float),
+                             (hipStream_t)stream, a);
+        }
+        HVIT_LAUNCH_CHECK();
+      }
+      a.count = 0;
+      maxe = 0;
+      return HVIT_OK;
+    };
+    for (int k = 0; k < count; ++k) {
+      const hvit_wprep_item_t& it = items[k];
       HVIT_CHECK(it.src && it.dst && it.numel >= 0 && it.numel % 4 == 0 && it.numel < (1LL << 31),
-                 "hvit_weight_prep: item %d: null pointer or numel %% 4 != 0", base + k);
-      HVIT_CHECK(it.kind >= 0 && it.kind <= 3, "hvit_weight_prep: item %d: kind", base + k);
+                 "hvit_weight_prep: item %d: null pointer or numel %% 4 != 0", k);
+      HVIT_CHECK(it.kind >= 0 && it.kind <= 3, "hvit_weight_prep: item %d: kind", k);
       HVIT_CHECK(it.kind != 3 || (it.gamma && it.beta && it.rmean && it.rvar && it.bias),
-                 "hvit_weight_prep: item %d: BN fold needs gamma, beta, rmean, rvar, bias", base + k);
+                 "hvit_weight_prep: item %d: BN fold needs gamma, beta, rmean, rvar, bias", k);
       HVIT_CHECK(it.kind == 0 || (long long)it.cout * it.cin * it.ks * it.ks == it.numel,
-                 "hvit_weight_prep: item %d: conv shape", base + k);
-      HVIT_CHECK(aligned16(it.src) && (it.kind != 0 || aligned16(it.dst)), "hvit_weight_prep: item %d: alignment",
-                 base + k);
+                 "hvit_weight_prep: item %d: conv shape", k);
+      HVIT_CHECK(it.kind == 0 || ((long long)it.cin * it.ks * it.ks <= WPT_MAXE &&
+                                  (long long)it.cout * it.ks * it.ks <= WPT_MAXE),
+                 "hvit_weight_prep: item %d: conv block above %d elements", k, WPT_MAXE);
+      HVIT_CHECK(aligned16(it.src) && (it.kind != 0 || aligned16(it.dst)), "hvit_weight_prep: item %d: alignment", k);
+      if ((it.kind == 0) != (pass == 0)) continue;
       const int cis = (it.cin > 0 && (it.cin & (it.cin - 1)) == 0) ? __builtin_ctz((unsigned)it.cin) : -1;
-      a.it[k] = WPrepItem{it.src,   it.dst,  (int)(it.numel / 4), it.kind, it.dt,   it.cout, it.cin,
-                          it.ks,    it.gamma, it.beta,             it.rmean, it.rvar, it.bias, it.eps, cis};
-      a.start[k + 1] = a.start[k] + (int)(it.numel / 4);
+      const int cos = (it.cout > 0 && (it.cout & (it.cout - 1)) == 0) ? __builtin_ctz((unsigned)it.cout) : -1;
+      a.it[a.count] = WPrepItem{it.src,   it.dst,  (int)(it.numel / 4), it.kind, it.dt,   it.cout, it.cin,
+                                it.ks,    it.gamma, it.beta,             it.rmean, it.rvar, it.bias, it.eps, cis, cos};
+      const int units = pass == 0 ? (int)(it.numel / 4) : (it.kind == 2 ? it.cin : it.cout);
+      if (pass == 1) maxe = std::max(maxe, (long)(it.kind == 2 ? it.cout : it.cin) * it.ks * it.ks);
+      a.start[a.count + 1] = a.start[a.count] + units;
+      if (++a.count == WPREP_MAX)
+        if (int rc = flush()) return rc;
     }
-    const int total = a.start[a.count];
-    if (total == 0) continue;
-    hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
-    HVIT_LAUNCH_CHECK();
+    if (int rc = flush()) return rc;
   }
   return HVIT_OK;
 }

@@ -198,6 +198,33 @@ def pack(hv, w, mode, dt):
     return import_module("hvit_amd.functional").pack_conv(w, mode, hv._lib.F32 if dt == "f32" else hv._lib.BF16)
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+def test_weight_prep_packs_equal_conv_pack(hv, dt):
+    """The multi-tensor weight preparation (hvit_weight_prep: one launch per
+    forward) packs every conv shape of the model -- and odd ones (Cin / Cout not
+    powers of two, 2x2 patch kernels) -- exactly as hvit_conv_weight_pack does
+    (kinds 1 / 2), plain casts included (kind 0), all items in one launch."""
+    from importlib import import_module
+    HF = import_module("hvit_amd.functional")
+    l = L(hv)
+    dtc = l.F32 if dt == "f32" else l.BF16
+    torch.manual_seed(3)
+    shapes = [(64, 1, 3), (128, 64, 3), (256, 128, 3), (512, 256, 2), (256, 512, 3), (1, 64, 3), (24, 3, 3),
+              (12, 20, 2)]
+    ws = [torch.randn(co, ci, k, k, device=DEV) for co, ci, k in shapes]
+    lin = torch.randn(96, 40, device=DEV)
+    items = [(w, kind, dtc) for w in ws for kind in (1, 2)] + ([(lin, 0, dtc)] if dt == "bf16" else [])
+    HF.prep_weights(items, torch.device(DEV))
+    got = {(id(w), kind): HF._prep_get(w, kind, dtc).clone() for w, kind, _ in items}
+    HF.prep_cache_clear()
+    torch.cuda.synchronize()
+    for w in ws:
+        for kind in (1, 2):
+            assert torch.equal(got[(id(w), kind)], pack(hv, w, kind - 1, dt)), (tuple(w.shape), kind)
+    if dt == "bf16":
+        assert torch.equal(got[(id(lin), 0)].view(-1), lin.to(torch.bfloat16).view(-1))
+
+
 CONV_CASES = [
     # N, Hs, Ws, C1, C2, U, Cout, KS
     (2, 16, 16, 64, 0, 1, 128, 3),
