@@ -620,6 +620,47 @@ def test_layernorm(hv, dt, M, D):
 
 
 # ------------------------------------------------------------- batchnorm ---
+@pytest.mark.parametrize("M,C,tr", [(524288, 128, 128), (131072, 256, 128), (4096, 512, 64), (1000, 100, 128),
+                                    (300, 64, 512)])
+def test_bn_finalize_vs_torch(hv, M, C, tr):
+    """hvit_bn_finalize (chunk merges, then the final merge in a fixed order)
+    against torch's batch statistics from the same tile partials, the
+    running-stat update and num_batches_tracked, at the model's conv shapes and
+    ragged ones (partial last tile, partial channel block); three calls back to
+    back give bit-identical statistics."""
+    l = L(hv)
+    torch.manual_seed(C)
+    x = torch.randn(M, C, device=DEV, dtype=torch.float64) * 3 + torch.linspace(-2, 2, C, device=DEV, dtype=torch.float64)
+    nt = (M + tr - 1) // tr
+    pad = torch.zeros(nt * tr - M, C, device=DEV, dtype=torch.float64)
+    tiles = torch.cat([x, pad]).view(nt, tr, C)
+    cnt = torch.full((nt, 1), float(tr), device=DEV, dtype=torch.float64)
+    cnt[-1] = M - (nt - 1) * tr
+    tm = tiles.sum(1) / cnt
+    dev_ = torch.cat([x - tm.repeat_interleave(tr, 0)[:M], pad])
+    tq = (dev_.view(nt, tr, C) ** 2).sum(1)
+    part0 = torch.stack([tm, tq], -1).float().contiguous()
+    rm_ref, rv_ref = x.mean(0), x.var(0, unbiased=False)
+    outs = []
+    for _ in range(3):
+        part = part0.clone()
+        mean, inv = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        rmean, rvar = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+        l.call("hvit_bn_finalize", part.data_ptr(), nt, tr, M, C, mean.data_ptr(), inv.data_ptr(), rmean.data_ptr(),
+               rvar.data_ptr(), nbt.data_ptr(), 0.1, 1e-5, s())
+        torch.cuda.synchronize()
+        outs.append((mean, inv, rmean, rvar))
+        assert nbt.item() == 1
+    mean, inv, rmean, rvar = outs[0]
+    assert (mean.double() - rm_ref).abs().max().item() < 1e-5 * (1 + rm_ref.abs().max().item())
+    assert ((inv.double() - (rv_ref + 1e-5).rsqrt()).abs() / (rv_ref + 1e-5).rsqrt()).max().item() < 1e-5
+    assert (rmean.double() - 0.1 * rm_ref).abs().max().item() < 1e-5
+    unb = x.var(0, unbiased=True)
+    assert ((rvar.double() - (0.9 + 0.1 * unb)).abs() / (0.9 + 0.1 * unb)).max().item() < 1e-5
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("N,H,W,C,pool,p", [(2, 32, 32, 64, 2, 0.0), (3, 15, 17, 16, 2, 0.3),
                                             (2, 16, 16, 256, 1, 0.1), (1, 8, 8, 8, 1, 0.0)])
