@@ -244,6 +244,9 @@ def main():
         # visible GPUs round-robin) only rehearses the DP path on a one-GPU box
         backend = os.environ.get("HVIT_DIST_BACKEND", "nccl")
         if backend == "nccl":
+            # the step is captured with its bucket all-reduces: no event cache shared
+            # between eager and captured collectives (dp.NCCL_ENV)
+            os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:

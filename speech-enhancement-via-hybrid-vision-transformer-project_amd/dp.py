@@ -54,6 +54,7 @@ over xGMI; gloo works for CPU tests and for ranks that share one GPU.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Optional
 
 import weakref
@@ -62,6 +63,19 @@ import torch
 import torch.distributed as dist
 
 from . import functional as HF
+
+# Environment a process group that carries captured DP steps is created with.
+# TORCH_NCCL_CUDA_EVENT_CACHE=0: with torch's per-device CUDA-event cache (on by
+# default) an event of an eager collective still polled by the process group's
+# watchdog thread could be handed to a collective recorded inside a stream
+# capture, and the watchdog's next query of it fails ("operation not permitted
+# on an event last recorded in a capturing stream") and aborts the process --
+# seen twice in round 5 on RCCL world-1 runs that capture DP steps.  Applied as a
+# default when this module is imported (callers that create the process group
+# before importing it set the variable themselves; bench.py does).
+NCCL_ENV = {"TORCH_NCCL_CUDA_EVENT_CACHE": "0"}
+for _k, _v in NCCL_ENV.items():
+    os.environ.setdefault(_k, _v)
 
 
 _GLOO_GROUPS: Dict[tuple, object] = {}
