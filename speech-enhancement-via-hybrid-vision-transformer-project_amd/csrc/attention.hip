@@ -1128,29 +1128,16 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
           kv[kt] ? *(const u32x4*)(base + 2 * D + (long)key * pitch + 32 * s2 + 8 * fq) : (u32x4){0u, 0u, 0u, 0u};
     }
   }
-  // delta = rowsum(dO * O) (two threads per query), lse in log2 units
-  {
-    const int qd = threadIdx.x >> 1, hf = threadIdx.x & 1;
-    float dl = 0.f;
-    if (FULL || qd < N) {
-      const bf16_t* dp = dob + (long)qd * D + 32 * hf;
-      const bf16_t* op = o + ((long)b * N + qd) * D + h * 64 + 32 * hf;
+  // delta = rowsum(dO * O) (two threads per query): this thread's O half-row and
+  // lse now (in flight with the staging), its dO half-row from the staged image
+  // after the barrier below (dO is read from HBM once)
+  const int qd = threadIdx.x >> 1, hf = threadIdx.x & 1;
+  const bool qdv = FULL || qd < N;
+  u32x4 orow[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const u32x4 x = *(const u32x4*)(dp + 8 * c), y = *(const u32x4*)(op + 8 * c);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          dl += __uint_as_float(x[e] << 16) * __uint_as_float(y[e] << 16) +
-                __uint_as_float(x[e] & 0xffff0000u) * __uint_as_float(y[e] & 0xffff0000u);
-      }
-    }
-    dl += __shfl_xor(dl, 1, 64);
-    if (hf == 0) {
-      Dl[qd] = qd < N ? dl : 0.f;
-      Ls[qd] = qd < N ? lse[bh * N + qd] * 1.4426950408889634f : 0.f;
-      if (qd < N) delta[bh * N + qd] = dl;
-    }
-  }
+  for (int c = 0; c < 4; ++c)
+    orow[c] = qdv ? *(const u32x4*)(o + ((long)b * N + qd) * D + h * 64 + 32 * hf + 8 * c) : (u32x4){0u, 0u, 0u, 0u};
+  const float lq = (qdv && hf == 0) ? lse[bh * N + qd] * 1.4426950408889634f : 0.f;
   // the forward's keep bits of this (b, h), transposed: Kb[word][query] (mhsa_dkv_v2's layout)
   constexpr bool use_kb = DM == 1;
   if (use_kb)
@@ -1169,6 +1156,25 @@ __global__ __launch_bounds__(FB_WAVES * 64) void mhsa_bwd_fused(
     kshift[kt] = kbit & 31;
   }
   __syncthreads();
+  {
+    float dl = 0.f;
+    if (qdv) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const u32x4 x = *(const u32x4*)(Ds + v2_off(qd, 4 * hf + c)), y = orow[c];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          dl += __uint_as_float(x[e] << 16) * __uint_as_float(y[e] << 16) +
+                __uint_as_float(x[e] & 0xffff0000u) * __uint_as_float(y[e] & 0xffff0000u);
+      }
+    }
+    dl += __shfl_xor(dl, 1, 64);
+    if (hf == 0) {  // (read in the step loop, after the barriers below)
+      Dl[qd] = qdv ? dl : 0.f;
+      Ls[qd] = lq;
+      if (qdv) delta[bh * N + qd] = dl;
+    }
+  }
   // K^T of this wave's 32 keys as the A operand of dQ^T = K^T dS^T (keys 4g + e, 16 + 4g + e):
   // its K rows written from registers into a 4 KiB image (in the dQ rows' space, before they
   // are zeroed) and read back transposed
