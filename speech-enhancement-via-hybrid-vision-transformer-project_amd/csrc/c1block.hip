@@ -709,7 +709,9 @@ __global__ __launch_bounds__(THREADS) void c1m_sums_kernel(Args a_, const TD* __
     row[i] = red[i] + red[2 * a.C + i] + red[4 * a.C + i] + red[6 * a.C + i];
 }
 
-template <typename TD, int NCB>
+// FULL: even H and W, whole row chunks and whole group pairs (the model's
+// 256 x 256 input): no window / pixel range tests.
+template <typename TD, int NCB, bool FULL = false>
 __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __restrict__ dy,
                                                           const float* __restrict__ sums, int training,
                                                           float* __restrict__ part) {
@@ -751,11 +753,12 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
   // iteration (two groups) ahead
   auto issue = [&](int g, RawNcb<TD, NCB>& raw) {
     const int it = 4 * g + (l >> 4);
+    // (prefetches run past the block's last group: the window range test stays)
     const int itc = min(it, nwin - 1);
     int r, ox;
     win_rc(itc, Ww, r, ox);
     const int oy = oy0 + r;
-    if (it < nwin && oy < Ho && ox < Wo) raw.load(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c0);
+    if (it < nwin && (FULL || (oy < Ho && ox < Wo))) raw.load(dy + (((long)n * Ho + oy) * Wo + ox) * a.C + c0);
     else raw.zero();
   };
   RawNcb<TD, NCB> nxt[2];
@@ -773,8 +776,8 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
       f32x4 z[NCB];
       group_z<NCB>(xs, pitch, g, nwin, Ww, l, bw, z);
       const int it = 4 * g + (l >> 4);
-      const bool valid = it < nwin;
-      const int itc = min(it, nwin - 1);
+      const bool valid = FULL || it < nwin;
+      const int itc = FULL ? it : min(it, nwin - 1);
       int r, ox;
     win_rc(itc, Ww, r, ox);
       const int oy = oy0 + r;
@@ -783,7 +786,8 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
       // the lane's 4 pixels: inside the image and inside the block's windows?
       float inb[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) inb[q] = (valid && oy * 2 + (q >> 1) < a.H && ox * 2 + (q & 1) < a.W) ? 1.f : 0.f;
+      for (int q = 0; q < 4; ++q)
+        inb[q] = (FULL || (valid && oy * 2 + (q >> 1) < a.H && ox * 2 + (q & 1) < a.W)) ? 1.f : 0.f;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
         int arg;
@@ -794,7 +798,8 @@ __global__ __launch_bounds__(THREADS) void c1m_bwd_kernel(Args a_, const TD* __r
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float gq = arg == q ? gv : 0.f;
-          dz[q] = inb[q] * fmaf(cbz[cb], z[cb][q], fmaf(k.sc[cb], gq, ca[cb]));  // ca = cbz = 0 in eval
+          const float v = fmaf(cbz[cb], z[cb][q], fmaf(k.sc[cb], gq, ca[cb]));  // ca = cbz = 0 in eval
+          dz[q] = FULL ? v : inb[q] * v;
         }
         float lo[4];
 #pragma unroll
@@ -1140,7 +1145,12 @@ extern "C" int hvit_c1block_bwd(int dt, const hvit_conv_geom_t* g, const void* w
   if (mf) {
     with_ncb(C, [&](auto nc) {
       constexpr int NCB = decltype(nc)::value;
-      if (dy_dt == HVIT_BF16)
+      const int Ww = (a.W + pool - 1) / pool;
+      const bool full = pool == 2 && a.H % 2 == 0 && a.W % 2 == 0 && Hw % a.RB == 0 && (a.RB * Ww) % 8 == 0;
+      if (dy_dt == HVIT_BF16 && full)
+        hipLaunchKernelGGL((c1m_bwd_kernel<bf16_t, NCB, true>), dim3(blocks), dim3(THREADS), lds, st, a,
+                           (const bf16_t*)dy, sums, training, ws);
+      else if (dy_dt == HVIT_BF16)
         hipLaunchKernelGGL((c1m_bwd_kernel<bf16_t, NCB>), dim3(blocks), dim3(THREADS), lds, st, a, (const bf16_t*)dy,
                            sums, training, ws);
       else
