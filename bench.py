@@ -244,9 +244,6 @@ def main():
         # visible GPUs round-robin) only rehearses the DP path on a one-GPU box
         backend = os.environ.get("HVIT_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            # the step is captured with its bucket all-reduces: no event cache shared
-            # between eager and captured collectives (dp.NCCL_ENV)
-            os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -313,6 +310,9 @@ def main():
                 step()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if use_dist:
+            from hvit_amd.dp import quiesce_for_capture
+            quiesce_for_capture()  # the watchdog retires the warm-up collectives first
         graph = torch.cuda.CUDAGraph()
         # thread-local capture: under DP the process group's watchdog thread
         # polls the events of earlier collectives; in the default (global) mode

@@ -54,7 +54,6 @@ over xGMI; gloo works for CPU tests and for ranks that share one GPU.
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Dict, List, Optional
 
 import weakref
@@ -64,18 +63,25 @@ import torch.distributed as dist
 
 from . import functional as HF
 
-# Environment a process group that carries captured DP steps is created with.
-# TORCH_NCCL_CUDA_EVENT_CACHE=0: with torch's per-device CUDA-event cache (on by
-# default) an event of an eager collective still polled by the process group's
-# watchdog thread could be handed to a collective recorded inside a stream
-# capture, and the watchdog's next query of it fails ("operation not permitted
-# on an event last recorded in a capturing stream") and aborts the process --
-# seen twice in round 5 on RCCL world-1 runs that capture DP steps.  Applied as a
-# default when this module is imported (callers that create the process group
-# before importing it set the variable themselves; bench.py does).
-NCCL_ENV = {"TORCH_NCCL_CUDA_EVENT_CACHE": "0"}
-for _k, _v in NCCL_ENV.items():
-    os.environ.setdefault(_k, _v)
+# Before a DP step is captured: every earlier collective complete AND retired by
+# the process group's watchdog thread.  The watchdog polls each enqueued work's
+# end event (every ~100 ms) until it sees it complete; the bucket all-reduces
+# run on RCCL's internal stream, which the capture then joins, and a poll of an
+# event of that stream while it is being captured fails ("operation not
+# permitted on an event last recorded in a capturing stream") and aborts the
+# process -- seen intermittently in round 5 on RCCL world-1 runs whose capture
+# followed eager warm-up steps directly.  Synchronising and then waiting a few
+# watchdog periods lets the watchdog retire those works first.  Captured
+# collectives are not enqueued to the watchdog, and replays enqueue nothing.
+WATCHDOG_DRAIN_S = 0.35
+
+
+def quiesce_for_capture(device=None) -> None:
+    """Call right before capturing a step that contains collectives."""
+    import time
+    torch.cuda.synchronize(device)
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        time.sleep(WATCHDOG_DRAIN_S)
 
 
 _GLOO_GROUPS: Dict[tuple, object] = {}

@@ -140,7 +140,11 @@ class GraphedTrainStep:
         # capture (executes nothing), then replay it as this call's step
         e.x = noisy.detach().clone()
         e.t = clean.detach().clone()
-        torch.cuda.synchronize(noisy.device)
+        if self.reducer is not None:
+            from .dp import quiesce_for_capture
+            quiesce_for_capture(noisy.device)  # the watchdog retires the eager steps' collectives first
+        else:
+            torch.cuda.synchronize(noisy.device)
         g = torch.cuda.CUDAGraph()
         # thread-local capture: a data-parallel reducer's process-group watchdog
         # thread polls earlier collectives' events, which a global-mode capture

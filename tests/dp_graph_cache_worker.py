@@ -27,7 +27,6 @@ KW = dict(encoder_channels=[8, 16, 32], embed_dim=128, num_heads=2, num_layers=2
 def main():
     port = int(sys.argv[1])
     torch.cuda.set_device(0)
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # dp.NCCL_ENV
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     import importlib

@@ -27,7 +27,6 @@ KW = dict(encoder_channels=[8, 16, 32], embed_dim=128, num_heads=2, num_layers=2
 def main():
     port = int(sys.argv[1])
     torch.cuda.set_device(0)
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # dp.NCCL_ENV
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     import hvit_amd_loader
@@ -63,6 +62,8 @@ def main():
         for _ in range(2):
             step(ma, ra, oa)
     torch.cuda.current_stream().wait_stream(side)
+    from hvit_amd.dp import quiesce_for_capture
+    quiesce_for_capture()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph, capture_error_mode="thread_local"):  # (the watchdog thread polls events)
         static_loss = step(ma, ra, oa)
