@@ -308,6 +308,11 @@ __global__ __launch_bounds__(256) void c1_wgrad_kernel(const T* __restrict__ x, 
 }
 
 // --------------------------------------------------------------- Cout = 1 ---
+// the staged input strip of `pix` output pixels (taps reach W + 1 either way), whole KiB
+__host__ __device__ inline size_t o1_strip_bytes(int pix, int W, int C, size_t esz) {
+  return ((size_t)(pix + 2 * W + 2) * C * esz + 1023) / 1024 * 1024;
+}
+
 // y[p] = act(sum_{tap, ci} in[p + tap][ci] * w[tap][ci]); in = src upsampled by U
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void o1_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, TO* __restrict__ y,
@@ -334,6 +339,132 @@ __global__ __launch_bounds__(256) void o1_fwd_kernel(const T* __restrict__ x, co
     }
     if (act_tanh) s = tanhf(s);
     y[p] = Elem<TO>::from_f(s);
+  }
+}
+
+// The same for U == 1, bf16, CC = C / 8 <= 8 (the decoder's final 3x3 conv,
+// 64 -> 1): a workgroup's 256 output pixels, their input strip [p0 - W - 1,
+// pend + W + 1) staged once by LDS-DMA (as o1_wgrad_strip_kernel); thread
+// (pixel, channel chunk) sums its 9 taps x 8 channels with the weights in
+// registers, the CC chunks of a pixel (adjacent lanes) are added by shuffles.
+// The element-wise form above re-read every input vector once per tap from
+// L2 and spent three integer divisions per pixel (~24 us for 131k pixels).
+template <int CC>
+__global__ __launch_bounds__(256) void o1_fwd_strip_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                           void* __restrict__ y, int y_f32, int N, int H, int W,
+                                                           int act_tanh, int pix) {
+  extern __shared__ __attribute__((aligned(16))) char o1s[];
+  constexpr int C = CC * 8;
+  const int P = N * H * W;
+  const int p0 = blockIdx.x * pix, pend = min(P, p0 + pix);
+  const long base = (long)p0 - W - 1;
+  const int ns = (pend - p0) + 2 * W + 2;
+  {
+    constexpr int upp = C * 2 / 16;
+    const int nu = ns * upp;
+    const long u0 = base * upp, ulim = (long)P * upp;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(ulim * 16), 0x00020000);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i0 = wid * 64; i0 < nu; i0 += 256) {
+      const long q = u0 + i0 + lane;
+      const unsigned voff = (i0 + lane < nu && q >= 0 && q < ulim) ? (unsigned)(q * 16) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(o1s + (size_t)i0 * 16), 16,
+                                               voff, 0, 0, 0);
+    }
+  }
+  const int cc = threadIdx.x % CC, lg = threadIdx.x / CC;
+  constexpr int G = 256 / CC;
+  float wr[9][8];  // w packed [tap][ci]: this thread's chunk
+#pragma unroll
+  for (int t = 0; t < 9; ++t) Vec8<bf16_t>::load(w + t * C + cc * 8, wr[t]);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the strip
+  __syncthreads();
+  const bf16_t* xs = (const bf16_t*)o1s;
+  PixCursor pc(p0 + lg, H, W);
+  // (the CC lanes of a pixel share p: they leave the loop together, so the
+  // chunk shuffles below only meet active lanes)
+  for (int p = p0 + lg; p < pend; p += G, pc.advance(G, H, W)) {
+    float s = 0.f;
+    const bf16_t* c = xs + (size_t)(p - base) * C + cc * 8;
+    const bool up = pc.y > 0, dn = pc.y + 1 < H, lf = pc.x > 0, rt = pc.x + 1 < W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool ok = (dy < 0 ? up : dy > 0 ? dn : true) && (dx < 0 ? lf : dx > 0 ? rt : true);
+      if (!ok) continue;
+      float v[8];
+      Vec8<bf16_t>::load(c + (dy * W + dx) * C, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[e] * wr[t][e];
+    }
+#pragma unroll
+    for (int o = 1; o < CC; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (cc == 0) {
+      if (act_tanh) s = tanhf(s);
+      if (y_f32) ((float*)y)[p] = s;
+      else ((bf16_t*)y)[p] = f2bf(s);
+    }
+  }
+}
+
+// Form 2 of the strip forward: one thread per output pixel over all C channels
+// (no cross-lane sums: the chunk form's three dependent shuffles per pixel left
+// it latency-bound at two workgroups per CU); the weights as bf16 [tap][ci] in
+// LDS, read at one address by the whole wave.
+template <int CC>
+__global__ __launch_bounds__(256) void o1_fwd_px_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                        void* __restrict__ y, int y_f32, int N, int H, int W,
+                                                        int act_tanh, int pix) {
+  extern __shared__ __attribute__((aligned(16))) char o1s[];
+  constexpr int C = CC * 8;
+  const int P = N * H * W;
+  const int p0 = blockIdx.x * pix, pend = min(P, p0 + pix);
+  const long base = (long)p0 - W - 1;
+  const int ns = (pend - p0) + 2 * W + 2;
+  const size_t wofs = o1_strip_bytes(pix, W, C, 2);
+  {
+    constexpr int upp = C * 2 / 16;
+    const int nu = ns * upp;
+    const long u0 = base * upp, ulim = (long)P * upp;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(ulim * 16), 0x00020000);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i0 = wid * 64; i0 < nu; i0 += 256) {
+      const long q = u0 + i0 + lane;
+      const unsigned voff = (i0 + lane < nu && q >= 0 && q < ulim) ? (unsigned)(q * 16) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(o1s + (size_t)i0 * 16), 16,
+                                               voff, 0, 0, 0);
+    }
+  }
+  for (int i = threadIdx.x; i < 9 * CC; i += 256) ((u32x4*)(o1s + wofs))[i] = ((const u32x4*)w)[i];
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  const bf16_t* xs = (const bf16_t*)o1s;
+  const bf16_t* ws = (const bf16_t*)(o1s + wofs);
+  PixCursor pc(p0 + (int)threadIdx.x, H, W);
+  for (int p = p0 + threadIdx.x; p < pend; p += 256, pc.advance(256, H, W)) {
+    const bf16_t* c = xs + (size_t)(p - base) * C;
+    const bool up = pc.y > 0, dn = pc.y + 1 < H, lf = pc.x > 0, rt = pc.x + 1 < W;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool ok = (dy < 0 ? up : dy > 0 ? dn : true) && (dx < 0 ? lf : dx > 0 ? rt : true);
+      if (!ok) continue;
+#pragma unroll
+      for (int k = 0; k < CC; ++k) {
+        float v[8], wv[8];
+        Vec8<bf16_t>::load(c + (dy * W + dx) * C + 8 * k, v);
+        Vec8<bf16_t>::load(ws + t * C + 8 * k, wv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e & 3] += v[e] * wv[e];
+      }
+    }
+    float s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    if (act_tanh) s = tanhf(s);
+    if (y_f32) ((float*)y)[p] = s;
+    else ((bf16_t*)y)[p] = f2bf(s);
   }
 }
 
@@ -365,10 +496,52 @@ __global__ __launch_bounds__(256) void o1_dgrad_kernel(const TD* __restrict__ dz
   }
 }
 
-// part[blk][tap][ci] = sum_p dz[p] * in[p + tap][ci]
-__host__ __device__ inline size_t o1_strip_bytes(int pix, int W, int C, size_t esz) {
-  return ((size_t)(pix + 2 * W + 2) * C * esz + 1023) / 1024 * 1024;
+// The same for U == 1, bf16, CC <= 8: a workgroup's 256 input pixels, the dz
+// values their taps reach ([q0 - W - 1, qend + W + 1), f32) staged in LDS once;
+// thread (pixel, chunk) with its 9 x 8 weights in registers, one 16-byte store.
+template <int CC>
+__global__ __launch_bounds__(256) void o1_dgrad_strip_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ w,
+                                                             bf16_t* __restrict__ du, int N, int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) float dzs[];
+  constexpr int C = CC * 8;
+  const int P = N * H * W;
+  const int q0 = blockIdx.x * WG_PIX_O1, qend = min(P, q0 + WG_PIX_O1);
+  const long base = (long)q0 - W - 1;
+  const int ns = (qend - q0) + 2 * W + 2;
+  for (int i = threadIdx.x; i < ns; i += 256) {
+    const long q = base + i;
+    dzs[i] = (q >= 0 && q < P) ? bf2f(dz[q]) : 0.f;
+  }
+  const int cc = threadIdx.x % CC, lg = threadIdx.x / CC;
+  constexpr int G = 256 / CC;
+  // w: the dgrad (mode-1, flipped) packing [ci][ky'][kx'][co = 1]: tap t's weight of
+  // channel ci is w[ci * 9 + 8 - t] (o1_dgrad_kernel's table)
+  float wr[9][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wr[t][e] = bf2f(w[(cc * 8 + e) * 9 + 8 - t]);
+  __syncthreads();
+  PixCursor pc(q0 + lg, H, W);
+  for (int q = q0 + lg; q < qend; q += G, pc.advance(G, H, W)) {
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* c = dzs + (q - base);
+    // tap t reads dz at (y - dy, x - dx): inside the image?
+    const bool up = pc.y + 1 < H, dn = pc.y > 0, lf = pc.x + 1 < W, rt = pc.x > 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool ok = (dy < 0 ? up : dy > 0 ? dn : true) && (dx < 0 ? lf : dx > 0 ? rt : true);
+      if (!ok) continue;
+      const float d = c[-dy * W - dx];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += d * wr[t][e];
+    }
+    Vec8<bf16_t>::store(du + (size_t)q * C + cc * 8, o);
+  }
 }
+
+// part[blk][tap][ci] = sum_p dz[p] * in[p + tap][ci]
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void o1_wgrad_kernel(const T* __restrict__ x, const TD* __restrict__ dz,
                                                        float* __restrict__ part, int N, int Hs, int Ws, int U, int C) {
@@ -564,6 +737,44 @@ int hvit_thin_o1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, 
   const int C = g->C1;
   HVIT_CHECK(C % 8 == 0, "thin conv: Cin=%d must be a multiple of 8", C);
   const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
+  static const int fpix = getenv("HVIT_O1F_PIX") ? atoi(getenv("HVIT_O1F_PIX")) : WG_PIX_O1;  // A/B
+  const size_t sstrip = o1_strip_bytes(fpix, g->Ws, C, 2);
+  if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && sstrip <= 150 * 1024 && P * C * 2L < (1L << 31) &&
+      !getenv("HVIT_O1_FLAT")) {
+    const int nb = (int)((P + fpix - 1) / fpix);
+    auto go = [&](auto kern) {
+      allow_lds(kern, sstrip);
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(256), sstrip, st, (const bf16_t*)g->src1, (const bf16_t*)w, y,
+                         y_dt == HVIT_F32 ? 1 : 0, g->N, g->Hs, g->Ws, act_tanh, fpix);
+    };
+    static const int form = getenv("HVIT_O1F_FORM") ? atoi(getenv("HVIT_O1F_FORM")) : 1;  // A/B
+    if (form == 2) {
+      const size_t s2 = sstrip + 9 * C * 2;
+      auto go2 = [&](auto kern) {
+        allow_lds(kern, s2);
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(256), s2, st, (const bf16_t*)g->src1, (const bf16_t*)w, y,
+                           y_dt == HVIT_F32 ? 1 : 0, g->N, g->Hs, g->Ws, act_tanh, fpix);
+      };
+      switch (C / 8) {
+        case 1: go2(o1_fwd_px_kernel<1>); break;
+        case 2: go2(o1_fwd_px_kernel<2>); break;
+        case 4: go2(o1_fwd_px_kernel<4>); break;
+        case 8: go2(o1_fwd_px_kernel<8>); break;
+        default: goto flat;
+      }
+    } else {
+      switch (C / 8) {
+        case 1: go(o1_fwd_strip_kernel<1>); break;
+        case 2: go(o1_fwd_strip_kernel<2>); break;
+        case 4: go(o1_fwd_strip_kernel<4>); break;
+        case 8: go(o1_fwd_strip_kernel<8>); break;
+        default: goto flat;
+      }
+    }
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
+flat:
   const size_t smem = 9 * C * sizeof(float);
   dim3 grid((unsigned)std::min<long>((P + 255) / 256, 8192));
   if (dt == HVIT_BF16 && y_dt == HVIT_F32)
@@ -589,6 +800,24 @@ int hvit_thin_o1_dgrad(int dt, const hvit_conv_geom_t* g, const void* dz, const 
   const int H = g->Hs * g->U, W = g->Ws * g->U;
   const long total = (long)g->N * H * W * (C / 8);
   const size_t smem = 9 * C * sizeof(float);
+  if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && (64 % (C / 8)) == 0 && !getenv("HVIT_O1_FLAT")) {
+    const long P = (long)g->N * H * W;
+    const int nb = (int)((P + WG_PIX_O1 - 1) / WG_PIX_O1);
+    const size_t sd = sizeof(float) * (WG_PIX_O1 + 2 * W + 2);
+    HVIT_CHECK(sd <= 64 * 1024, "thin conv dgrad: W=%d too wide", W);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(256), sd, st, (const bf16_t*)dz, (const bf16_t*)w, (bf16_t*)du, g->N, H,
+                         W);
+    };
+    switch (C / 8) {
+      case 1: go(o1_dgrad_strip_kernel<1>); break;
+      case 2: go(o1_dgrad_strip_kernel<2>); break;
+      case 4: go(o1_dgrad_strip_kernel<4>); break;
+      default: go(o1_dgrad_strip_kernel<8>); break;
+    }
+    HVIT_LAUNCH_CHECK();
+    return HVIT_OK;
+  }
   dim3 grid((unsigned)std::min<long>((total + 255) / 256, 16384));
   if (dt == HVIT_BF16)
     hipLaunchKernelGGL((o1_dgrad_kernel<bf16_t, bf16_t>), grid, dim3(256), smem, st, (const bf16_t*)dz,
