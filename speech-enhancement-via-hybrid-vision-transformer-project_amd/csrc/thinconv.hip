@@ -408,66 +408,6 @@ __global__ __launch_bounds__(256) void o1_fwd_strip_kernel(const bf16_t* __restr
   }
 }
 
-// Form 2 of the strip forward: one thread per output pixel over all C channels
-// (no cross-lane sums: the chunk form's three dependent shuffles per pixel left
-// it latency-bound at two workgroups per CU); the weights as bf16 [tap][ci] in
-// LDS, read at one address by the whole wave.
-template <int CC>
-__global__ __launch_bounds__(256) void o1_fwd_px_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                        void* __restrict__ y, int y_f32, int N, int H, int W,
-                                                        int act_tanh, int pix) {
-  extern __shared__ __attribute__((aligned(16))) char o1s[];
-  constexpr int C = CC * 8;
-  const int P = N * H * W;
-  const int p0 = blockIdx.x * pix, pend = min(P, p0 + pix);
-  const long base = (long)p0 - W - 1;
-  const int ns = (pend - p0) + 2 * W + 2;
-  const size_t wofs = o1_strip_bytes(pix, W, C, 2);
-  {
-    constexpr int upp = C * 2 / 16;
-    const int nu = ns * upp;
-    const long u0 = base * upp, ulim = (long)P * upp;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)(ulim * 16), 0x00020000);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i0 = wid * 64; i0 < nu; i0 += 256) {
-      const long q = u0 + i0 + lane;
-      const unsigned voff = (i0 + lane < nu && q >= 0 && q < ulim) ? (unsigned)(q * 16) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(o1s + (size_t)i0 * 16), 16,
-                                               voff, 0, 0, 0);
-    }
-  }
-  for (int i = threadIdx.x; i < 9 * CC; i += 256) ((u32x4*)(o1s + wofs))[i] = ((const u32x4*)w)[i];
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  __syncthreads();
-  const bf16_t* xs = (const bf16_t*)o1s;
-  const bf16_t* ws = (const bf16_t*)(o1s + wofs);
-  PixCursor pc(p0 + (int)threadIdx.x, H, W);
-  for (int p = p0 + threadIdx.x; p < pend; p += 256, pc.advance(256, H, W)) {
-    const bf16_t* c = xs + (size_t)(p - base) * C;
-    const bool up = pc.y > 0, dn = pc.y + 1 < H, lf = pc.x > 0, rt = pc.x + 1 < W;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int dy = t / 3 - 1, dx = t % 3 - 1;
-      const bool ok = (dy < 0 ? up : dy > 0 ? dn : true) && (dx < 0 ? lf : dx > 0 ? rt : true);
-      if (!ok) continue;
-#pragma unroll
-      for (int k = 0; k < CC; ++k) {
-        float v[8], wv[8];
-        Vec8<bf16_t>::load(c + (dy * W + dx) * C + 8 * k, v);
-        Vec8<bf16_t>::load(ws + t * C + 8 * k, wv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e & 3] += v[e] * wv[e];
-      }
-    }
-    float s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    if (act_tanh) s = tanhf(s);
-    if (y_f32) ((float*)y)[p] = s;
-    else ((bf16_t*)y)[p] = f2bf(s);
-  }
-}
-
 // du[q][ci] = sum_tap dz[q - (tap - 1)] * w[tap][ci]   (q over the conv-input grid)
 template <typename T, typename TD>
 __global__ __launch_bounds__(256) void o1_dgrad_kernel(const TD* __restrict__ dz, const T* __restrict__ w,
@@ -737,7 +677,10 @@ int hvit_thin_o1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, 
   const int C = g->C1;
   HVIT_CHECK(C % 8 == 0, "thin conv: Cin=%d must be a multiple of 8", C);
   const long P = (long)g->N * g->Hs * g->U * g->Ws * g->U;
-  static const int fpix = getenv("HVIT_O1F_PIX") ? atoi(getenv("HVIT_O1F_PIX")) : WG_PIX_O1;  // A/B
+  // 128 output pixels per workgroup (1,024 workgroups at B = 32: four per CU overlap
+  // their strip loads with each other's sums): 14.7 us vs 15.8 at 256, 24.9 at 512;
+  // a thread-per-pixel form (no lane shuffles, weights from LDS) ran 15.7-17.1
+  static const int fpix = getenv("HVIT_O1F_PIX") ? atoi(getenv("HVIT_O1F_PIX")) : 128;
   const size_t sstrip = o1_strip_bytes(fpix, g->Ws, C, 2);
   if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && sstrip <= 150 * 1024 && P * C * 2L < (1L << 31) &&
       !getenv("HVIT_O1_FLAT")) {
@@ -747,29 +690,12 @@ int hvit_thin_o1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, 
       hipLaunchKernelGGL(kern, dim3(nb), dim3(256), sstrip, st, (const bf16_t*)g->src1, (const bf16_t*)w, y,
                          y_dt == HVIT_F32 ? 1 : 0, g->N, g->Hs, g->Ws, act_tanh, fpix);
     };
-    static const int form = getenv("HVIT_O1F_FORM") ? atoi(getenv("HVIT_O1F_FORM")) : 1;  // A/B
-    if (form == 2) {
-      const size_t s2 = sstrip + 9 * C * 2;
-      auto go2 = [&](auto kern) {
-        allow_lds(kern, s2);
-        hipLaunchKernelGGL(kern, dim3(nb), dim3(256), s2, st, (const bf16_t*)g->src1, (const bf16_t*)w, y,
-                           y_dt == HVIT_F32 ? 1 : 0, g->N, g->Hs, g->Ws, act_tanh, fpix);
-      };
-      switch (C / 8) {
-        case 1: go2(o1_fwd_px_kernel<1>); break;
-        case 2: go2(o1_fwd_px_kernel<2>); break;
-        case 4: go2(o1_fwd_px_kernel<4>); break;
-        case 8: go2(o1_fwd_px_kernel<8>); break;
-        default: goto flat;
-      }
-    } else {
-      switch (C / 8) {
-        case 1: go(o1_fwd_strip_kernel<1>); break;
-        case 2: go(o1_fwd_strip_kernel<2>); break;
-        case 4: go(o1_fwd_strip_kernel<4>); break;
-        case 8: go(o1_fwd_strip_kernel<8>); break;
-        default: goto flat;
-      }
+    switch (C / 8) {
+      case 1: go(o1_fwd_strip_kernel<1>); break;
+      case 2: go(o1_fwd_strip_kernel<2>); break;
+      case 4: go(o1_fwd_strip_kernel<4>); break;
+      case 8: go(o1_fwd_strip_kernel<8>); break;
+      default: goto flat;
     }
     HVIT_LAUNCH_CHECK();
     return HVIT_OK;
