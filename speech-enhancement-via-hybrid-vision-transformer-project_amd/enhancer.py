@@ -8,8 +8,10 @@ STFT / iSTFT framing stays on the host, as the north star says.  librosa is
 not available here, so the framing is ``torch.stft`` / ``torch.istft`` with the
 reference's settings (n_fft 512, hop 128, win 512, periodic Hann,
 center=True, constant padding -- librosa >= 0.10's ``pad_mode`` default;
-enhancer.py:82-89, :111-118).  That equivalence is not checked against
-librosa here (parity unpinned for the framing).  WAV I/O uses
+enhancer.py:82-89, :111-118).  tests/test_enhancer.py checks both against a
+numpy restatement of librosa 0.10's algorithm (oracle/stft_restated.py; an
+inconsistent spectrum for the iSTFT, ragged lengths); against librosa's own
+output the framing stays parity unpinned.  WAV I/O uses
 ``scipy.io.wavfile`` (soundfile is absent); files at another sample rate are
 refused rather than resampled.  The model call itself is the HIP path.
 """

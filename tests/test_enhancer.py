@@ -81,3 +81,44 @@ def test_load_model_for_inference_trainer_checkpoint(hv, tmp_path):
         assert torch.equal(a, b), k
     torch.save(src.state_dict(), tmp_path / "bare.pth")
     E.load_model_for_inference(tmp_path / "bare.pth", hv.HybridViT(**kw), device="cpu")
+
+
+# ---- the host framing against librosa 0.10's algorithm, restated -------------
+# (oracle/stft_restated.py; librosa itself is absent, so this pins the product's
+# torch.stft / torch.istft calls against the published algorithm, not against
+# librosa's output: the framing stays "parity unpinned" against the reference)
+
+@pytest.mark.parametrize("n", [32000, 4001, 511, 300])
+def test_stft_matches_restated_librosa(hv, n):
+    from hvit_amd import data as Dt
+    from hvit_amd import enhancer as E
+    from oracle import stft_restated as R
+
+    y = np.random.Generator(np.random.PCG64(n)).standard_normal(n).astype(np.float32)
+    ref = R.stft(y)
+    got = E.AudioEnhancer(Identity(), device="cpu").stft(y).numpy()
+    assert got.shape == ref.shape
+    tol = 1e-10 * np.abs(ref).max()
+    assert np.abs(got - ref).max() <= tol
+    # the training-data path (data.magnitude, f32) frames the same way
+    mag = Dt.magnitude(y).numpy()
+    assert mag.shape == ref.shape
+    assert np.abs(mag - np.abs(ref)).max() <= 2e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("n", [32000, 4001, 700])
+def test_istft_matches_restated_librosa(hv, n):
+    from hvit_amd import enhancer as E
+    from oracle import stft_restated as R
+
+    rng = np.random.Generator(np.random.PCG64(7 + n))
+    frames = 1 + n // 128
+    # an arbitrary (inconsistent) spectrum: exercises the overlap-add and the
+    # window-square normalisation, not just the analysis / synthesis round trip
+    spec = rng.standard_normal((257, frames)) + 1j * rng.standard_normal((257, frames))
+    spec[0].imag = 0.0
+    spec[-1].imag = 0.0
+    ref = R.istft(spec, length=n)
+    got = E.AudioEnhancer(Identity(), device="cpu").istft(torch.as_tensor(spec), n)
+    assert got.shape == ref.shape == (n,)
+    assert np.abs(got - ref).max() <= 1e-10 * np.abs(ref).max()
