@@ -38,8 +38,10 @@ enum {
   HVIT_ACT_MUL_AUX = 5,     /* GELU_BWD whose aux already holds gelu'(h): v *= aux */
   HVIT_ACT_RELU = 6,        /* conv forward only: v = max(v + bias, 0) (eval-mode BatchNorm folded) */
   HVIT_ACT_GELU = 7,        /* linear forward: y = dropout(gelu(v)) only (fc1 when no backward runs) */
-  HVIT_ACT_RELU_POOL2 = 8   /* conv forward only (bf16, even Ho / Wo, 64-channel-multiple sources): relu(v + bias)
+  HVIT_ACT_RELU_POOL2 = 8,  /* conv forward only (bf16, even Ho / Wo, 64-channel-multiple sources): relu(v + bias)
                                then 2x2 max-pool, y = [N, Ho/2, Wo/2, Cout] (eval BatchNorm folded, pooled block) */
+  HVIT_ACT_GELU_DUAL_DK = 9 /* GELU_DUAL_D storing dropout-mask * gelu'(v): the backward's MUL_AUX then needs no
+                               mask (pass no dropout there) */
 };
 /* flags of the backward calls that accumulate into caller memory:
  * HVIT_ACC_ZEROED says the caller already zeroed the accumulator outputs (one
@@ -81,7 +83,8 @@ typedef struct {
 /* Fused GEMM epilogue (applied in this order):
  *   v  = acc (+ bias[n]) (+ rowadd[(m % rowadd_rows) * N + n])
  *   GELU_DUAL: y = v (pre-activation); out2 = dropout(gelu(v))      -> stop
- *     (GELU_DUAL_D: y = gelu'(v) instead, the MUL_AUX operand of the backward)
+ *     (GELU_DUAL_D: y = gelu'(v) instead, the MUL_AUX operand of the backward;
+ *      GELU_DUAL_DK: y = keep * scale * gelu'(v), the dropout mask folded in)
  *   TANH: v = tanh(v) ; v = dropout(v) ; GELU_BWD: v *= gelu'(aux[m, n])
  *     (MUL_AUX: v *= aux[m, n])
  *   resid: v = resid[m, n] + rowscale[m / rows_per_sample] * v     (f32)

@@ -16,6 +16,7 @@ import torch
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU_DUAL, ACT_TANH, ACT_GELU_BWD, ACT_GELU_DUAL_D, ACT_MUL_AUX, ACT_RELU, ACT_GELU, ACT_RELU_POOL2 = (
     0, 1, 2, 3, 4, 5, 6, 7, 8)
+ACT_GELU_DUAL_DK = 9
 ACC_ZEROED = 1
 ACC_DEFER = 2
 

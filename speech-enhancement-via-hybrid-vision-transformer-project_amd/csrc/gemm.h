@@ -603,6 +603,10 @@ __device__ __forceinline__ void epi_apply4(const Epi& ep, uint32_t dkey, int m, 
     gelu_gg4(v, g, d);
 #pragma unroll
     for (int e = 0; e < 4; ++e) g[e] *= keep[e];
+    if (ep.gd == 2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] *= keep[e];
+    }
     if (ep.out) store4v<FAST>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, nv, ep.out_dt);
     store4v<FAST>(ep.out2, (long)m * ep.ldo2 + n, g, nv, ep.out2_dt);
     return;
@@ -1421,6 +1425,10 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           gelu_gg4(vb, gb, db);
           ga *= ka;
           gb *= kb;
+          if (ep.gd == 2) {  // GELU_DUAL_DK: the backward's multiplier carries the mask
+            da *= ka;
+            db *= kb;
+          }
           // (no out: the inference form, HVIT_ACT_GELU -- only gelu(v) is stored)
           if (ep.out) *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? wide8(da, db) : wide8(va, vb);
           *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = wide8(ga, gb);
@@ -1609,6 +1617,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
           f32x4 g, d;
           gelu_gg4(v, g, d);
           g *= k;
+          if (ep.gd == 2) d *= k;  // GELU_DUAL_DK
           if (ep.out) store4v<true>(ep.out, (long)m * ep.ldo + n, ep.gd ? d : v, 4, ep.out_dt);
           store4v<true>(ep.out2, (long)m * ep.ldo2 + n, g, 4, ep.out2_dt);
         }

@@ -27,8 +27,11 @@ Epi to_epi(const hvit_epilogue_t* e, void* out, int out_dt, long ldo) {
   ep.ldo = ldo;
   if (!e) return ep;
   // GELU_DUAL_D / MUL_AUX: GELU_DUAL / GELU_BWD with gelu'(h) in place of h
-  ep.act = e->act == HVIT_ACT_GELU_DUAL_D ? HVIT_ACT_GELU_DUAL : e->act == HVIT_ACT_MUL_AUX ? HVIT_ACT_GELU_BWD : e->act;
-  ep.gd = e->act == HVIT_ACT_GELU_DUAL_D || e->act == HVIT_ACT_MUL_AUX;
+  // (GELU_DUAL_DK: gd = 2, the stored gelu'(h) carries the dropout multiplier)
+  ep.act = (e->act == HVIT_ACT_GELU_DUAL_D || e->act == HVIT_ACT_GELU_DUAL_DK) ? HVIT_ACT_GELU_DUAL
+           : e->act == HVIT_ACT_MUL_AUX                                      ? HVIT_ACT_GELU_BWD
+                                                                              : e->act;
+  ep.gd = e->act == HVIT_ACT_GELU_DUAL_DK ? 2 : (e->act == HVIT_ACT_GELU_DUAL_D || e->act == HVIT_ACT_MUL_AUX);
   if (e->act == HVIT_ACT_RELU || e->act == HVIT_ACT_RELU_POOL2) {  // flags of the plain-store epilogue
     ep.act = HVIT_ACT_NONE;
     ep.relu = 1;
@@ -85,8 +88,8 @@ int take_side(const hvit_slab_sum_t* jp, Epi& ep, int M, hipStream_t st) {
 
 int check_epi(const hvit_epilogue_t* e) {
   if (!e) return HVIT_OK;
-  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_RELU_POOL2, "epilogue: bad act %d", e->act);
-  HVIT_CHECK((e->act != HVIT_ACT_GELU_DUAL && e->act != HVIT_ACT_GELU_DUAL_D) || e->out2,
+  HVIT_CHECK(e->act >= HVIT_ACT_NONE && e->act <= HVIT_ACT_GELU_DUAL_DK, "epilogue: bad act %d", e->act);
+  HVIT_CHECK((e->act != HVIT_ACT_GELU_DUAL && e->act != HVIT_ACT_GELU_DUAL_D && e->act != HVIT_ACT_GELU_DUAL_DK) || e->out2,
              "epilogue: GELU_DUAL needs out2");
   HVIT_CHECK((e->act != HVIT_ACT_GELU_BWD && e->act != HVIT_ACT_MUL_AUX) || e->aux, "epilogue: GELU_BWD needs aux");
   HVIT_CHECK(!(e->dropout.p < 0.f || e->dropout.p >= 1.f), "epilogue: dropout p out of range");

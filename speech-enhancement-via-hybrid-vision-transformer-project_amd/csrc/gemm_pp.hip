@@ -259,6 +259,10 @@ __device__ __forceinline__ static void run(const LdDense<bf16_t, true>& la, cons
       gelu_gg4(vb8, gb, ddb);
       ga *= ka;
       gb *= kb;
+      if (ep.gd == 2) {  // GELU_DUAL_DK
+        dda *= ka;
+        ddb *= kb;
+      }
       st16(ep.gd ? pack8(dda, ddb) : pack8(va8, vb8), rout, (unsigned)(((long)m * ep.ldo + n) * 2) | kill);
       st16(pack8(ga, gb), rout2, (unsigned)(((long)m * ep.ldo2 + n) * 2) | kill);
     } else {  // K_GELU_BWD: v *= keep * gelu'(h)  (aux = gelu'(h) when gd, else h)

@@ -299,6 +299,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 && NB == 2) ? (BN == 64
         gelu_gg4(vb, gb, db);
         ga *= ka;
         gb *= kb;
+        if (ep.gd == 2) {  // GELU_DUAL_DK: the backward's multiplier carries the mask
+          da *= ka;
+          db *= kb;
+        }
         // (no out: the inference form, HVIT_ACT_GELU -- only gelu(v) is stored)
         if (ep.out) *(u32x4*)((bf16_t*)ep.out + (long)m * ep.ldo + n8) = ep.gd ? pack8(da, db) : pack8(va, vb);
         *(u32x4*)((bf16_t*)ep.out2 + (long)m * ep.ldo2 + n8) = pack8(ga, gb);

@@ -820,6 +820,11 @@ DEFER = os.environ.get("HVIT_DEFER", "1") != "0"
 # A/B knob: 0 = the qkv bias gradient by a column reduction of dqkv after the
 # attention backward (instead of the backward's partial rows)
 ATTN_DB = os.environ.get("HVIT_ATTN_DB", "1") != "0"
+# the fc1 forward folds its dropout multiplier into the stored gelu'(h)
+# (GELU_DUAL_DK: dh = dA * [keep * scale * gelu'(h)]), so the fc2 data-gradient
+# epilogue multiplies without re-hashing the mask.  A/B knob: 0 = round-5 form
+# (gelu'(h) stored, the mask re-hashed in the backward)
+FC1_FOLD = os.environ.get("HVIT_FC1_FOLD", "1") != "0"
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
@@ -1162,15 +1167,17 @@ class ViTBlockFn(torch.autograd.Function):
                  epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), s)
         xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
         W1 = cast(f1w, dt)
-        # the fc1 epilogue keeps gelu'(h) (not h) for the backward: the fc2 dgrad
-        # epilogue then multiplies instead of re-evaluating erf / exp per element;
+        # the fc1 epilogue keeps gelu'(h) (not h) for the backward -- times the
+        # dropout multiplier (FC1_FOLD) -- so the fc2 dgrad epilogue only multiplies
+        # (no erf / exp, no mask hash per element);
         # with no backward to run (eval / no-grad inference) it stores gelu(h) only
         a = _empty((M, hid), dt, dev)
         if not nograd:
             gh = _empty((M, hid), dt, dev)
             with timed("vit_linear_fwd", 2.0 * M * hid * D):
                 call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, gh.data_ptr(),
-                     dt, epilogue(act=L.ACT_GELU_DUAL_D, out2=a, drop=d_fc1.c()), s)
+                     dt, epilogue(act=L.ACT_GELU_DUAL_DK if FC1_FOLD else L.ACT_GELU_DUAL_D, out2=a,
+                                  drop=d_fc1.c()), s)
         else:
             gh = None
             with timed("vit_linear_fwd", 2.0 * M * hid * D):
@@ -1246,7 +1253,7 @@ class ViTBlockFn(torch.autograd.Function):
         nrow = (M + 63) // 64
         cparts = torch.empty((nrow, hid), dtype=torch.float32, device=dev)
         df1b = torch.empty(hid, dtype=torch.float32, device=dev)
-        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=drf1, colsum=cparts, side=j2)
+        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=None if FC1_FOLD else drf1, colsum=cparts, side=j2)
         _launch("vit_linear_dgrad", 2.0 * M * D * hid,
                 lambda e: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt, e,
                                s), e_fc2, (gh, cparts))

@@ -101,6 +101,11 @@ def test_linear_fwd_kinds_exact(env, cfg):
     F.gelu(hp).backward(torch.ones_like(hp))
     check_bf16(h, hp.grad, acc=1e-4, what=f"fc1 gelu'(h) cfg {cfg}")
     check_bf16(a, F.gelu(ref) * mask / 0.9, acc=1e-4, what=f"fc1 a (D) cfg {cfg}")
+    # GELU_DUAL_DK (the model's default): the stored multiplier carries the dropout mask
+    L.call("hvit_linear_fwd", L.BF16, x.data_ptr(), w1.data_ptr(), b1.data_ptr(), M, HID, D, h.data_ptr(), L.BF16,
+           HF.epilogue(act=L.ACT_GELU_DUAL_DK, out2=a, drop=L.dropout(0.1, 21, 302)), s())
+    check_bf16(h, hp.grad * mask / 0.9, acc=1e-4, what=f"fc1 keep * gelu'(h) cfg {cfg}")
+    check_bf16(a, F.gelu(ref) * mask / 0.9, acc=1e-4, what=f"fc1 a (DK) cfg {cfg}")
     # proj and fc2: f32 residual + DropPath row scale * dropout(v + b)
     res = torch.randn(M, D, device=DEV)
     rs = torch.rand(32, device=DEV) + 0.5
@@ -146,6 +151,15 @@ def test_linear_dgrad_kinds_exact(env, cfg):
     ref = (g2.float() @ w2.float()) * mk / 0.9 * gd.float()
     check_bf16(dh, ref, what=f"fc2 dgrad MUL_AUX cfg {cfg}")
     check_f32(cs, ref.sum(0), acc=1e-4, what=f"fc2 dgrad MUL_AUX colsum cfg {cfg}")
+    # with GELU_DUAL_DK's multiplier (mask folded in): MUL_AUX without a dropout
+    gk = (hp.grad * mk / 0.9).to(BF)
+    csr.fill_(float("nan"))
+    L.call("hvit_linear_dgrad", L.BF16, g2.data_ptr(), w2.data_ptr(), M, D, HID, dh.data_ptr(), L.BF16,
+           HF.epilogue(act=L.ACT_MUL_AUX, aux=gk, colsum=csr), s())
+    cs = csr.sum(0)
+    ref = (g2.float() @ w2.float()) * gk.float()
+    check_bf16(dh, ref, what=f"fc2 dgrad MUL_AUX (DK) cfg {cfg}")
+    check_f32(cs, ref.sum(0), acc=1e-4, what=f"fc2 dgrad MUL_AUX (DK) colsum cfg {cfg}")
     # fc1 / qkv dgrad (f32 out), proj dgrad (bf16 out)
     for name, N, K, odt in (("fc1", HID, D, L.F32), ("qkv", 3 * D, D, L.F32), ("proj", D, D, L.BF16)):
         dy = rb(M, N)

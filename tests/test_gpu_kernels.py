@@ -84,6 +84,11 @@ def test_linear_fwd_epilogues(hv, dt):
     F.gelu(hp).backward(torch.ones_like(hp))
     assert rel(h.float(), hp.grad) < tol(dt)
     assert rel(a.float(), F.gelu(ref) * mask / 0.75) < tol(dt)
+    # GELU_DUAL_DK: the first output is keep * scale * gelu'(v)
+    l.call("hvit_linear_fwd", l.dt_of(x), x.data_ptr(), w.data_ptr(), b.data_ptr(), M, N, K, h.data_ptr(),
+           l.dt_of(h), HF.epilogue(act=l.ACT_GELU_DUAL_DK, out2=a, drop=dr), s())
+    assert rel(h.float(), hp.grad * mask / 0.75) < tol(dt)
+    assert rel(a.float(), F.gelu(ref) * mask / 0.75) < tol(dt)
     # residual + per-sample scale + dropout
     resid = torch.randn(M, N, device=DEV)
     rs = torch.tensor([0.0, 1.25, 1.25, 0.5], device=DEV)
