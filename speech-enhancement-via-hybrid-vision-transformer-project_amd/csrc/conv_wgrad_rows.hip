@@ -253,14 +253,19 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_rows_kernel(RowsArgs a) {
   rows_body<BM>(a, smem);
 }
 
-// split count: balanced grid (see conv_wgrad_splits), >= 4 stages per split
+// split count: balanced grid (see conv_wgrad_splits), >= 4 stages per split,
+// at most 512 workgroups: every split writes and the reduction re-reads a full
+// f32 weight slab (~75 MB per conv at 768 workgroups), and two rounds of 256
+// long-K workgroups beat three of shorter ones (step 5.233 -> 5.214 ms,
+// gpurun_out/r5n, r5o; 384: 5.210 vs 5.169 -- too few workgroups)
 int rows_splits(long tiles, int stages) {
+  static const long maxwg = getenv("HVIT_ROWS_MAXWG") ? atol(getenv("HVIT_ROWS_MAXWG")) : 512;  // A/B knob
   const long maxs = std::max(1, std::min(256, stages / 4));
   int best = 1;
   double bs = -1e30;
   for (long s = 1; s <= maxs; ++s) {
     const long nwg = tiles * s;
-    if (nwg > 768 && s > 1) break;
+    if (nwg > maxwg && s > 1) break;
     const long per = (nwg + 255) / 256;
     double score = (double)nwg / (256.0 * per) - 0.02 * (double)nwg / 256.0;
     if (nwg < 384) score -= 0.5 * (384.0 - (double)nwg) / 384.0;
