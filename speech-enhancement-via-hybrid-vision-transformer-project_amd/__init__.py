@@ -26,10 +26,12 @@ from .hybrid_vit import (  # noqa: F401
 from .losses import CombinedLoss, create_loss_function  # noqa: F401
 from .optim import FusedAdamW, clip_grad_norm_, create_optimizer  # noqa: F401
 from .train_step import GraphedTrainStep  # noqa: F401
+from .config import load_all_configs, load_config, merge_configs  # noqa: F401
 from . import _lib  # noqa: F401
 
 __all__ = [
     "HybridViT", "create_hybrid_vit", "ConvBlock", "TransposeConvBlock", "FeedForward", "PatchEmbedding",
     "PositionalEncoding", "MultiHeadSelfAttention", "TransformerEncoderBlock", "VisionTransformer",
     "CombinedLoss", "create_loss_function", "FusedAdamW", "clip_grad_norm_", "create_optimizer", "GraphedTrainStep",
+    "load_all_configs", "load_config", "merge_configs",
 ]

@@ -122,3 +122,34 @@ def test_istft_matches_restated_librosa(hv, n):
     got = E.AudioEnhancer(Identity(), device="cpu").istft(torch.as_tensor(spec), n)
     assert got.shape == ref.shape == (n,)
     assert np.abs(got - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+def test_load_all_configs_merge_order(hv, tmp_path, capsys):
+    """load_all_configs (utils/config.py:77-110): data, model, train YAMLs in
+    that order, nested dicts merged key by key, a later file's keys winning;
+    a missing file is reported and skipped; a missing directory raises."""
+    import yaml
+
+    (tmp_path / "data_config.yaml").write_text(yaml.safe_dump({"audio": {"sample_rate": 16000, "n_fft": 512},
+                                                                "data": {"a": 1}}))
+    (tmp_path / "model_config.yaml").write_text(yaml.safe_dump({"audio": {"n_fft": 1024, "hop_length": 256},
+                                                                 "model": {"transformer": {"embed_dim": 64}}}))
+    cfg = hv.load_all_configs(tmp_path)
+    assert cfg == {"audio": {"sample_rate": 16000, "n_fft": 1024, "hop_length": 256}, "data": {"a": 1},
+                   "model": {"transformer": {"embed_dim": 64}}}
+    assert "train_config.yaml" in capsys.readouterr().out
+    with pytest.raises(FileNotFoundError):
+        hv.load_all_configs(tmp_path / "absent")
+    base = {"x": {"y": 1}}
+    assert hv.merge_configs(base, {"x": {"z": 2}}) == {"x": {"y": 1, "z": 2}} and base == {"x": {"y": 1}}
+
+
+def test_enhance_cli_argument_errors(hv):
+    """enhance.py keeps the reference's mode checks (enhance.py:90-103)."""
+    import enhance
+
+    with pytest.raises(SystemExit):
+        enhance.main(["--checkpoint", "x.pth"])  # neither mode
+    with pytest.raises(SystemExit):
+        enhance.main(["--checkpoint", "x.pth", "--input", "a.wav", "--output", "b.wav", "--input-dir", "i",
+                      "--output-dir", "o"])  # both modes
