@@ -312,7 +312,7 @@ def main():
         torch.cuda.synchronize()
         if use_dist:
             from hvit_amd.dp import quiesce_for_capture
-            quiesce_for_capture()  # the watchdog retires the warm-up collectives first
+            quiesce_for_capture()  # device idle; the captured collectives go to dp.capture_group
         graph = torch.cuda.CUDAGraph()
         # thread-local capture: under DP the process group's watchdog thread
         # polls the events of earlier collectives; in the default (global) mode

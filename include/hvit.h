@@ -152,10 +152,10 @@ int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, in
  * gemm_ring.h); what 1 = the fused first block's matrix-core kernels (1 on, 0:
  * the VALU kernels); what 2 = workgroup target of the linear weight gradients'
  * split-K choice for the calls that follow (0: default 256; also sizes
- * hvit_wgrad_workspace); what 3 = the persistent epilogue-overlapped kernels of the
- * K = 512 linears (gemm_pp.hip: -1 automatic, 0 off, 1 = 256x128 tiles, 2 =
- * 128x128 tiles); what 4 = the attention backward for bf16 / head_dim 64 /
- * N <= 256 (1: the single-pass kernel, 0: the dQ and dK/dV kernel pair).
+ * hvit_wgrad_workspace); what 4 = the attention backward for bf16 / head_dim 64 /
+ * N <= 256 (1: the single-pass kernel, 0: the dQ and dK/dV kernel pair); what 5
+ * = the fp8 attention forward form (1: v2, 0: round 4's kernel, 2: v2 as two
+ * 8-wave workgroups per (b, h)).
  * Returns the previous value (-1 for an unknown knob). */
 int hvit_gemm_tune(int what, int value);
 /* dw[N,K] = dy^T x; db[N] = colsum(dy) (nullable; fused when db == dw + N*K) */

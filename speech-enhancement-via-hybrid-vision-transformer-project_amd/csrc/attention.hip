@@ -1396,19 +1396,16 @@ static bool v2_big(int N) { return N > 256; }  // the KMAX = 512 instantiations
 // to 4, the template the launches fall back to) cannot size the rows apart
 // from the grid.
 // (N > 256 takes the KMAX = 512 kernels, instantiated for 16 waves only)
-// the single-pass backward (mhsa_bwd_fused) for N <= 256; HVIT_ATTN_FUSED=0 or
-// hvit_gemm_tune(4, 0) selects the dQ + dK/dV kernel pair (A/B, tests)
+// the single-pass backward (mhsa_bwd_fused) for N <= 256; hvit_gemm_tune(4, 0)
+// selects the dQ + dK/dV kernel pair (tests)
 int& attn_fused_ref() {
-  static int v = getenv("HVIT_ATTN_FUSED") ? atoi(getenv("HVIT_ATTN_FUSED")) : 1;
+  static int v = 1;
   return v;
 }
 static bool v2_fused(int N) { return attn_fused_ref() != 0 && !v2_big(N); }
 static int v2_waves(int N) {
-  static const int w = [] {
-    const int e = getenv("HVIT_ATTN_WAVES") ? atoi(getenv("HVIT_ATTN_WAVES")) : 16;
-    return (e == 16 || e == 8) ? e : 4;
-  }();
-  return v2_big(N) ? 16 : w;
+  (void)N;
+  return 16;  // (8-wave workgroups measured slower at B·H = 256 and 192)
 }
 
 // ------------------------------------------------------------------- host ---

@@ -506,7 +506,7 @@ __global__ __launch_bounds__(WAVES * 64) void mhsa_fwd_fp8_v2(const bf16_t* __re
 // 0: the round-4 kernel, 1: v2 with one 16-wave workgroup per (b, h), 2: v2 with
 // two 8-wave workgroups per (b, h) (hvit_gemm_tune(5, v) for A/B)
 int& fp8_form_ref() {
-  static int v = getenv("HVIT_FP8_FORM") ? atoi(getenv("HVIT_FP8_FORM")) : 1;
+  static int v = 1;
   return v;
 }
 

@@ -937,12 +937,9 @@ inline int rows_per_block(int W, int P) {
 }
 
 // the matrix-core kernels apply (bf16 operands, pool 2, 16 <= Cout <= 64);
-// HVIT_C1MFMA=0 or hvit_gemm_tune(1, 0) forces the VALU kernels (A/B, tests)
+// hvit_gemm_tune(1, 0) forces the VALU kernels (tests)
 inline int& mfma_knob() {
-  static int knob = [] {
-    const char* e = getenv("HVIT_C1MFMA");
-    return e ? atoi(e) : 1;
-  }();
+  static int knob = 1;
   return knob;
 }
 inline bool use_mfma(int dt, int pool, int C) {

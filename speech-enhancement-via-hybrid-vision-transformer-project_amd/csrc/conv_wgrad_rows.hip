@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_rows_kernel(RowsArgs a) {
 // long-K workgroups beat three of shorter ones (step 5.233 -> 5.214 ms,
 // gpurun_out/r5n, r5o; 384: 5.210 vs 5.169 -- too few workgroups)
 int rows_splits(long tiles, int stages) {
-  static const long maxwg = getenv("HVIT_ROWS_MAXWG") ? atol(getenv("HVIT_ROWS_MAXWG")) : 512;  // A/B knob
+  constexpr long maxwg = 512;
   const long maxs = std::max(1, std::min(256, stages / 4));
   int best = 1;
   double bs = -1e30;
@@ -283,10 +283,8 @@ using namespace hvit_rows;
 
 // eligibility of the shifted-row path (bf16, 3x3 / stride 1 / pad 1, every
 // 64-channel block inside one source, whole 64-pixel stages inside one image,
-// 31-bit byte offsets); HVIT_WGRAD_ROWS=0 disables it (A/B only)
+// 31-bit byte offsets)
 bool conv_wgrad_rows_geom_ok(const hvit_conv_geom_t* g) {
-  static const bool on = !getenv("HVIT_WGRAD_ROWS") || atoi(getenv("HVIT_WGRAD_ROWS"));
-  if (!on) return false;
   if (g->KS != 3 || g->stride != 1 || g->pad != 1 || (g->U != 1 && g->U != 2)) return false;
   if (g->C1 % 64 || g->C2 % 64 || g->Cout % 64) return false;
   if (!aligned16(g->src1) || (g->src2 && !aligned16(g->src2))) return false;

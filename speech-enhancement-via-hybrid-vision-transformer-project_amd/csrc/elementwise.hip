@@ -399,6 +399,37 @@ __global__ __launch_bounds__(256) void weight_pack_tiled_kernel(WPrepArgs a) {
   }
 }
 
+// Packings whose block does not fit the LDS tile (Cin * KS * KS or Cout * KS
+// * KS above WPT_MAXE floats): one thread per destination element, gathering
+// from the source directly (start[] holds prefix sums of elements); the tiled
+// kernel's arithmetic element for element.
+__global__ __launch_bounds__(256) void weight_pack_flat_kernel(WPrepArgs a) {
+  const int total = a.start[a.count];
+  int j = 0;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+    while (u >= a.start[j + 1]) ++j;  // u only grows: the search resumes
+    const WPrepItem& w = a.it[j];
+    const int o = u - a.start[j];
+    const int K2 = w.ks * w.ks;
+    if (w.kind != 2) {  // [Cout][KS][KS][Cin] <- [Cout][Cin][KS][KS]
+      const int n = w.ci * K2;
+      const int b = o / n, r = o - b * n;
+      const int ci = r % w.ci, t = r / w.ci;
+      float x = w.src[(long)b * n + ci * K2 + t];
+      if (w.kind == 3) {
+        x *= w.gamma[b] * rsqrtf(w.rvar[b] + w.eps);
+        if (r == 0) w.bias[b] = w.beta[b] - w.rmean[b] * (w.gamma[b] * rsqrtf(w.rvar[b] + w.eps));
+      }
+      st_dt(w.dst, o, x, w.dt);
+    } else {  // flipped [Cin][KS][KS][Cout]
+      const int n = w.co * K2;
+      const int b = o / n, r = o - b * n;
+      const int co = r % w.co, tf = r / w.co;
+      st_dt(w.dst, o, w.src[((long)co * w.ci + b) * K2 + (K2 - 1 - tf)], w.dt);
+    }
+  }
+}
+
 __global__ void droppath_scale_kernel(int B, uint32_t thr, float ds, DSeed seed_, uint32_t site,
                                       float* out) {
   const unsigned long long seed = seed_;
@@ -706,8 +737,12 @@ extern "C" int hvit_sum_slabs(const float* ws, int splits, long long n, float* o
 
 extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void* stream) {
   HVIT_CHECK(count >= 0 && (count == 0 || items), "hvit_weight_prep: bad args");
-  // casts (kind 0) in the flat launch, packings (kinds 1-3) in the tiled one
-  for (int pass = 0; pass < 2; ++pass) {
+  // casts (kind 0) in the flat launch, packings (kinds 1-3) in the tiled one,
+  // packings whose block is above the LDS tile in the flat gather
+  auto big = [](const hvit_wprep_item_t& it) {
+    return (long long)it.cin * it.ks * it.ks > WPT_MAXE || (long long)it.cout * it.ks * it.ks > WPT_MAXE;
+  };
+  for (int pass = 0; pass < 3; ++pass) {
     WPrepArgs a;
     a.count = 0;
     a.start[0] = 0;
@@ -717,6 +752,8 @@ extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void*
       if (total > 0) {
         if (pass == 0)
           hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
+        else if (pass == 2)
+          hipLaunchKernelGGL(weight_pack_flat_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, a);
         else {
           if (maxe * (long)sizeof(float) > 65536)
             (void)hipFuncSetAttribute((const void*)weight_pack_tiled_kernel,
@@ -739,16 +776,13 @@ extern "C" int hvit_weight_prep(int count, const hvit_wprep_item_t* items, void*
                  "hvit_weight_prep: item %d: BN fold needs gamma, beta, rmean, rvar, bias", k);
       HVIT_CHECK(it.kind == 0 || (long long)it.cout * it.cin * it.ks * it.ks == it.numel,
                  "hvit_weight_prep: item %d: conv shape", k);
-      HVIT_CHECK(it.kind == 0 || ((long long)it.cin * it.ks * it.ks <= WPT_MAXE &&
-                                  (long long)it.cout * it.ks * it.ks <= WPT_MAXE),
-                 "hvit_weight_prep: item %d: conv block above %d elements", k, WPT_MAXE);
       HVIT_CHECK(aligned16(it.src) && (it.kind != 0 || aligned16(it.dst)), "hvit_weight_prep: item %d: alignment", k);
-      if ((it.kind == 0) != (pass == 0)) continue;
+      if (pass != (it.kind == 0 ? 0 : big(it) ? 2 : 1)) continue;
       const int cis = (it.cin > 0 && (it.cin & (it.cin - 1)) == 0) ? __builtin_ctz((unsigned)it.cin) : -1;
       const int cos = (it.cout > 0 && (it.cout & (it.cout - 1)) == 0) ? __builtin_ctz((unsigned)it.cout) : -1;
       a.it[a.count] = WPrepItem{it.src,   it.dst,  (int)(it.numel / 4), it.kind, it.dt,   it.cout, it.cin,
                                 it.ks,    it.gamma, it.beta,             it.rmean, it.rvar, it.bias, it.eps, cis, cos};
-      const int units = pass == 0 ? (int)(it.numel / 4) : (it.kind == 2 ? it.cin : it.cout);
+      const int units = pass == 0 ? (int)(it.numel / 4) : pass == 2 ? (int)it.numel : (it.kind == 2 ? it.cin : it.cout);
       if (pass == 1) maxe = std::max(maxe, (long)(it.kind == 2 ? it.cout : it.cin) * it.ks * it.ks);
       a.start[a.count + 1] = a.start[a.count] + units;
       if (++a.count == WPREP_MAX)

@@ -1834,11 +1834,9 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
                 int force_tile = 0) {
   Epi ep = ep_in;
   if (ep.slab_stride == 0) ep.slab_stride = (long)M * ep.ldo;
-  static const int remap = getenv("HVIT_XCD_REMAP") ? atoi(getenv("HVIT_XCD_REMAP")) : 1;  // A/B only
-  ep.xcd_remap = remap;
-  static const int dma = getenv("HVIT_GEMM_DMA") ? atoi(getenv("HVIT_GEMM_DMA")) : 1;  // A/B only
+  ep.xcd_remap = 1;
   // the DMA loop addresses operands with 32-bit byte offsets
-  ep.dma = dma && dense_bytes(la) < (1L << 31) && dense_bytes(lb) < (1L << 31);
+  ep.dma = dense_bytes(la) < (1L << 31) && dense_bytes(lb) < (1L << 31);
   auto vok = [](const void* p, long ld) { return !p || ((((uintptr_t)p) & 15) == 0 && ld % 4 == 0); };
   ep.vec_ok = N % 4 == 0 && vok(ep.out, ep.ldo) && vok(ep.out2, ep.ldo2) && vok(ep.aux, ep.ldaux) &&
               vok(ep.resid, ep.ldr) && vok(ep.rowadd, ep.rowadd_ld);
@@ -1855,7 +1853,7 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
   if (!tile) {
     // 128x64 also when 128x128 would leave fewer than ~1.5 workgroups per CU
     // or a half-empty last column tile (measured: 2.5 % per train step)
-    static const int policy = getenv("HVIT_TILE_POLICY") ? atoi(getenv("HVIT_TILE_POLICY")) : 2;
+    constexpr int policy = 2;  // (policies 0 / 1 measured slower: DESIGN.md §8)
     const long b128 = (long)cdiv(M, 128) * cdiv(N, 128) * splits;
     const long b12864 = (long)cdiv(M, 128) * cdiv(N, 64) * splits;
     if (N <= 64 && (long)cdiv(M, 128) * splits >= 160) tile = 12864;
@@ -1899,10 +1897,9 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
   if constexpr (DMA_OK) {
     const int bm = tile == 128 || tile == 12864 ? 128 : 64, bn = tile == 128 ? 128 : 64;
     // both operands k-major (the weight gradients): the register path measured
-    // faster (1.04 vs 0.82 ms/step); HVIT_DMA_MNMN=1 forces DMA there (A/B only)
-    static const bool mnmn = getenv("HVIT_DMA_MNMN") && atoi(getenv("HVIT_DMA_MNMN"));
-    // HVIT_CONV_DMA=0: conv A operands on the register-staged loop (A/B only)
-    static const bool conv_dma = !getenv("HVIT_CONV_DMA") || atoi(getenv("HVIT_CONV_DMA"));
+    // faster (1.04 vs 0.82 ms/step)
+    constexpr bool mnmn = false;
+    constexpr bool conv_dma = true;
     bool a_ok;
     if constexpr (CONV_A) a_ok = conv_dma;
     else a_ok = la.vok;
@@ -1921,12 +1918,11 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
             // one-buffer LDS-DMA kernels (3 workgroups per CU, out of phase, so one's
             // epilogue overlaps another's K loop) for the 128x128 forward kinds:
             // vit_linear_fwd 0.732 -> 0.721 ms/step.  Not for GELU_BWD (its h
-            // prefetch spills at 168 VGPRs: dgrad 0.737 -> 0.780).  HVIT_DMA1=0
-            // disables (A/B only)
-            static const bool nb1 = !getenv("HVIT_DMA1") || atoi(getenv("HVIT_DMA1"));
+            // prefetch spills at 168 VGPRs: dgrad 0.737 -> 0.780)
+            constexpr bool nb1 = true;
             // conv forward (BN statistics epilogue) too: conv_fwd 0.471 -> 0.447 ms/step;
-            // not the conv data gradient (0.346 -> 0.362).  HVIT_DMA1_CONV=0 disables (A/B)
-            static const bool nb1c = !getenv("HVIT_DMA1_CONV") || atoi(getenv("HVIT_DMA1_CONV"));
+            // not the conv data gradient (0.346 -> 0.362)
+            constexpr bool nb1c = true;
             if constexpr (BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
               if (CONV_A ? (nb1c && ep.stats) : nb1) {
                 hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 1>), g, dim3(GEMM_THREADS), 0, st,

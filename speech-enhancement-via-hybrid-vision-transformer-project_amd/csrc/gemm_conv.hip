@@ -52,8 +52,7 @@ extern "C" int hvit_conv_fwd(int dt, const hvit_conv_geom_t* g, const void* w_pa
     HVIT_CHECK(la.Ho > 0 && la.Wo > 0, "hvit_conv_fwd: empty output");
     int Kt = la.Kt;
     if constexpr (sizeof(T) == 2) {
-      // HVIT_CONV_FWD_TILE = 128 / 12864 / 64 forces the tile (A/B measurements only)
-      static const int ft = getenv("HVIT_CONV_FWD_TILE") ? atoi(getenv("HVIT_CONV_FWD_TILE")) : 0;
+      constexpr int ft = 0;  // automatic tile (forced 128x128 / 128x64 measured slower)
       if (conv_fast_ok(la, g->N))
         return launch_gemm<T>(conv_fast(la, g->N), dense<T, true>(w_packed, Kt, g->Cout, Kt), la.P, g->Cout, Kt, 1,
                               ep, (hipStream_t)stream, ft);

@@ -108,15 +108,12 @@ int check_epi(const hvit_epilogue_t* e) {
 long wg_target = 0;
 int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64, bool conv = false) {
   long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
-  static const long big = getenv("HVIT_WG_TARGET") ? atol(getenv("HVIT_WG_TARGET")) : 256;
-  static const long cbig = getenv("HVIT_CONV_WG_TARGET") ? atol(getenv("HVIT_CONV_WG_TARGET")) : 256;
-  const long target = bm * bn <= 64 * 64 ? 512 : conv ? cbig : wg_target > 0 ? wg_target : big;
+  const long target = bm * bn <= 64 * 64 ? 512 : conv ? 256 : wg_target > 0 ? wg_target : 256;
   long want = (target + tiles - 1) / tiles;
   long maxs = K / (4 * bk);
   // a multiple of 8 slices: with the XCD-aware tile order (gemm.h tile_of)
   // each XCD then reduces whole K slices, whose operand rows stay in its L2
-  static const bool split8 = !getenv("HVIT_SPLIT8") || atoi(getenv("HVIT_SPLIT8"));  // A/B only
-  if (split8 && want > 4 && maxs >= 8) want = std::min((want + 7) / 8 * 8, maxs / 8 * 8);
+  if (want > 4 && maxs >= 8) want = std::min((want + 7) / 8 * 8, maxs / 8 * 8);
   if (want > maxs) want = maxs;
   if (want > 256) want = 256;
   if (want < 1) want = 1;
@@ -131,7 +128,6 @@ int wgrad_splits(long M, long N, long K, int bm, int bn, int bk = 64, bool conv 
 // tools/wgrad_sweep.py, B=32): 288 WGs 226 us, 432 -> 169, 576 -> 203,
 // 792 -> 185.  HVIT_CONV_WG_TARGET selects the older fixed-target rule (A/B).
 int conv_wgrad_splits(int M, long N, long K, int bm, int bn, int bk = 64) {
-  if (getenv("HVIT_CONV_WG_TARGET")) return wgrad_splits(M, N, K, bm, bn, bk, true);
   const long tiles = (long)cdiv(M, bm) * cdiv(N, bn);
   const long maxs = std::max(1L, std::min(256L, K / (4 * bk)));
   int best = 1;

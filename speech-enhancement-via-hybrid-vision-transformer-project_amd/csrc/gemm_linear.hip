@@ -2,10 +2,6 @@
 #include "gemm_host.h"
 #include "gemm_ring.h"
 
-// persistent epilogue-overlapped kernels (gemm_pp.hip)
-bool hvit_pp_fwd(const void* x, const void* w, int M, int N, int K, const hvit::Epi& ep, hipStream_t st, int* rc);
-bool hvit_pp_dgrad(const void* dy, const void* w, int M, int N, int K, const hvit::Epi& ep, hipStream_t st, int* rc);
-int hvit_pp_tune(int value);
 int hvit_attn_tune(int value);
 int hvit_fp8_tune(int value);  // attention_fp8.hip
 
@@ -22,7 +18,6 @@ extern "C" int hvit_linear_fwd(int dt, const void* x, const void* w, const float
   if (M == 0) return HVIT_OK;
   if (dt == HVIT_BF16) {
     int rc = 0;
-    if (hvit_pp_fwd(x, w, M, N, K, ep, (hipStream_t)stream, &rc)) return rc;
     if (try_ring(dense<bf16_t, true>(x, K, M, K), dense<bf16_t, true>(w, K, N, K), M, N, K, 1, ep,
                  (hipStream_t)stream, &rc))
       return rc;
@@ -46,7 +41,6 @@ extern "C" int hvit_linear_dgrad(int dt, const void* dy, const void* w, int M, i
   if (M == 0) return HVIT_OK;
   if (dt == HVIT_BF16 && N % 8 == 0) {
     int rc = 0;
-    if (hvit_pp_dgrad(dy, w, M, N, K, ep, (hipStream_t)stream, &rc)) return rc;
     if (try_ring(dense<bf16_t, true>(dy, N, M, N), dense<bf16_t, false>(w, K, K, N), M, K, N, 1, ep,
                  (hipStream_t)stream, &rc))
       return rc;
@@ -165,16 +159,13 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
     return HVIT_OK;
   }
   // tall-skinny shapes (head, skip projections): one 64x64 tile per workgroup
-  // over a chunk of rows; HVIT_WGRAD_SMALL=0 disables (A/B only)
-  static const bool small_on = !getenv("HVIT_WGRAD_SMALL") || atoi(getenv("HVIT_WGRAD_SMALL"));
-  if (small_on && !tickets && hvit_wgrad_small_ok(dt, M, N, K) && (!db || db == dw + NK) &&
+  // over a chunk of rows
+  if (!tickets && hvit_wgrad_small_ok(dt, M, N, K) && (!db || db == dw + NK) &&
       ws_elems >= hvit_wgrad_small_ws(M, N, K)) {
     if (int rc = side_alone()) return rc;
     return hvit_wgrad_small(dy, x, M, N, K, dw, db, ws, ws_elems, stream, job);
   }
-  // HVIT_NO_RS=1: bias grad by a separate column reduction (A/B measurements only)
-  static const bool no_rs = getenv("HVIT_NO_RS") && atoi(getenv("HVIT_NO_RS"));
-  const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK && !no_rs;
+  const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK;
   // ring-pipelined kernels (gemm_ring.h) for bf16 without fused bias row sums
   const int rcfg = ring_default_cfg() >= 0 ? ring_default_cfg() : ring_pick(false, false, N, K, M);
   if (dt == HVIT_BF16 && !fused_db && N % 8 == 0 && K % 8 == 0 && rcfg > 0) {
@@ -251,7 +242,8 @@ int hvit_c1_tune(int value);  // c1block.hip
 
 extern "C" int hvit_gemm_tune(int what, int value) {
   if (what == 1) return hvit_c1_tune(value);
-  if (what == 3) return hvit_pp_tune(value);  // persistent kernels: -1 auto, 0 off, 1 / 2 forced tile
+  // (3: the round-5 persistent epilogue-overlapped kernels, measured slower and
+  // removed in round 6 -- git history before that round has gemm_pp.hip)
   if (what == 4) return hvit_attn_tune(value);  // attention backward for N <= 256: 1 single pass, 0 two kernels
   if (what == 5) return hvit_fp8_tune(value);  // fp8 attention forward: 0 round-4 kernel, 1 v2 16 waves, 2 v2 8 waves
   if (what == 2) {  // workgroup target of the linear weight gradients' split-K (0: default)

@@ -485,10 +485,10 @@ bool ring_ok(int cfg, const LdDense<bf16_t, KCA>& la, const LdDense<bf16_t, KCB>
   return dense_bytes(la) < (1L << 31) && dense_bytes(lb) < (1L << 31);
 }
 
-// the configuration the linear entry points use (HVIT_RING at load, or
-// hvit_gemm_tune for in-process A/B measurements)
+// the configuration the linear entry points use (-1 automatic; hvit_gemm_tune
+// for in-process A/B measurements and the tests)
 inline int& ring_cfg_ref() {
-  static int c = getenv("HVIT_RING") ? atoi(getenv("HVIT_RING")) : -1;
+  static int c = -1;
   return c;
 }
 inline int ring_default_cfg() { return ring_cfg_ref(); }

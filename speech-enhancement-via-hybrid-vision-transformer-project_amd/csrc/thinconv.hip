@@ -680,10 +680,9 @@ int hvit_thin_o1_fwd(int dt, const hvit_conv_geom_t* g, const void* w, void* y, 
   // 128 output pixels per workgroup (1,024 workgroups at B = 32: four per CU overlap
   // their strip loads with each other's sums): 14.7 us vs 15.8 at 256, 24.9 at 512;
   // a thread-per-pixel form (no lane shuffles, weights from LDS) ran 15.7-17.1
-  static const int fpix = getenv("HVIT_O1F_PIX") ? atoi(getenv("HVIT_O1F_PIX")) : 128;
+  constexpr int fpix = 128;
   const size_t sstrip = o1_strip_bytes(fpix, g->Ws, C, 2);
-  if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && sstrip <= 150 * 1024 && P * C * 2L < (1L << 31) &&
-      !getenv("HVIT_O1_FLAT")) {
+  if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && sstrip <= 150 * 1024 && P * C * 2L < (1L << 31)) {
     const int nb = (int)((P + fpix - 1) / fpix);
     auto go = [&](auto kern) {
       allow_lds(kern, sstrip);
@@ -726,7 +725,7 @@ int hvit_thin_o1_dgrad(int dt, const hvit_conv_geom_t* g, const void* dz, const 
   const int H = g->Hs * g->U, W = g->Ws * g->U;
   const long total = (long)g->N * H * W * (C / 8);
   const size_t smem = 9 * C * sizeof(float);
-  if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && (64 % (C / 8)) == 0 && !getenv("HVIT_O1_FLAT")) {
+  if (g->U == 1 && dt == HVIT_BF16 && C / 8 <= 8 && (64 % (C / 8)) == 0) {
     const long P = (long)g->N * H * W;
     const int nb = (int)((P + WG_PIX_O1 - 1) / WG_PIX_O1);
     const size_t sd = sizeof(float) * (WG_PIX_O1 + 2 * W + 2);

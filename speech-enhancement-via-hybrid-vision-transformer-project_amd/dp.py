@@ -63,41 +63,77 @@ import torch.distributed as dist
 
 from . import functional as HF
 
-# Before a DP step is captured: every earlier collective complete AND retired by
-# the process group's watchdog thread.  The watchdog polls each enqueued work's
-# end event (every ~100 ms) until it sees it complete; the bucket all-reduces
-# run on RCCL's internal stream, which the capture then joins, and a poll of an
-# event of that stream while it is being captured fails ("operation not
-# permitted on an event last recorded in a capturing stream") and aborts the
-# process -- seen intermittently in round 5 on RCCL world-1 runs whose capture
-# followed eager warm-up steps directly.  Synchronising and then waiting a few
-# watchdog periods lets the watchdog retire those works first.  Captured
-# collectives are not enqueued to the watchdog, and replays enqueue nothing.
-WATCHDOG_DRAIN_S = 0.35
+# Captured collectives run on a process group of their own.  Round 5 saw the
+# process group's watchdog thread abort a DP step capture (RCCL, world 1:
+# "operation not permitted on an event last recorded in a capturing stream").
+# The watchdog polls the end event of every collective issued OUTSIDE a capture
+# (hipEventQuery on ProcessGroupNCCL's work list, ~every 100 ms, until it sees
+# the event complete); those events are recorded on the group's internal NCCL
+# stream.  A collective issued during a capture on the SAME group makes that
+# stream join the capture, and HIP refuses a query of an event whose recording
+# stream is capturing -- so any eager bucket all-reduce the watchdog had not yet
+# retired when the capture began killed the process.  Now every collective a
+# capture contains goes to a second NCCL group (``capture_group``) whose
+# communicator is connected eagerly (ncclCommSplit / eager_connect: no
+# collective) and which never runs a collective outside a capture; captured
+# collectives are never put on the watchdog's list (ProcessGroupNCCL enqueues
+# only uncaptured works).  So the watchdog's list holds only the eager group's
+# works, whose stream never joins a capture: no poll can meet a capturing
+# stream, whatever the timing.  (Round 5's stopgap slept 0.35 s before every
+# capture; gone.)
+_GROUPS: Dict[tuple, tuple] = {}
 
 
-def quiesce_for_capture(device=None) -> None:
-    """Call right before capturing a step that contains collectives."""
-    import time
-    torch.cuda.synchronize(device)
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        time.sleep(WATCHDOG_DRAIN_S)
-
-
-_GLOO_GROUPS: Dict[tuple, object] = {}
+def _cached_group(kind: str, group, make):
+    """One helper group per (default group, kind, ranks): the entry keeps the
+    default group OBJECT it was made under and is reused only while that same
+    object is the default group (a destroy_process_group() + re-init gives a new
+    one, possibly at the same id())."""
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
+    key = (kind, ranks)
+    e = _GROUPS.get(key)
+    if e is not None and e[0] is dist.group.WORLD:
+        return e[1]
+    g = make(ranks)
+    _GROUPS[key] = (dist.group.WORLD, g)
+    return g
 
 
 def _gloo_group(group):
-    """A gloo group over ``group``'s ranks, created once per (default group,
-    ranks) and reused (set_rows() rebuilds the reducer).  Created with local
-    synchronization, so only the member ranks take part: a reducer built on a
-    subgroup by that subgroup's ranks alone does not wait for the others."""
-    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
-    key = (id(dist.group.WORLD), ranks)
-    g = _GLOO_GROUPS.get(key)
-    if g is None:
-        g = _GLOO_GROUPS[key] = dist.new_group(ranks=list(ranks), backend="gloo", use_local_synchronization=True)
-    return g
+    """A gloo group over ``group``'s ranks, reused (set_rows() rebuilds the
+    reducer).  Created with local synchronization, so only the member ranks take
+    part: a reducer built on a subgroup by that subgroup's ranks alone does not
+    wait for the others."""
+    return _cached_group("gloo", group, lambda ranks: dist.new_group(ranks=list(ranks), backend="gloo",
+                                                                     use_local_synchronization=True))
+
+
+def capture_group(group=None):
+    """The NCCL group that carries a reducer's collectives while a hipGraph is
+    being captured (see above).  Its communicator is connected here, without a
+    collective.  On the world group every rank calls this (the reducer is built
+    on every rank); a subgroup's is made by its members alone, which a default
+    group bound to a device (ncclCommSplit from the parent) does not allow."""
+    def make(ranks):
+        sub = group is not None and len(ranks) != dist.get_world_size()
+        bound = getattr(dist.distributed_c10d._get_default_group(), "bound_device_id", None) is not None
+        if sub and bound:
+            return None  # (capture with such a reducer raises in GradAllReducer._coll_group)
+        g = dist.new_group(ranks=list(ranks), backend="nccl", use_local_synchronization=sub)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        be = g._get_backend(dev)
+        if hasattr(be, "eager_connect_single_device"):
+            be.eager_connect_single_device(dev)  # (idempotent when new_group already split it)
+        return g
+
+    return _cached_group("capture", group, make)
+
+
+def quiesce_for_capture(device=None) -> None:
+    """Call right before capturing a step that contains collectives: the
+    device is idle (the eager warm-up's collectives have finished).  No wait
+    for the watchdog is needed (see capture_group)."""
+    torch.cuda.synchronize(device)
 
 
 class GradAllReducer:
@@ -158,6 +194,10 @@ class GradAllReducer:
         self._host_group = self.group
         if self._agree and dist.get_backend(self.group) != "gloo":
             self._host_group = _gloo_group(self.group)
+        # collectives issued inside a hipGraph capture go to their own NCCL group
+        # (capture_group: the watchdog never polls a work of it)
+        self._nccl = dist.get_backend(self.group) == "nccl" and torch.cuda.is_available()
+        self._cap_group = capture_group(self.group) if self._nccl else None
         self.reset()
         self._publish()
 
@@ -197,10 +237,20 @@ class GradAllReducer:
             if bufs:
                 with torch.no_grad():
                     fb = torch.cat([t.reshape(-1).float() for t in bufs])
-                    work = dist.broadcast(fb, self._bcast_src(), group=self.group, async_op=True)
+                    work = dist.broadcast(fb, self._bcast_src(), group=self._coll_group(), async_op=True)
                 self._bcast.append((work, fb, bufs))
                 if len(self._bcast) > 4:  # forwards without a finish() (no-grad passes in train mode): keep the last
                     self._bcast.pop(0)[0].wait()
+
+    def _coll_group(self):
+        """The group for a collective issued now: the capture group while the
+        current stream is being captured, else the reducer's group."""
+        if self._nccl and torch.cuda.is_current_stream_capturing():
+            if self._cap_group is None:
+                raise RuntimeError("hvit GradAllReducer: capturing collectives on a subgroup needs a default "
+                                   "process group not bound to a device (init_process_group without device_id)")
+            return self._cap_group
+        return self.group
 
     def _float_buffers(self):
         # the module's current buffers (a .to() / .cuda() since construction replaces them)
@@ -301,7 +351,7 @@ class GradAllReducer:
                     srcs.append(v)
             if dsts:
                 torch._foreach_copy_(dsts, srcs)
-            self.works[b] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.works[b] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self._coll_group(), async_op=True)
 
     def finish(self):
         """Wait for every bucket (launching any whose hooks did not fire, e.g.
@@ -356,7 +406,8 @@ class GradAllReducer:
             if bufs:
                 with torch.no_grad():
                     fb = torch.cat([t.reshape(-1).float() for t in bufs])
-                    bcast = (dist.broadcast(fb, self._bcast_src(), group=self.group, async_op=True), fb, bufs)
+                    bcast = (dist.broadcast(fb, self._bcast_src(), group=self._coll_group(), async_op=True), fb,
+                             bufs)
         if bcast is not None:
             work, fb, bufs = bcast
             work.wait()

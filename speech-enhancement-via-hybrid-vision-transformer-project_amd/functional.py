@@ -170,7 +170,7 @@ def _zs(ctx, n):
 
 
 # Cache of prepared weights, filled by prep_weights() with one multi-tensor
-# launch: (id(param), kind, dt) -> (param._version, tensor, param, BN
+# launch: (id(param), kind, dt) -> (_sig(param), tensor, param, BN
 # versions).  A lookup requires the parameter to be unmodified since
 # preparation.  Entries survive from one forward to the next only for
 # inference forwards (prep_weights(reuse=True): eval + no_grad, the caller
@@ -184,19 +184,27 @@ def prep_cache_clear() -> None:
     _PREP.clear()
 
 
+def _sig(t):
+    """What a prepared copy of ``t`` is valid for: its version counter and its
+    storage (``param.data = ...`` and ``.to()`` move the storage without a version
+    bump; a replayed graph updates in place with neither, hence the clears in
+    GraphedTrainStep and FusedAdamW.step)."""
+    return (t._version, t.data_ptr())
+
+
 def _prep_get(t, kind, dt):
     hit = _PREP.get((id(t), kind, dt))
-    if hit is not None and hit[0] == t._version and hit[2] is t:
+    if hit is not None and hit[0] == _sig(t) and hit[2] is t:
         return hit[1]
     return None
 
 
 def _bn_versions(bn):
-    return tuple(x._version for x in bn[:4]) + tuple(id(x) for x in bn[:4])
+    return tuple(_sig(x) for x in bn[:4]) + tuple(id(x) for x in bn[:4])
 
 
 # Persistent bf16 copies of linear weights ("shadows"): id(param) ->
-# [weakref(param), bf16 tensor, param._version the copy matches or None].
+# [weakref(param), bf16 tensor, _sig(param) the copy matches or None].
 # FusedAdamW writes a parameter's shadow in the same pass that updates the
 # parameter (optim.py), so the next forward skips that cast.
 _SHADOW = {}
@@ -212,7 +220,7 @@ def shadow_mark(p):
     """Record that ``p``'s shadow now equals bf16(p) at its current version."""
     e = _SHADOW.get(id(p))
     if e is not None and e[0]() is p:
-        e[2] = p._version
+        e[2] = _sig(p)
 
 
 def prep_weights(items, dev, reuse: bool = False):
@@ -229,7 +237,7 @@ def prep_weights(items, dev, reuse: bool = False):
     for w, kind, dt, *bn in items:
         key = (id(w), kind, dt)
         hit = old.get(key)
-        if (hit is not None and hit[2] is w and hit[0] == w._version and
+        if (hit is not None and hit[2] is w and hit[0] == _sig(w) and
                 (kind != 3 or hit[3] == _bn_versions(bn[0]))):
             _PREP[key] = hit  # unchanged since it was prepared (repeated inference forwards)
             continue
@@ -243,8 +251,8 @@ def prep_weights(items, dev, reuse: bool = False):
             e = _SHADOW.get(id(w))
             if e is None or e[0]() is not w or e[1].shape != w.shape:
                 e = _SHADOW[id(w)] = [weakref.ref(w), _empty(w.shape, dt, dev), None]
-            if e[2] == w._version:
-                _PREP[(id(w), kind, dt)] = (w._version, e[1], w, None)
+            if e[2] == _sig(w):
+                _PREP[(id(w), kind, dt)] = (_sig(w), e[1], w, None)
                 continue
             todo.append((w, kind, dt, e[1], None))
             continue
@@ -263,7 +271,7 @@ def prep_weights(items, dev, reuse: bool = False):
             arr[i] = L.WPrepItem(w.data_ptr(), out.data_ptr(), w.numel(), kind, dt, co, ci, ks)
     call("hvit_weight_prep", len(todo), arr, stream_ptr())
     for w, kind, dt, out, bn in todo:
-        _PREP[(id(w), kind, dt)] = (w._version, out, w, _bn_versions(bn) if kind == 3 else None)
+        _PREP[(id(w), kind, dt)] = (_sig(w), out, w, _bn_versions(bn) if kind == 3 else None)
         if kind == 0 and dt == BF16:
             shadow_mark(w)
 
@@ -479,10 +487,10 @@ def linear_wgrad_now(dt, dy, x, M, N, K, tag="vit_linear_wgrad", dest=None, side
 # gradients only add their split-K slab sums (a launch each on the side stream,
 # where no following launch carries them) and contend for the CUs; fewer
 # side-stream splits (HVIT_SIDE_WG 128 / 64) were slower still (5.79 / 6.10).
-SIDE = os.environ.get("HVIT_SIDE", "0") == "1"  # A/B knob: 1 = weight gradients on the side stream
+SIDE = False  # True: weight gradients on the side stream (tests/test_gpu_determinism.py runs both)
 # workgroup target of the side stream's linear weight gradients (split-K
-# choice; 0 = the library default) -- A/B knob
-SIDE_WG = int(os.environ.get("HVIT_SIDE_WG", "0"))
+# choice; 0 = the library default)
+SIDE_WG = 0
 _SIDE_STREAMS = {}
 _SIDE_OPEN = set()
 _SIDE_TASKS = set()  # autograd graph tasks that have the join queued
@@ -660,7 +668,7 @@ class CastFn(torch.autograd.Function):
         return cast(g, ctx.src_dt), None
 
 
-SKIPGRAD = os.environ.get("HVIT_SKIPGRAD", "1") != "0"  # A/B knob: 0 = autograd adds the skip gradients
+SKIPGRAD = True  # False: autograd adds the skip gradients
 
 
 class SkipGrad:
@@ -810,21 +818,24 @@ class ConvBNActFn(torch.autograd.Function):
         return (dx1, dx2, dw, dgamma, dbeta) + (None,) * 12
 
 
-C1BLOCK = os.environ.get("HVIT_C1BLOCK", "1") != "0"  # A/B knob: 0 = the unfused conv + bn_act path
-EVALFOLD = os.environ.get("HVIT_EVALFOLD", "1") != "0"  # A/B knob: 0 = eval convs keep z + bn_act
-KEEPBITS = os.environ.get("HVIT_KEEPBITS", "1") != "0"  # A/B knob: 0 = the attention backward re-hashes dropout
-LNDROP = os.environ.get("HVIT_LNDROP", "1") != "0"  # A/B knob: 0 = separate LayerNorm backward and dropout pass
-# A/B knob: 0 = ViT weight gradients reduce their split-K slabs in a launch of
-# their own and the qkv bias gradient is a column reduction of dqkv
-DEFER = os.environ.get("HVIT_DEFER", "1") != "0"
-# A/B knob: 0 = the qkv bias gradient by a column reduction of dqkv after the
-# attention backward (instead of the backward's partial rows)
-ATTN_DB = os.environ.get("HVIT_ATTN_DB", "1") != "0"
+# Path switches (module attributes; the tests flip some of them to compare the
+# fused form with the separate one).  Round 6 retired their environment reads:
+# every A/B they served is concluded.
+C1BLOCK = True  # False: the unfused conv + bn_act path
+EVALFOLD = True  # False: eval convs keep z + bn_act
+KEEPBITS = True  # False: the attention backward re-hashes dropout
+LNDROP = True  # False: separate LayerNorm backward and dropout pass
+# False: ViT weight gradients reduce their split-K slabs in a launch of their
+# own and the qkv bias gradient is a column reduction of dqkv
+DEFER = True
+# False: the qkv bias gradient by a column reduction of dqkv after the attention
+# backward (instead of the backward's partial rows)
+ATTN_DB = True
 # the fc1 forward folds its dropout multiplier into the stored gelu'(h)
 # (GELU_DUAL_DK: dh = dA * [keep * scale * gelu'(h)]), so the fc2 data-gradient
-# epilogue multiplies without re-hashing the mask.  A/B knob: 0 = round-5 form
+# epilogue multiplies without re-hashing the mask.  False: the round-5 form
 # (gelu'(h) stored, the mask re-hashed in the backward)
-FC1_FOLD = os.environ.get("HVIT_FC1_FOLD", "1") != "0"
+FC1_FOLD = True
 
 
 def c1block_ok(x1, x2, w, U, pool) -> bool:
@@ -1005,7 +1016,7 @@ def _ln(x2d, gw, gb, dt):
     return y, mean, rstd
 
 
-_LN_SLAB = bool(int(__import__("os").environ.get("HVIT_LN_SLAB", "1")))
+_LN_SLAB = True
 
 
 def _ln_bwd(dy, x, mean, rstd, gw, resid, zs: ZSlot):

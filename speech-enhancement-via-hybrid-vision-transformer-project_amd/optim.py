@@ -238,6 +238,9 @@ class FusedAdamW(torch.optim.Optimizer):
                     if _bump is not None:
                         _bump(p)  # the kernel wrote p in place: keep version counters honest
                     HF.shadow_mark(p)
+        # parameters changed: no inference forward may reuse a packed / BN-folded
+        # copy (a captured replay of this step bumps no version counter)
+        HF.prep_cache_clear()
         return loss
 
 

@@ -286,6 +286,10 @@ def _worker_subgroup(rank, world, port, q):
         fake = types.SimpleNamespace(_agree=True, _host_group=None)
         g = ts.GraphedTrainStep(None, None, types.SimpleNamespace(capturable=True), reducer=fake)
         agree = (g._every_rank(rank != 1), g._every_rank(True), g._every_rank(False))
+        # uniform_shapes: the caller's promise replaces the agreement (no collective)
+        gu = ts.GraphedTrainStep(None, None, types.SimpleNamespace(capturable=True), reducer=fake,
+                                 uniform_shapes=True)
+        ok_sub = ok_sub and gu._every_rank(rank != 1) == (rank != 1)
         dist.barrier()
         q.put((rank, ok_sub, agree))
     finally:

@@ -207,7 +207,8 @@ def pack(hv, w, mode, dt):
 def test_weight_prep_packs_equal_conv_pack(hv, dt):
     """The multi-tensor weight preparation (hvit_weight_prep: one launch per
     forward) packs every conv shape of the model -- and odd ones (Cin / Cout not
-    powers of two, 2x2 patch kernels) -- exactly as hvit_conv_weight_pack does
+    powers of two, 2x2 patch kernels, blocks too large for the LDS tile) --
+    exactly as hvit_conv_weight_pack does
     (kinds 1 / 2), plain casts included (kind 0), all items in one launch."""
     from importlib import import_module
     HF = import_module("hvit_amd.functional")
@@ -215,7 +216,8 @@ def test_weight_prep_packs_equal_conv_pack(hv, dt):
     dtc = l.F32 if dt == "f32" else l.BF16
     torch.manual_seed(3)
     shapes = [(64, 1, 3), (128, 64, 3), (256, 128, 3), (512, 256, 2), (256, 512, 3), (1, 64, 3), (24, 3, 3),
-              (12, 20, 2)]
+              (12, 20, 2),
+              (8, 4608, 3), (4616, 6, 3)]  # blocks above the LDS tile (Cin or Cout x 9 > 40960): the flat gather
     ws = [torch.randn(co, ci, k, k, device=DEV) for co, ci, k in shapes]
     lin = torch.randn(96, 40, device=DEV)
     items = [(w, kind, dtc) for w in ws for kind in (1, 2)] + ([(lin, 0, dtc)] if dt == "bf16" else [])

@@ -532,23 +532,14 @@ def _mhsa_fp8_emulated(sd, pfx, x, H, p_attn, p, training, want_attn=False):
     return o, None
 
 
-def test_large_config_fp8_train_step_grads(hv, monkeypatch):
-    """BASELINE config 5 train step (D=768 / 12 heads / 12 layers, bf16, dropout
-    off, B=4) with the fp8 attention forward: the loss and EVERY parameter
-    gradient per tensor (relative L2) against the fp32 CPU oracle.  Bars
-    calibrated as the bf16 B=32 test's: torch bf16 autocast of the oracle gives
-    the bf16 error e_tb, and the same with the attention core replaced by an
-    emulation of the fp8 forward's roundings (straight-through, bf16 backward)
-    gives the fp8 error e_t8; our bf16 path must stay within 2 e_tb + 1e-2 and
-    our fp8 path within 2 e_t8 + 1e-2 per tensor.  The per-group table goes to
-    gpurun_out/fp8_grad_calibration.json when HVIT_RECORD is set."""
+def _config5_step_grads(hv, monkeypatch, B, sx, stg, record):
     import json
     cfg = O.HViTConfig(**LARGE)
     cfg.dropout = cfg.attn_dropout = cfg.drop_path_rate = 0.0
     shapes = O.state_dict_shapes(cfg)
     W = CF.weights(shapes)
-    x = torch.as_tensor(CF.spectrogram((4, 1, 256, 256), 80))
-    t = torch.as_tensor(CF.spectrogram((4, 1, 256, 256), 81))
+    x = torch.as_tensor(CF.spectrogram((B, 1, 256, 256), sx))
+    t = torch.as_tensor(CF.spectrogram((B, 1, 256, 256), stg))
     sd = O.make_state(shapes, W, requires_grad=True)
     lo_t = O.combined_loss(O.forward(sd, x, cfg, training=True), t)
     lo_t.backward()
@@ -586,12 +577,35 @@ def test_large_config_fp8_train_step_grads(hv, monkeypatch):
                 bad.append((name, k, round(e, 4), round(et, 4)))
     out = {n: {g: {"ours": v[0], "torch_emulation": v[1], "worst_tensor": v[2]} for g, v in d.items()}
            for n, d in table.items()}
-    print("config 5 B=4 step, worst rel-L2 per group:", json.dumps(out, indent=1))
+    print(f"config 5 B={B} step, worst rel-L2 per group:", json.dumps(out, indent=1))
     if os.environ.get("HVIT_RECORD"):
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-        with open(os.path.join(ROOT, "gpurun_out", "fp8_grad_calibration.json"), "w") as f:
-            json.dump({"loss_oracle": lo, "groups": out, "violations": bad}, f, indent=1)
+        with open(os.path.join(ROOT, "gpurun_out", record), "w") as f:
+            json.dump({"batch": B, "loss_oracle": lo, "groups": out, "violations": bad}, f, indent=1)
     assert not bad, bad
+
+
+def test_large_config_fp8_train_step_grads(hv, monkeypatch):
+    """BASELINE config 5 train step (D=768 / 12 heads / 12 layers, bf16, dropout
+    off, B=4) with the fp8 attention forward: the loss and EVERY parameter
+    gradient per tensor (relative L2) against the fp32 CPU oracle.  Bars
+    calibrated as the bf16 B=32 test's: torch bf16 autocast of the oracle gives
+    the bf16 error e_tb, and the same with the attention core replaced by an
+    emulation of the fp8 forward's roundings (straight-through, bf16 backward)
+    gives the fp8 error e_t8; our bf16 path must stay within 2 e_tb + 1e-2 and
+    our fp8 path within 2 e_t8 + 1e-2 per tensor.  The per-group table goes to
+    gpurun_out/fp8_grad_calibration.json when HVIT_RECORD is set."""
+    _config5_step_grads(hv, monkeypatch, 4, 80, 81, "fp8_grad_calibration.json")
+
+
+def test_large_config_b16_train_step_grads(hv, monkeypatch):
+    """BASELINE config 5 at its own batch, B=16 (M = 4,096 token rows: the
+    bench's tile counts, split-K plans and LayerNorm row paths), bf16 and fp8
+    attention: the loss and every parameter gradient per tensor against the
+    fp32 CPU oracle, bars calibrated as in the B=4 test (2x torch bf16 autocast
+    of the oracle, with the fp8 forward's roundings emulated for the fp8 path,
+    + 1e-2).  Table: gpurun_out/fp8_grad_calibration_b16.json (HVIT_RECORD)."""
+    _config5_step_grads(hv, monkeypatch, 16, 82, 83, "fp8_grad_calibration_b16.json")
 
 
 def test_large_config_fp8_attention(hv):
