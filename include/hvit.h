@@ -158,6 +158,12 @@ int hvit_linear_wgrad_tk(int dt, const void* dy, const void* x, int M, int N, in
  * 8-wave workgroups per (b, h)).
  * Returns the previous value (-1 for an unknown knob). */
 int hvit_gemm_tune(int what, int value);
+/* Diagnostics only (tools/wgrad_layout_probe.py): C[M,N] = sum_k A[m,k] B[n,k]
+ * as f32 split-K slabs ws[splits][M*N + M]; kca / kcb: 1 = operand stored with
+ * K contiguous ([M][K] / [N][K]), 0 = [K][M] / [K][N]; cfg 0 = gemm.h's kernels,
+ * 1-5 = a ring configuration (error if it does not apply). */
+int hvit_probe_gemm_splitk(int kca, int kcb, const void* a, const void* b, int M, int N, int K, int splits,
+                           float* ws, int cfg, void* stream);
 /* dw[N,K] = dy^T x; db[N] = colsum(dy) (nullable; fused when db == dw + N*K) */
 int hvit_linear_wgrad(int dt, const void* dy, const void* x, int M, int N, int K, float* dw, float* db,
                       float* ws, long long ws_elems, void* stream);

@@ -151,6 +151,7 @@ _SIGS = {
     "hvit_adamw_dev": ([i32, P(AdamWItem), P(AdamWHyper), vp, vp, vp], i32),
     "hvit_rng_advance": ([vp, vp, vp], i32),
     "hvit_gemm_tune": ([i32, i32], i32),
+    "hvit_probe_gemm_splitk": ([i32, i32, vp, vp, i32, i32, i32, i32, vp, i32, vp], i32),
     "hvit_step_bump": ([vp, i32, f32, vp], i32),
 }
 

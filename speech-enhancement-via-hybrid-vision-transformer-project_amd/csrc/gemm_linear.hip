@@ -58,12 +58,24 @@ int hvit_wgrad_small(const void* dy, const void* x, int M, int N, int K, float* 
                      long long ws_elems, void* stream,
                      hvit_slab_sum_t* job = nullptr);
 
+// Weight-gradient plan (hvit_gemm_tune(6, v)): 0 = round 5's (ring_pick /
+// gemm.h per shape, split-K to ~256 workgroups), 1 = eight K slices for the
+// token-major ViT shapes (1,024 tokens each at B = 32) on the 128x128 ring, or
+// gemm.h's 128x128 kernels for N * K <= 512 * 512 (tools/wgrad_layout_probe.py,
+// profiles/r6_wgrad_layout_probe.txt)
+static int& wgrad_plan_ref() {
+  static int v = 0;
+  return v;
+}
+static int wgrad_plan_splits(int M) { return std::max(1, std::min(8, M / 1024)); }
+
 extern "C" long long hvit_wgrad_workspace(int M, int N, int K) {
   // dw is [N_out x K_in] reduced over M rows; slabs only when splitting, each
   // slab followed by N_out bias partials (enough for every tile configuration
   // the entry point may pick: gemm.h's 128x128, the ring's 128x128 / 128x64,
   // the tall-skinny kernel of wgrad_small.hip)
   int s = std::max(wgrad_splits(N, K, M, LIN_WG_BM, LIN_WG_BN), wgrad_splits(N, K, M, 128, 64));
+  s = std::max(s, wgrad_plan_splits(M));
   const long long g = s > 1 ? (long long)s * ((long long)N * K + N) : 0;
   // + room for the two-level bias column sums of a tall dy (hvit_reduce_rows_ws)
   return std::max(std::max(g, 64LL * N),
@@ -167,10 +179,15 @@ static int linear_wgrad_impl(int dt, const void* dy, const void* x, int M, int N
   }
   const bool fused_db = db && dt == HVIT_BF16 && db == dw + NK;
   // ring-pipelined kernels (gemm_ring.h) for bf16 without fused bias row sums
-  const int rcfg = ring_default_cfg() >= 0 ? ring_default_cfg() : ring_pick(false, false, N, K, M);
+  const bool plan1 = wgrad_plan_ref() == 1 && dt == HVIT_BF16 && !fused_db && ring_default_cfg() < 0;
+  const int rcfg = ring_default_cfg() >= 0 ? ring_default_cfg()
+                   : plan1                 ? ((long)N * K <= 512L * 512 ? 0 : 2)
+                                           : ring_pick(false, false, N, K, M);
+  if (plan1) splits = wgrad_plan_splits(M);
+  if ((long long)splits * (NK + N) > ws_elems || !ws) splits = 1;
   if (dt == HVIT_BF16 && !fused_db && N % 8 == 0 && K % 8 == 0 && rcfg > 0) {
     const RingCfg r = ring_cfg(rcfg);
-    int s = wgrad_splits(N, K, M, r.bm, r.bn);
+    int s = plan1 ? wgrad_plan_splits(M) : wgrad_splits(N, K, M, r.bm, r.bn);
     if ((long long)s * (NK + N) > ws_elems || !ws) s = 1;
     s = plan_splits<bf16_t>(M, s);
     Epi e;
@@ -244,6 +261,11 @@ extern "C" int hvit_gemm_tune(int what, int value) {
   if (what == 1) return hvit_c1_tune(value);
   // (3: the round-5 persistent epilogue-overlapped kernels, measured slower and
   // removed in round 6 -- git history before that round has gemm_pp.hip)
+  if (what == 6) {  // weight-gradient plan (wgrad_plan_ref)
+    const int old = wgrad_plan_ref();
+    wgrad_plan_ref() = value;
+    return old;
+  }
   if (what == 4) return hvit_attn_tune(value);  // attention backward for N <= 256: 1 single pass, 0 two kernels
   if (what == 5) return hvit_fp8_tune(value);  // fp8 attention forward: 0 round-4 kernel, 1 v2 16 waves, 2 v2 8 waves
   if (what == 2) {  // workgroup target of the linear weight gradients' split-K (0: default)
@@ -255,4 +277,37 @@ extern "C" int hvit_gemm_tune(int what, int value) {
   const int old = ring_cfg_ref();
   ring_cfg_ref() = value;
   return old;
+}
+
+// Diagnostics (tools/wgrad_layout_probe.py): a weight-gradient-shaped split-K
+// GEMM C[M, N] = sum_k A[m, k] B[n, k] into f32 slabs ws[splits][M * N + M]
+// with each operand K-contiguous (kc = 1: rows of K, the forward layout) or
+// M / N-contiguous (kc = 0: [K][M] / [K][N], the layout a weight gradient
+// reads its token-major operands in), on pipeline cfg (0: gemm.h's kernels,
+// 1-5: a gemm_ring.h configuration).  Used to price the operand layout and the
+// tile / split choice of the weight gradients; not on the model's path.
+extern "C" int hvit_probe_gemm_splitk(int kca, int kcb, const void* a, const void* b, int M, int N, int K, int splits,
+                                      float* ws, int cfg, void* stream) {
+  HVIT_CHECK(a && b && ws && M > 0 && N > 0 && K > 0 && splits >= 1, "hvit_probe_gemm_splitk: bad args");
+  HVIT_CHECK(aligned16(a) && aligned16(b) && M % 8 == 0 && N % 8 == 0 && K % 64 == 0, "hvit_probe_gemm_splitk: align");
+  Epi e;
+  e.out_dt = HVIT_F32;
+  e.ldo = N;
+  e.mode = splits > 1 ? EPI_SLAB : EPI_STORE;
+  e.out = ws;
+  e.slab_stride = (long)M * N + M;
+  hipStream_t st = (hipStream_t)stream;
+  auto go = [&](auto la, auto lb) -> int {
+    int rc = 0;
+    if (cfg > 0) {
+      if (try_ring(la, lb, M, N, K, splits, e, st, &rc, cfg)) return rc;
+      hvit_set_error("hvit_probe_gemm_splitk: ring configuration %d does not apply", cfg);
+      return HVIT_ERR_ARG;
+    }
+    return launch_gemm<bf16_t>(la, lb, M, N, K, splits, e, st);
+  };
+  if (kca && kcb) return go(dense<bf16_t, true>(a, K, M, K), dense<bf16_t, true>(b, K, N, K));
+  if (kca) return go(dense<bf16_t, true>(a, K, M, K), dense<bf16_t, false>(b, N, N, K));
+  if (kcb) return go(dense<bf16_t, false>(a, M, M, K), dense<bf16_t, true>(b, K, N, K));
+  return go(dense<bf16_t, false>(a, M, M, K), dense<bf16_t, false>(b, N, N, K));
 }

@@ -669,6 +669,9 @@ class CastFn(torch.autograd.Function):
 
 
 SKIPGRAD = True  # False: autograd adds the skip gradients
+# the gradient at a LayerNorm output (a linear's data gradient) in the compute
+# dtype; False: f32 (the round-5 form)
+LN_DY_LOW = True
 
 
 class SkipGrad:
@@ -1276,10 +1279,14 @@ class ViTBlockFn(torch.autograd.Function):
             j1 = None
         else:
             df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id), side=jc)
-        dxn2 = torch.empty((M, D), dtype=torch.float32, device=dev)
+        # the gradient at the LayerNorm output in the compute dtype (bf16 under the
+        # bf16 model, as torch autocast's linear backward gives it): 8 MB less to
+        # store and to re-read per LayerNorm backward at B=32 (dx stays f32)
+        dxn2 = _empty((M, D), dt if LN_DY_LOW else F32, dev)
         e_fc1 = epilogue(side=j1)
         _launch("vit_linear_dgrad", 2.0 * M * hid * D,
-                lambda e: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(), F32,
+                lambda e: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(),
+                               L.dt_of(dxn2),
                                e, s), e_fc1)
         jln = None
         if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass; its
@@ -1332,11 +1339,11 @@ class ViTBlockFn(torch.autograd.Function):
             jq = None
         else:
             dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
-        dxn1 = torch.empty((M, D), dtype=torch.float32, device=dev)
+        dxn1 = _empty((M, D), dt if LN_DY_LOW else F32, dev)
         e_qkv = epilogue(side=jq)
         _launch("vit_linear_dgrad", 2.0 * M * 3 * D * D,
                 lambda e: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
-                               F32, e, s), e_qkv)
+                               L.dt_of(dxn1), e, s), e_qkv)
         if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
             dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         else:
@@ -1377,8 +1384,8 @@ class HeadFn(torch.autograd.Function):
         M = B * Nt
         dy = cast(dy, dt)
         dw, db, jw = _linear_wgrad_bias_maybe_side(ctx, dt, dy, xn, M, C, D)
-        dxn = torch.empty((M, D), dtype=torch.float32, device=dy.device)
-        call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), F32,
+        dxn = _empty((M, D), dt if LN_DY_LOW else F32, dy.device)
+        call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), L.dt_of(dxn),
              epilogue(side=jw) if jw is not None else None, stream_ptr())  # (carries the wgrad's slab sum)
         if ctx.ho is not None and ctx.ho.drop is not None:  # the last block's fc2 dropout, fused
             dx, dnw, dnb = ctx.ho.fuse(dxn, x2d, m, r, nw, None, ctx.zs)
