@@ -185,6 +185,30 @@ int hvit_linear_wgrad_bias_defer(int dt, const void* dy, const void* x, int M, i
                                  void* stream);
 int hvit_sum_slabs_strided(const float* ws, int splits, long long stride, long long n, float* out, void* stream);
 
+/* ---- Grouped weight gradients (the ViT Linears' dW of several blocks in one
+ * launch; attention.py:55,58 qkv / proj, components.py:224,227 fc1 / fc2 --
+ * the reference's autograd computes each as its own addmm).  Problem p:
+ * dw[n_out][k_in] = dy[M][0:n_out]^T x[M][0:k_in] (bf16 operands with row
+ * pitches ldy / ldx, f32 result, overwritten).  Every 256x256 output tile runs
+ * over the whole token range M; when the tiles do not divide evenly over the
+ * CUs, the remainder tiles are split into K pieces summed in piece order by
+ * the last piece to arrive (deterministic).  ws: hvit_linear_wgrad_group_ws()
+ * f32 elements; tickets: hvit_linear_wgrad_group_tickets() uint32 counters,
+ * zeroed by the caller once, left zeroed by every call. */
+typedef struct {
+  const void* dy;
+  int ldy;
+  const void* x;
+  int ldx;
+  float* dw;
+  int n_out, k_in;
+} hvit_wgrad_prob_t;
+int hvit_linear_wgrad_group_ok(int dt, int M, int n_out, int k_in); /* 1: the shape can join a group */
+long long hvit_linear_wgrad_group_ws(void);
+long long hvit_linear_wgrad_group_tickets(void);
+int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* probs, int nprobs, float* ws, long long ws_elems,
+                            unsigned* tickets, long long n_tickets, void* stream);
+
 /* ---- Convolution as implicit GEMM (ConvBlock conv components.py:55-62,
  * TransposeConvBlock upsample+conv components.py:146-158, PatchEmbedding
  * conv components.py:275-280, decoder concat hybrid_vit.py:389).

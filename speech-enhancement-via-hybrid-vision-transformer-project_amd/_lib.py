@@ -39,6 +39,11 @@ class SlabSum(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("n", i64), ("stride", i64), ("splits", i32)]
 
 
+class WgradProb(C.Structure):
+    """hvit_wgrad_prob_t: one weight gradient of a grouped launch."""
+    _fields_ = [("dy", vp), ("ldy", i32), ("x", vp), ("ldx", i32), ("dw", vp), ("n_out", i32), ("k_in", i32)]
+
+
 class Epilogue(C.Structure):
     _fields_ = [
         ("act", i32), ("out2", vp), ("out2_dt", i32), ("aux", vp), ("aux_dt", i32),
@@ -93,6 +98,10 @@ _SIGS = {
                                      i32),
     "hvit_mhsa_bias_rows": ([i32, i32, i32, i32, i32], i64),
     "hvit_sum_slabs_strided": ([vp, i32, i64, i64, vp, vp], i32),
+    "hvit_linear_wgrad_group_ok": ([i32, i32, i32, i32], i32),
+    "hvit_linear_wgrad_group_ws": ([], i64),
+    "hvit_linear_wgrad_group_tickets": ([], i64),
+    "hvit_linear_wgrad_group": ([i32, i32, P(WgradProb), i32, vp, i64, vp, i64, vp], i32),
     "hvit_linear_wgrad_tk": ([i32, vp, vp, i32, i32, i32, vp, vp, vp, i64, vp, i64, i32, vp], i32),
     "hvit_conv_fwd": ([i32, P(ConvGeom), vp, vp, vp, i32, vp, P(Epilogue), vp], i32),
     "hvit_conv_dgrad": ([i32, P(ConvGeom), vp, vp, vp, i32, vp], i32),

@@ -332,6 +332,10 @@ class GradAllReducer:
         flat = self.flats[b][self._gen]
         if flat is None or flat.device != dev:
             flat = self.flats[b][self._gen] = torch.empty(total, dtype=torch.float32, device=dev)
+        if dev.type == "cuda":
+            # weight gradients queued for a grouped launch (functional.wgrad_enqueue)
+            # are computed before any bucket reads them
+            HF.wgrad_flush(dev)
         ctx = contextlib.nullcontext()
         if dev.type == "cuda" and HF.side_pending(dev):
             # weight gradients still in flight on the side stream (functional.on_side):

@@ -566,6 +566,98 @@ def side_ok(prefs) -> bool:
     return True
 
 
+# ---------------------------------------------------------------------------
+# Grouped weight gradients (round 6, hvit_linear_wgrad_group).  Each ViT Linear's
+# weight gradient is a GEMM with a small output and a long token reduction
+# (8,192 tokens at B = 32): alone it fills the chip only by splitting K into
+# short slices with f32 partial slabs.  Nothing reads a weight gradient before
+# the optimizer, so the ViT blocks' backward queues them instead (the operands
+# are kept alive by the queue) and one launch runs the whole queue: every
+# 256x256 output tile over the full token range, written once.  The queue is
+# flushed (1) by an autograd final callback at the end of the backward, (2) by
+# the data-parallel reducer right before it launches a bucket (dp.py), and (3)
+# by any caller that needs the gradients earlier (wgrad_flush).  A parameter
+# that already holds a .grad (accumulation) is not queued: autograd adds its
+# gradient at once.  The tensor handed to autograd is a fresh view of the
+# result buffer; the queue holds a different view of the same storage, so
+# autograd adopts the handed view as .grad without a copy (a copy made before
+# the flush would copy unwritten memory: the flush re-copies such a .grad).
+WGRAD_GROUP = True
+_WG_QUEUE = {}    # device index -> [(dy, x, dw_view, n, k, M, pref)]
+_WG_TASKS = set()  # autograd graph tasks that have the flush queued
+_WG_TICKETS = {}  # device index -> zeroed uint32 counters (left zeroed by every launch)
+
+
+def wgrad_group_ok(dt, M, N, K, pref=None) -> bool:
+    """The weight gradient dW[N, K] over M tokens may join the group queue."""
+    if not WGRAD_GROUP or SIDE or dt != BF16:
+        return False
+    if pref is not None:
+        p = pref()
+        if p is not None and p.grad is not None:
+            return False
+    return bool(L.lib().hvit_linear_wgrad_group_ok(dt, M, N, K))
+
+
+def wgrad_enqueue(dy, x, M, N, K, dest=None, pref=None) -> torch.Tensor:
+    """Queue dW[N, K] = dy[M, :N]^T x[M, :K] (bf16 operands, row pitches taken
+    from the tensors); returns the f32 gradient tensor, final once the queue
+    is flushed."""
+    dev = dy.device
+    i = _dev_index(dev)
+    dw = dest.view(N, K) if dest is not None else torch.empty((N, K), dtype=torch.float32, device=dev)
+    q = _WG_QUEUE.setdefault(i, [])
+    q.append((dy, x, dw.view(-1), N, K, M, pref))
+    task = torch._C._current_graph_task_id()
+    if task >= 0 and task not in _WG_TASKS:
+        _WG_TASKS.add(task)
+        torch.autograd.Variable._execution_engine.queue_callback(_wgrad_flush_all)
+    return dw
+
+
+def _wgrad_flush_all():
+    for i in list(_WG_QUEUE):
+        wgrad_flush(torch.device("cuda", i))
+    _WG_TASKS.clear()
+
+
+def wgrad_flush(dev=None) -> None:
+    """Launch every queued weight gradient of ``dev`` (one grouped launch per
+    token count) on the current stream."""
+    i = _dev_index(dev) if dev is not None else torch.cuda.current_device()
+    q = _WG_QUEUE.pop(i, None)
+    if not q:
+        return
+    d = torch.device("cuda", i)
+    tk = _WG_TICKETS.get(i)
+    if tk is None:
+        tk = _WG_TICKETS[i] = torch.zeros(int(L.lib().hvit_linear_wgrad_group_tickets()), dtype=torch.int32,
+                                          device=d)
+    ws = torch.empty(int(L.lib().hvit_linear_wgrad_group_ws()), dtype=torch.float32, device=d)
+    by_m = {}
+    for job in q:
+        by_m.setdefault(job[5], []).append(job)
+    for M, jobs in by_m.items():
+        arr = (L.WgradProb * len(jobs))()
+        flops = 0.0
+        for j, (dy, x, dw, n, k, _, _) in enumerate(jobs):
+            arr[j] = L.WgradProb(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), n, k)
+            flops += 2.0 * M * n * k
+
+        def launch(arr=arr, n=len(jobs), M=M, jobs=jobs):
+            call("hvit_linear_wgrad_group", BF16, M, arr, n, ws.data_ptr(), ws.numel(), tk.data_ptr(), tk.numel(),
+                 stream_ptr())
+
+        with timed("vit_linear_wgrad", flops):
+            launch()
+        _record("vit_linear_wgrad", (lambda launch=launch, ws=ws: launch(), flops))
+    for dy, x, dw, n, k, _, pref in q:
+        p = pref() if pref is not None else None
+        if p is not None and p.grad is not None and p.grad.data_ptr() != dw.data_ptr():
+            # autograd copied the handed tensor before it was written
+            p.grad.copy_(dw.view(n, k))
+
+
 class Deferred:
     """A weight gradient whose split-K slab sum is handed to the next linear
     launch on the stream (hvit_linear_wgrad_defer): ``job`` goes into that
@@ -1206,6 +1298,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
         # the parameters whose gradients the side stream may produce (side_ok)
         ctx.prefs = tuple(weakref.ref(p) for p in (qkvw, qkvb, pw, f1w, f1b, f2w))
+        ctx.wrefs = tuple(weakref.ref(p) for p in (qkvw, pw, f1w, f2w))  # (the grouped weight gradients)
         ctx.kbits = kbits
         # the fc2 branch's dropout / DropPath of the incoming gradient, for the
         # next consumer of x2 to fuse into its LayerNorm backward (GradHandoff)
@@ -1248,6 +1341,12 @@ class ViTBlockFn(torch.autograd.Function):
         # gradients (side_ok), or else on this stream with each split-K slab sum riding
         # on the data-gradient launch that follows it (epilogue side job)
         side = side_ok(ctx.prefs)
+        # or queued for one grouped launch with the other blocks' (wgrad_enqueue):
+        # each then carries nothing, and the bias / LayerNorm partial-row sums the
+        # weight-gradient launches carried ride on the data-gradient launches
+        wq, wp, w1, w2 = ctx.wrefs
+        group = (not side and wgrad_group_ok(dt, M, D, hid, w2) and wgrad_group_ok(dt, M, hid, D, w1)
+                 and wgrad_group_ok(dt, M, D, D, wp) and wgrad_group_ok(dt, M, 3 * D, D, wq))
 
         def wdest(wid, N, K):
             d = grad_dest(*wid)
@@ -1258,6 +1357,8 @@ class ViTBlockFn(torch.autograd.Function):
             with on_side(dev, (g2, a, df2w)):
                 linear_wgrad_now(dt, g2, a, M, D, hid, dest=df2w)
             j2 = None
+        elif group:
+            df2w, j2 = wgrad_enqueue(g2, a, M, D, hid, grad_dest(*d2_id), w2), None
         else:
             df2w, j2 = linear_wgrad_deferred(dt, g2, a, M, D, hid, dest=grad_dest(*d2_id))
         dh = _empty((M, hid), dt, dev)
@@ -1277,6 +1378,8 @@ class ViTBlockFn(torch.autograd.Function):
             with on_side(dev, (dh, xn2, cparts, df1b, df1w)):
                 linear_wgrad_now(dt, dh, xn2, M, hid, D, dest=df1w, side=jc)
             j1 = None
+        elif group:
+            df1w, j1 = wgrad_enqueue(dh, xn2, M, hid, D, grad_dest(*d1_id), w1), jc
         else:
             df1w, j1 = linear_wgrad_deferred(dt, dh, xn2, M, hid, D, dest=grad_dest(*d1_id), side=jc)
         # the gradient at the LayerNorm output in the compute dtype (bf16 under the
@@ -1304,6 +1407,8 @@ class ViTBlockFn(torch.autograd.Function):
             with on_side(dev, (g1, o, dpw) + (jln.ws if jln is not None else ())):
                 linear_wgrad_now(dt, g1, o, M, D, D, dest=dpw, side=jln)
             jp = None
+        elif group:
+            dpw, jp = wgrad_enqueue(g1, o, M, D, D, grad_dest(*dp_id), wp), jln
         else:
             dpw, jp = linear_wgrad_deferred(dt, g1, o, M, D, D, dest=grad_dest(*dp_id), side=jln)
         do = _empty((M, D), dt, dev)
@@ -1337,6 +1442,8 @@ class ViTBlockFn(torch.autograd.Function):
             with on_side(dev, (dqkv, xn1, dqkvw, dqkvb) + ((jb.ws,) if jb is not None else ())):
                 linear_wgrad_now(dt, dqkv, xn1, M, 3 * D, D, dest=dqkvw, side=jb)
             jq = None
+        elif group:
+            dqkvw, jq = wgrad_enqueue(dqkv, xn1, M, 3 * D, D, grad_dest(*dq_id), wq), jb
         else:
             dqkvw, jq = linear_wgrad_deferred(dt, dqkv, xn1, M, 3 * D, D, dest=grad_dest(*dq_id), side=jb)
         dxn1 = _empty((M, D), dt if LN_DY_LOW else F32, dev)

@@ -169,7 +169,8 @@ def test_side_stream_weight_gradients_equal_single_stream(hv, kw):
     x = torch.rand(shape, generator=g).to(DEV)
     t = torch.rand(shape, generator=g).to(DEV)
     runs = []
-    old = HF.SIDE
+    old, oldg = HF.SIDE, HF.WGRAD_GROUP
+    HF.WGRAD_GROUP = False  # (the per-Linear weight gradients on either stream; the grouped launch is not)
     try:
         for side in (False, True):
             HF.SIDE = side
@@ -181,7 +182,7 @@ def test_side_stream_weight_gradients_equal_single_stream(hv, kw):
             torch.cuda.synchronize()
             runs.append((first, {n: p.grad.clone() for n, p in m.named_parameters()}))
     finally:
-        HF.SIDE = old
+        HF.SIDE, HF.WGRAD_GROUP = old, oldg
     for n in runs[0][0]:
         assert torch.equal(runs[0][0][n], runs[1][0][n]), n
         assert torch.equal(runs[0][1][n], runs[1][1][n]), n
