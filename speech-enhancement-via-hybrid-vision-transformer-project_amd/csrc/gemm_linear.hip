@@ -256,6 +256,7 @@ extern "C" int hvit_debug_gemm_stamps(unsigned long long* host, int n) {
 // gemm.h's kernels only, 1-5 = one ring configuration; see gemm_ring.h).
 // Returns the previous value.
 int hvit_c1_tune(int value);  // c1block.hip
+int hvit_wgrad_group_tune(int value);  // wgrad_group.hip
 
 extern "C" int hvit_gemm_tune(int what, int value) {
   if (what == 1) return hvit_c1_tune(value);
@@ -266,6 +267,7 @@ extern "C" int hvit_gemm_tune(int what, int value) {
     wgrad_plan_ref() = value;
     return old;
   }
+  if (what == 7) return hvit_wgrad_group_tune(value);  // grouped weight gradients: 0 256x256 tiles, 1 256x128
   if (what == 4) return hvit_attn_tune(value);  // attention backward for N <= 256: 1 single pass, 0 two kernels
   if (what == 5) return hvit_fp8_tune(value);  // fp8 attention forward: 0 round-4 kernel, 1 v2 16 waves, 2 v2 8 waves
   if (what == 2) {  // workgroup target of the linear weight gradients' split-K (0: default)

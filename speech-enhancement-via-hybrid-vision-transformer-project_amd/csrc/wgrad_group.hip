@@ -31,8 +31,158 @@
 namespace hvit_wg {
 using namespace hvit;
 
-constexpr int BM = 256, BN = 256, MAXP = 56;
-using Core = RingCore<BM, BN, 2, 4, 2, false, false>;
+constexpr int BM = 256, MAXP = 56;  // (every configuration's tiles are BM = 256 rows of dw)
+
+// The weight gradients' K loop with 32-deep stages: both operands token-major
+// (MN images, transposed fragment reads), one 16x16x32 MFMA k-step per stage,
+// NB stages in the LDS ring so NB - 1 of them (NB - 1 x 32 KiB at 256 x 256)
+// are in flight under each stage's MFMAs -- the 64-deep two-stage ring keeps
+// one 64 KiB stage in flight and its K loop waited on that stage's landing
+// (counters, profiles/r6_wgrad_group_pmc.json: ~41 % of wave cycles in
+// s_waitcnt at 31 % MFMA busy).  The images are the first 32 k rows of
+// gemm.h's 64-deep MN images (DmaImg / MnSwz: rows are k, so the same source
+// swizzle and transposed reads apply).
+template <int BM_, int BN_, int WM, int WN, int NB, bool PIPE>
+struct Ring32 {
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  using IA = DmaImg<BM_, false>;
+  using IB = DmaImg<BN_, false>;
+  static constexpr int BK = 32;
+  static constexpr int ABYTES = IA::BYTES / 2, BBYTES = IB::BYTES / 2;
+  static constexpr int WTM = BM_ / WM, WTN = BN_ / WN, FM = WTM / 16, FN = WTN / 16;
+  static constexpr int PA = IA::PIECES / 2 / NW, PB = IB::PIECES / 2 / NW;
+  static constexpr int INFL = PA + PB;  // this wave's DMA instructions per stage
+  static constexpr int STAGE = ABYTES + BBYTES;
+  static constexpr int SM = NB * STAGE;
+  static_assert(IA::PIECES % (2 * NW) == 0 && IB::PIECES % (2 * NW) == 0, "stage pieces must split over the waves");
+  static_assert(NB >= 2 && (NB - 2) * INFL <= 63, "ring depth / vmcnt range");
+  static constexpr int MPD = (FM * FN) / INFL > 0 ? (FM * FN) / INFL : 1;
+  static_assert(MPD * INFL <= FM * FN, "interleave");
+
+  __device__ __forceinline__ static __amdgpu_buffer_rsrc_t rsrc(const LdDense<bf16_t, false>& l) {
+    const long bytes = (long)l.K * l.ld * 2;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)l.p, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                             0x00020000);
+  }
+
+  __device__ __forceinline__ static void run(const LdDense<bf16_t, false>& la, const LdDense<bf16_t, false>& lb,
+                                             char* smem, int m0, int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN]) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int nk = (kend - kbeg) / BK;
+    if (nk <= 0) return;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(la), rb = rsrc(lb);
+    const unsigned oa = (unsigned)(((long)kbeg * la.ld + m0) * 2), da = (unsigned)((long)BK * la.ld * 2);
+    const unsigned ob = (unsigned)(((long)kbeg * lb.ld + n0) * 2), db = (unsigned)((long)BK * lb.ld * 2);
+    unsigned va[PA], vb[PB];
+#pragma unroll
+    for (int i = 0; i < PA; ++i) va[i] = IA::src_off(wid + NW * i, lane, la.ld);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) vb[i] = IB::src_off(wid + NW * i, lane, lb.ld);
+    // stage t -> ring buffer t % NB; stages past the end re-read the last one
+    // into a buffer never read again (a constant DMA count per iteration)
+    auto issue = [&](int t) {
+      char* abuf = smem + (t % NB) * STAGE;
+      char* bbuf = abuf + ABYTES;
+      const int ts = t < nk ? t : nk - 1;
+      const unsigned sa = oa + (unsigned)ts * da, sb = ob + (unsigned)ts * db;
+#pragma unroll
+      for (int i = 0; i < PA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(abuf + (wid + NW * i) * 1024),
+                                                 16, va[i], sa, 0, 0);
+#pragma unroll
+      for (int i = 0; i < PB; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(bbuf + (wid + NW * i) * 1024),
+                                                 16, vb[i], sb, 0, 0);
+    };
+#pragma unroll
+    for (int t = 0; t < NB - 1; ++t) issue(t);
+    for (int t = 0; t < nk; ++t) {
+      // stage t landed for this wave (NB-2 younger stages stay in flight) and,
+      // after the barrier, for every wave; every wave has also finished reading
+      // stage t-1, whose buffer (t+NB-1) % NB the issue below refills
+      __builtin_amdgcn_s_waitcnt(vm_imm((NB - 2) * INFL));
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* at = smem + (t % NB) * STAGE;
+      const char* bt = at + ABYTES;
+      u32x4 fa[FM], fb[FN];
+      if constexpr (!PIPE) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = IA::frag(at, wm * WTM + i * 16, 0, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, 0, lane);
+        issue(t + NB - 1);
+        lgkm_wait0();
+        lds_pin(fa);
+        lds_pin(fb);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
+                                                                __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+      } else {
+        // B fragments and the first half of the A fragments, then the second
+        // half's reads in flight under the first half's MFMAs (with the stage's
+        // DMA issue spread over them)
+        constexpr int H = FM / 2;
+        u32x4 fa0[H], fa1[H];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, 0, lane);
+#pragma unroll
+        for (int i = 0; i < H; ++i) fa0[i] = IA::frag(at, wm * WTM + i * 16, 0, lane);
+        lgkm_wait0();
+        lds_pin(fb);
+        lds_pin(fa0);
+#pragma unroll
+        for (int i = 0; i < H; ++i) fa1[i] = IA::frag(at, wm * WTM + (H + i) * 16, 0, lane);
+        issue(t + NB - 1);
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa0[i]),
+                                                                __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, H * 2, 0);  // the second half's fragment reads first
+#pragma unroll
+        for (int k = 0; k < INFL; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, (H * FN) / INFL, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                // one DMA piece
+        }
+        lgkm_wait0();
+        lds_pin(fa1);
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[H + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa1[i]),
+                                                                    __builtin_bit_cast(s16x8, fb[j]), acc[H + i][j], 0, 0,
+                                                                    0);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(vm_imm(0));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+};
+
+// the K loop of a configuration: gemm_ring.h's 64-deep ring or the 32-deep one
+template <int BN, int WM, int WN, int NB, int DEEP>
+struct CoreOf {
+  using T = RingCore<256, BN, WM, WN, NB, false, false>;
+};
+template <int BN, int WM, int WN, int NB>
+struct CoreOf<BN, WM, WN, NB, 1> {
+  using T = Ring32<256, BN, WM, WN, NB, false>;
+};
+template <int BN, int WM, int WN, int NB>
+struct CoreOf<BN, WM, WN, NB, 2> {
+  using T = Ring32<256, BN, WM, WN, NB, true>;
+};
 
 struct Prob {
   const bf16_t* dy;
@@ -51,7 +201,7 @@ struct Table {
   int GB8;             // phase-B blocks / 8 (grid = R * G + 8 * GB8)
   int R, T;            // whole-tile rounds, tiles
   int rem0, s, pu;     // first phase-B tile, pieces per tile, units (64-token stages) per piece
-  float* slabs;        // [G][BM * BN]
+  float* slabs;        // [G][BM * 256] (a piece's slab holds BM x BN, pitch BN)
   unsigned* tickets;   // one per phase-B tile, zero on entry and on exit
 };
 
@@ -61,9 +211,17 @@ __device__ __forceinline__ const Prob& find(const Table& tb, int t) {
   return tb.p[i];
 }
 
+// tile configurations: BN columns of dw per tile, WM x WN waves, NB ring stages
+//   0: 256 x 256, 2 x 4 waves, 2 stages (128 KiB: one stage in flight)
+//   1: 256 x 128, 4 x 2 waves, 3 stages (144 KiB: two stages in flight)
+//   2: 256 x 256, 2 x 4 waves, 32-deep stages, 4 in the ring (128 KiB: three 32 KiB stages in flight)
+//   3: the same with 5 stages (160 KiB: four in flight)
+//   4: cfg 2 with half of each stage's fragment reads under the other half's MFMAs
+//   5: cfg 4 with 3 stages
+template <int BN, int WM, int WN, int NB, int DEEP>
 __global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
+  using Core = typename CoreOf<BN, WM, WN, NB, DEEP>::T;
   constexpr int NT = Core::NT, FM = Core::FM, FN = Core::FN, WTM = Core::WTM, WTN = Core::WTN;
-  constexpr int WN = 4;
   constexpr int CP = BN + 4;  // LDS tile pitch (floats)
   constexpr int C8 = BN / 8, RS8 = NT / C8, NR8 = 64 / RS8;
   constexpr int SM_E = 64 * CP * 4 + 16;
@@ -94,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
     const int m0 = (lt / pr.tn) * BM, n0 = (lt % pr.tn) * BN;
     const int kbeg = pb ? (w % tb.s) * tb.pu * 64 : 0;
     const int kend = pb ? min(tb.M, kbeg + tb.pu * 64) : tb.M;
-    float* dst = pb ? tb.slabs + (long)w * (BM * BN) : pr.dw + (long)m0 * pr.k_in + n0;
+    float* dst = pb ? tb.slabs + (long)w * (BM * 256) : pr.dw + (long)m0 * pr.k_in + n0;
     const int ldo = pb ? BN : pr.k_in;
     LdDense<bf16_t, false> la, lb;
     la.p = pr.dy; la.ld = pr.ldy; la.rows = pr.n_out; la.K = tb.M; la.vok = true;
@@ -104,7 +262,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    Core::run(la, lb, smem, m0, n0, kbeg, kend, acc, none);
+    if constexpr (DEEP) Core::run(la, lb, smem, m0, n0, kbeg, kend, acc);
+    else Core::run(la, lb, smem, m0, n0, kbeg, kend, acc, none);
     // the result staged through LDS in 64-row passes; a thread stores 8
     // adjacent f32 columns per row (two 16-byte stores)
 #pragma unroll
@@ -149,7 +308,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
     if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const float* s0 = tb.slabs + (long)(rt * tb.s) * (BM * BN);
+    const float* s0 = tb.slabs + (long)(rt * tb.s) * (BM * 256);
     float* dw = pr.dw + (long)m0 * pr.k_in + n0;
 #pragma unroll 2
     for (int i = 0; i < BM / RS8; ++i) {
@@ -157,7 +316,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
       const float* src = s0 + row * BN + c8 * 8;
       f32x4 sa = *(const f32x4*)src, sb = *(const f32x4*)(src + 4);
       for (int z = 1; z < tb.s; ++z) {
-        const float* q = src + (long)z * (BM * BN);
+        const float* q = src + (long)z * (BM * 256);
         sa += *(const f32x4*)q;
         sb += *(const f32x4*)(q + 4);
       }
@@ -201,16 +360,28 @@ static void plan(Table& tb, int T, int M) {
   }
 }
 
+// tile configuration (hvit_gemm_tune(7, v), A/B measurements)
+static int& cfg_ref() {
+  static int c = 2;  // (isolated loop, tools/wgrad_group_probe.py: 6 blocks at B = 32 356 -> 333-341 us, config 5 770 -> 720)
+  return c;
+}
+
 }  // namespace hvit_wg
 
 using namespace hvit_wg;
 
+int hvit_wgrad_group_tune(int value) {
+  const int old = cfg_ref();
+  if (value >= 0 && value <= 5) cfg_ref() = value;
+  return old;
+}
+
 extern "C" int hvit_linear_wgrad_group_ok(int dt, int M, int n_out, int k_in) {
-  return dt == HVIT_BF16 && M > 0 && M % 64 == 0 && n_out > 0 && k_in > 0 && n_out % BM == 0 && k_in % BN == 0 &&
+  return dt == HVIT_BF16 && M > 0 && M % 64 == 0 && n_out > 0 && k_in > 0 && n_out % BM == 0 && k_in % 256 == 0 &&
          (long long)M * std::max(n_out, k_in) * 2 < (1LL << 31);
 }
 
-extern "C" long long hvit_linear_wgrad_group_ws(void) { return (long long)num_cus() * BM * BN; }
+extern "C" long long hvit_linear_wgrad_group_ws(void) { return (long long)num_cus() * BM * 256; }
 extern "C" long long hvit_linear_wgrad_group_tickets(void) { return (long long)num_cus(); }
 
 extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* probs, int nprobs, float* ws,
@@ -233,6 +404,8 @@ extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* p
                "hvit_linear_wgrad_group: problem %d operand too large for 32-bit offsets", i);
   }
   hipStream_t st = (hipStream_t)stream;
+  const int cfg = cfg_ref();
+  const int BN = cfg == 1 ? 128 : 256;
   for (int c0 = 0; c0 < nprobs; c0 += MAXP) {
     const int np = std::min(MAXP, nprobs - c0);
     Table tb{};
@@ -257,7 +430,19 @@ extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* p
     tb.tickets = tickets;
     plan(tb, T, M);
     if (T == 0) continue;
-    hipLaunchKernelGGL(wgrad_group_kernel, dim3(tb.R * tb.G + 8 * tb.GB8), dim3(512), 0, st, tb);
+    const dim3 grid(tb.R * tb.G + 8 * tb.GB8);
+    if (cfg == 1)
+      hipLaunchKernelGGL((wgrad_group_kernel<128, 4, 2, 3, 0>), grid, dim3(512), 0, st, tb);
+    else if (cfg == 2)
+      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 4, 1>), grid, dim3(512), 0, st, tb);
+    else if (cfg == 3)
+      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 5, 1>), grid, dim3(512), 0, st, tb);
+    else if (cfg == 4)
+      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 4, 2>), grid, dim3(512), 0, st, tb);
+    else if (cfg == 5)
+      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 3, 2>), grid, dim3(512), 0, st, tb);
+    else
+      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 2, 0>), grid, dim3(512), 0, st, tb);
     HVIT_LAUNCH_CHECK();
   }
   return HVIT_OK;

@@ -190,9 +190,11 @@ class GradAllReducer:
         # host-side group for the token-bound agreement: a CPU all_reduce on gloo
         # needs no device sync (on an nccl group an int read back would stall the
         # host until the whole backward had run)
+        # (also GraphedTrainStep's per-call eager / replay agreement: a replaying rank's
+        # collectives go to the capture group, an eager rank's to this group)
         self._agree = bool(self.sliced) and self.world > 1
         self._host_group = self.group
-        if self._agree and dist.get_backend(self.group) != "gloo":
+        if self.world > 1 and dist.get_backend(self.group) != "gloo":
             self._host_group = _gloo_group(self.group)
         # collectives issued inside a hipGraph capture go to their own NCCL group
         # (capture_group: the watchdog never polls a work of it)

@@ -24,10 +24,10 @@ shape (LRU-capped):
 * the optimizer's hyper-parameters are read on the device
   (``FusedAdamW.sync_hyper`` before every call), so a replay uses the current
   learning rate of an LR scheduler (trainer.py:304-309), not the captured one;
-* under data parallelism with a sliced ``GradAllReducer`` (whose eager steps
-  agree the token bound over a gloo group), every call first agrees over that
-  group whether any rank must run an eager step; then all ranks do, so no rank
-  waits in a host collective that a replaying rank never enters.
+* under data parallelism (a ``GradAllReducer`` over more than one rank) every
+  call first agrees over a gloo group whether any rank must run an eager step;
+  then all ranks do, so no rank waits in a collective (RCCL on the eager group,
+  or a sliced reducer's host agreement) that a replaying rank never enters.
 
 ``step(noisy, clean)`` returns the loss as a device tensor (the graph's static
 output for replays: read it before the next call with the same shape).
@@ -92,18 +92,20 @@ class GraphedTrainStep:
         return (tuple(x.shape), x.dtype, tuple(t.shape), t.dtype, x.device)
 
     def _every_rank(self, flag: bool) -> bool:
-        """True when ``flag`` holds on every rank of the reducer's group.  Only
-        a reducer whose ``finish()`` runs a host (gloo) agreement in eager steps
-        needs this: if one rank ran such an eager step while another replayed a
-        graph (which runs no host collective), the eager rank would wait forever.
-        So every call agrees first -- one gloo all-reduce of a flag, outside any
-        graph -- and all ranks run eager when any of them must.  Cost: host time
-        only (one 8-byte gloo all-reduce, measured 0.22 / 0.49 / 0.86 ms at 2 / 4 /
-        8 ranks on an 8-CPU host), which overlaps the previous replay's GPU time;
+        """True when ``flag`` holds on every rank of the reducer's group.  Ranks
+        must agree on eager vs replay: a replayed step's bucket all-reduces run on
+        the reducer's capture group (dp.capture_group) and an eager step's on its
+        own group, so a rank replaying while another runs eager would wait in
+        collectives of different communicators (and a sliced reducer's eager
+        finish() also runs a host gloo agreement a replay never enters).  So every
+        call agrees first -- one gloo all-reduce of a flag, outside any graph --
+        and all ranks run eager when any of them must.  Cost: host time only (one
+        8-byte gloo all-reduce, measured 0.22 / 0.49 / 0.86 ms at 2 / 4 / 8 ranks
+        on an 8-CPU host), which overlaps the previous replay's GPU time (~5 ms);
         ``uniform_shapes=True`` skips it when the caller feeds every rank the same
-        shape sequence."""
+        shape sequence (every rank's mode is then the same by construction)."""
         r = self.reducer
-        if r is None or not getattr(r, "_agree", False) or self.uniform_shapes:
+        if r is None or getattr(r, "world", 1) <= 1 or self.uniform_shapes:
             return flag
         import torch.distributed as dist
 

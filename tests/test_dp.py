@@ -283,7 +283,7 @@ def _worker_subgroup(rank, world, port, q):
             ok_sub = ok_sub and model.fc1.weight.grad is not None
             red.remove()
         # GraphedTrainStep's path agreement (gloo MIN over the reducer's host group)
-        fake = types.SimpleNamespace(_agree=True, _host_group=None)
+        fake = types.SimpleNamespace(_agree=True, _host_group=None, world=world)
         g = ts.GraphedTrainStep(None, None, types.SimpleNamespace(capturable=True), reducer=fake)
         agree = (g._every_rank(rank != 1), g._every_rank(True), g._every_rank(False))
         # uniform_shapes: the caller's promise replaces the agreement (no collective)

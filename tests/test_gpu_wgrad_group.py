@@ -61,26 +61,35 @@ def check(outs, probs):
         assert bad == 0, f"problem {i} ({n}x{k}): {bad} elements off (max |d| {d.max().item():.3e}, bound {bound:.3e})"
 
 
+@pytest.fixture(params=[2, 0], ids=["ring32x4", "ring64x2"])
+def cfg(request, hv):
+    """Tile configurations (hvit_gemm_tune(7, v)): the default 32-deep four-stage ring and the
+    64-deep two-stage ring of gemm_ring.h."""
+    old = hv._lib.lib().hvit_gemm_tune(7, request.param)
+    yield request.param
+    hv._lib.lib().hvit_gemm_tune(7, old)
+
+
 @pytest.mark.parametrize("layers,M,D,hid", [
     (6, 8192, 512, 2048),   # B=32 default model: 288 tiles -> 1 round + 32 tiles in 8 pieces
     (2, 8192, 512, 2048),   # 96 tiles: remainder pieces only
     (12, 4096, 768, 3072),  # config 5 (B=16): 1296 tiles -> 5 rounds + 16 tiles in 16 pieces
     (1, 1024, 512, 2048),   # 48 tiles, short token range
 ])
-def test_wgrad_group_matches_fp32(hv, layers, M, D, hid):
+def test_wgrad_group_matches_fp32(hv, cfg, layers, M, D, hid):
     torch.backends.cuda.matmul.allow_tf32 = False
     probs = vit_problems(layers, M, D, hid)
     check(run_group(hv, probs, M), probs)
 
 
-def test_wgrad_group_single_problem_many_pieces_and_strided_dy(hv):
+def test_wgrad_group_single_problem_many_pieces_and_strided_dy(hv, cfg):
     probs = vit_problems(1, 8192, 512, 2048, seed=3, wide=True)[2:3]  # proj: 4 tiles, 64 pieces each
     check(run_group(hv, probs, 8192), probs)
     probs = vit_problems(1, 8192, 512, 2048, seed=4, wide=True)
     check(run_group(hv, probs, 8192), probs)
 
 
-def test_wgrad_group_deterministic(hv):
+def test_wgrad_group_deterministic(hv, cfg):
     probs = vit_problems(6, 8192, 512, 2048, seed=5)
     a = run_group(hv, probs, 8192)
     b = run_group(hv, probs, 8192)
