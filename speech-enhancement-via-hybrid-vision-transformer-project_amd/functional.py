@@ -586,6 +586,7 @@ WGRAD_GROUP = True
 _WG_QUEUE = {}    # device index -> [(dy, x, dw_view, n, k, M, pref)]
 _WG_TASKS = set()  # autograd graph tasks that have the flush queued
 _WG_TICKETS = {}  # device index -> zeroed uint32 counters (left zeroed by every launch)
+WG_FIXUPS = 0  # gradients autograd copied instead of adopting (re-copied by the flush; tests expect none)
 
 
 def wgrad_group_ok(dt, M, N, K, pref=None) -> bool:
@@ -605,9 +606,14 @@ def wgrad_enqueue(dy, x, M, N, K, dest=None, pref=None) -> torch.Tensor:
     is flushed."""
     dev = dy.device
     i = _dev_index(dev)
-    dw = dest.view(N, K) if dest is not None else torch.empty((N, K), dtype=torch.float32, device=dev)
+    # the queue holds the storage's base tensor, autograd gets a view of it: a
+    # view keeps its base alive (._base), so holding a view of the RETURNED
+    # tensor would count as a second reference to it and make AccumulateGrad
+    # copy it (unwritten) instead of adopting it
+    base = dest if dest is not None else torch.empty(N * K, dtype=torch.float32, device=dev)
+    dw = base.view(N, K)
     q = _WG_QUEUE.setdefault(i, [])
-    q.append((dy, x, dw.view(-1), N, K, M, pref))
+    q.append((dy, x, base, N, K, M, pref))
     task = torch._C._current_graph_task_id()
     if task >= 0 and task not in _WG_TASKS:
         _WG_TASKS.add(task)
@@ -655,6 +661,8 @@ def wgrad_flush(dev=None) -> None:
         p = pref() if pref is not None else None
         if p is not None and p.grad is not None and p.grad.data_ptr() != dw.data_ptr():
             # autograd copied the handed tensor before it was written
+            global WG_FIXUPS
+            WG_FIXUPS += 1
             p.grad.copy_(dw.view(n, k))
 
 

@@ -131,6 +131,7 @@ def test_model_grads_grouped_equal_per_linear(hv):
         finally:
             HF.WGRAD_GROUP = True
     assert not HF._WG_QUEUE, "the backward's final callback must flush the queue"
+    assert HF.WG_FIXUPS == 0, "autograd must adopt the queued gradients (no copy of an unwritten tensor)"
     for n, g0 in grads[False].items():
         g1 = grads[True][n]
         if n.startswith("transformer.blocks.") and n.endswith(("attn.qkv.weight", "attn.proj.weight",
