@@ -202,8 +202,18 @@ typedef struct {
   int ldx;
   float* dw;
   int n_out, k_in;
+  /* patch > 0: x is not a token-major matrix but the NHWC image [*, img_h,
+   * img_w, img_c] of a patch embedding (Conv2d k = stride = patch,
+   * components.py:275-280, hybrid_vit.py:127): token t = (image, py, px) of the
+   * (img_h/patch) x (img_w/patch) grid, row t of x = the patch's (ky, kx, c)
+   * values, k_in = patch^2 * img_c; dw is then [n_out][ky][kx][c] (the packed
+   * conv layout, hvit_conv_weight_unpack gives torch's).  Needs a grid width
+   * dividing 32, tokens per image a multiple of 32, patch * img_c a multiple
+   * of 256.  ldx is ignored. */
+  int patch, img_h, img_w, img_c;
 } hvit_wgrad_prob_t;
 int hvit_linear_wgrad_group_ok(int dt, int M, int n_out, int k_in); /* 1: the shape can join a group */
+int hvit_linear_wgrad_group_patch_ok(int dt, int M, int n_out, int patch, int img_h, int img_w, int img_c);
 long long hvit_linear_wgrad_group_ws(void);
 long long hvit_linear_wgrad_group_tickets(void);
 int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* probs, int nprobs, float* ws, long long ws_elems,

@@ -41,7 +41,8 @@ class SlabSum(C.Structure):
 
 class WgradProb(C.Structure):
     """hvit_wgrad_prob_t: one weight gradient of a grouped launch."""
-    _fields_ = [("dy", vp), ("ldy", i32), ("x", vp), ("ldx", i32), ("dw", vp), ("n_out", i32), ("k_in", i32)]
+    _fields_ = [("dy", vp), ("ldy", i32), ("x", vp), ("ldx", i32), ("dw", vp), ("n_out", i32), ("k_in", i32),
+                ("patch", i32), ("img_h", i32), ("img_w", i32), ("img_c", i32)]
 
 
 class Epilogue(C.Structure):
@@ -99,6 +100,7 @@ _SIGS = {
     "hvit_mhsa_bias_rows": ([i32, i32, i32, i32, i32], i64),
     "hvit_sum_slabs_strided": ([vp, i32, i64, i64, vp, vp], i32),
     "hvit_linear_wgrad_group_ok": ([i32, i32, i32, i32], i32),
+    "hvit_linear_wgrad_group_patch_ok": ([i32, i32, i32, i32, i32, i32, i32], i32),
     "hvit_linear_wgrad_group_ws": ([], i64),
     "hvit_linear_wgrad_group_tickets": ([], i64),
     "hvit_linear_wgrad_group": ([i32, i32, P(WgradProb), i32, vp, i64, vp, i64, vp], i32),

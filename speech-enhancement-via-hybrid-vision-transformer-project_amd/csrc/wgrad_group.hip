@@ -31,7 +31,7 @@
 namespace hvit_wg {
 using namespace hvit;
 
-constexpr int BM = 256, MAXP = 56;  // (every configuration's tiles are BM = 256 rows of dw)
+constexpr int BM = 256, MAXP = 64;  // (every configuration's tiles are BM = 256 rows of dw)
 
 // The weight gradients' K loop with 32-deep stages: both operands token-major
 // (MN images, transposed fragment reads), one 16x16x32 MFMA k-step per stage,
@@ -42,6 +42,18 @@ constexpr int BM = 256, MAXP = 56;  // (every configuration's tiles are BM = 256
 // s_waitcnt at 31 % MFMA busy).  The images are the first 32 k rows of
 // gemm.h's 64-deep MN images (DmaImg / MnSwz: rows are k, so the same source
 // swizzle and transposed reads apply).
+// B operand geometry: dense token-major rows (P = 0), or the implicit
+// im2col of a patch embedding (Conv2d k = stride = P, components.py:275-280):
+// token t = (image, py, px) of an Hp x Wp grid, its row (ky, kx, c) =
+// x[image, P*py + ky, P*px + kx, c] of an NHWC [*, H, Wimg, C] image.  A
+// 32-token stage is 32 / Wp whole patch rows of one image, so a lane's source
+// offset inside a stage is fixed and consecutive stages are a constant stride
+// apart; a 256-column tile lies inside one ky (P*C % 256 == 0).
+struct BGeo {
+  short P, Wimg, Wp, C;
+  int ext;  // bytes of x (buffer range)
+};
+
 template <int BM_, int BN_, int WM, int WN, int NB, bool PIPE>
 struct Ring32 {
   static constexpr int NW = WM * WN, NT = 64 * NW;
@@ -66,20 +78,37 @@ struct Ring32 {
   }
 
   __device__ __forceinline__ static void run(const LdDense<bf16_t, false>& la, const LdDense<bf16_t, false>& lb,
-                                             char* smem, int m0, int n0, int kbeg, int kend, f32x4 (&acc)[FM][FN]) {
+                                             const BGeo& bg, char* smem, int m0, int n0, int kbeg, int kend,
+                                             f32x4 (&acc)[FM][FN]) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
     const int nk = (kend - kbeg) / BK;
     if (nk <= 0) return;
-    const __amdgpu_buffer_rsrc_t ra = rsrc(la), rb = rsrc(lb);
+    const __amdgpu_buffer_rsrc_t ra = rsrc(la);
+    const __amdgpu_buffer_rsrc_t rb =
+        bg.P ? __builtin_amdgcn_make_buffer_rsrc((void*)lb.p, (short)0, (int)bg.ext, 0x00020000) : rsrc(lb);
     const unsigned oa = (unsigned)(((long)kbeg * la.ld + m0) * 2), da = (unsigned)((long)BK * la.ld * 2);
-    const unsigned ob = (unsigned)(((long)kbeg * lb.ld + n0) * 2), db = (unsigned)((long)BK * lb.ld * 2);
+    unsigned ob, db;
+    if (bg.P) {
+      const int pc = bg.P * bg.C;
+      ob = (unsigned)((((long)(kbeg / bg.Wp) * bg.P * bg.Wimg + (long)(n0 / pc) * bg.Wimg) * bg.C + n0 % pc) * 2);
+      db = (unsigned)((long)(BK / bg.Wp) * bg.P * bg.Wimg * bg.C * 2);
+    } else {
+      ob = (unsigned)(((long)kbeg * lb.ld + n0) * 2);
+      db = (unsigned)((long)BK * lb.ld * 2);
+    }
     unsigned va[PA], vb[PB];
 #pragma unroll
     for (int i = 0; i < PA; ++i) va[i] = IA::src_off(wid + NW * i, lane, la.ld);
 #pragma unroll
-    for (int i = 0; i < PB; ++i) vb[i] = IB::src_off(wid + NW * i, lane, lb.ld);
+    for (int i = 0; i < PB; ++i) {
+      // IB::src_off with the row (token) offset of the operand's geometry
+      const int row = (wid + NW * i) * IB::RPP + lane / IB::NCH;
+      const int c = (lane % IB::NCH) ^ IB::swz(row);
+      const long roff = bg.P ? ((long)(row / bg.Wp) * bg.P * bg.Wimg + (row % bg.Wp) * bg.P) * bg.C : (long)row * lb.ld;
+      vb[i] = (unsigned)((roff + c * 8) * 2);
+    }
     // stage t -> ring buffer t % NB; stages past the end re-read the last one
     // into a buffer never read again (a constant DMA count per iteration)
     auto issue = [&](int t) {
@@ -184,14 +213,14 @@ struct CoreOf<BN, WM, WN, NB, 2> {
   using T = Ring32<256, BN, WM, WN, NB, true>;
 };
 
-struct Prob {
+struct Prob {  // (kernel-argument table: kept small, MAXP of them)
   const bf16_t* dy;
   const bf16_t* x;
   float* dw;
-  int ldy, ldx;     // row pitches (elements) of dy [M][ldy] and x [M][ldx]
-  int n_out, k_in;  // dw [n_out][k_in]
-  int tn;           // k_in / BN
-  int tile0;        // first tile of this problem in the launch's tile order
+  int ldy, ldx;  // row pitches (elements) of dy [M][ldy] and x [M][ldx]
+  int k_in;      // dw [n_out][k_in]
+  int tile0;     // first tile of this problem in the launch's tile order
+  BGeo bg;       // x's geometry (bg.P = 0: dense rows of pitch ldx)
 };
 
 struct Table {
@@ -249,20 +278,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
     const int t = pb ? tb.rem0 + w / tb.s : (b / tb.G) * tb.G + w;
     const Prob& pr = find(tb, t);
     const int lt = t - pr.tile0;
-    const int m0 = (lt / pr.tn) * BM, n0 = (lt % pr.tn) * BN;
+    const int tn = pr.k_in / BN;
+    const int m0 = (lt / tn) * BM, n0 = (lt % tn) * BN;
     const int kbeg = pb ? (w % tb.s) * tb.pu * 64 : 0;
     const int kend = pb ? min(tb.M, kbeg + tb.pu * 64) : tb.M;
     float* dst = pb ? tb.slabs + (long)w * (BM * 256) : pr.dw + (long)m0 * pr.k_in + n0;
     const int ldo = pb ? BN : pr.k_in;
     LdDense<bf16_t, false> la, lb;
-    la.p = pr.dy; la.ld = pr.ldy; la.rows = pr.n_out; la.K = tb.M; la.vok = true;
-    lb.p = pr.x; lb.ld = pr.ldx; lb.rows = pr.k_in; lb.K = tb.M; lb.vok = true;
+    la.p = pr.dy; la.ld = pr.ldy; la.rows = 0; la.K = tb.M; la.vok = true;  // (rows: unused by MN images)
+    lb.p = pr.x; lb.ld = pr.ldx; lb.rows = 0; lb.K = tb.M; lb.vok = true;
     f32x4 acc[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if constexpr (DEEP) Core::run(la, lb, smem, m0, n0, kbeg, kend, acc);
+    if constexpr (DEEP) Core::run(la, lb, pr.bg, smem, m0, n0, kbeg, kend, acc);
     else Core::run(la, lb, smem, m0, n0, kbeg, kend, acc, none);
     // the result staged through LDS in 64-row passes; a thread stores 8
     // adjacent f32 columns per row (two 16-byte stores)
@@ -384,12 +414,44 @@ extern "C" int hvit_linear_wgrad_group_ok(int dt, int M, int n_out, int k_in) {
 extern "C" long long hvit_linear_wgrad_group_ws(void) { return (long long)num_cus() * BM * 256; }
 extern "C" long long hvit_linear_wgrad_group_tickets(void) { return (long long)num_cus(); }
 
+// the patch-embedding B geometry of problem q (P = 0: dense); "" when valid
+static const char* patch_geo(const hvit_wgrad_prob_t& q, int M, BGeo& g) {
+  g = BGeo{0, 0, 0, 0, 0};
+  if (q.patch <= 0) return "";
+  const int P = q.patch, H = q.img_h, W = q.img_w, C = q.img_c;
+  if (H <= 0 || W <= 0 || C <= 0 || H % P || W % P) return "image H / W must be positive multiples of the patch";
+  const int Hp = H / P, Wp = W / P;
+  if (q.k_in != P * P * C) return "k_in must be patch * patch * C";
+  if (32 % Wp) return "the patch grid width must divide 32";
+  if ((Hp * Wp) % 32 || M % (Hp * Wp)) return "tokens per image must be a multiple of 32 dividing M";
+  if ((P * C) % 256 || C % 8) return "patch * C must be a multiple of 256 (C of 8)";
+  const long long ext = (long long)(M / (Hp * Wp)) * H * W * C * 2;
+  if (ext >= (1LL << 31) || W > 32767 || C > 32767 || P > 32767) return "image too large for 32-bit offsets";
+  g = BGeo{(short)P, (short)W, (short)Wp, (short)C, (int)ext};
+  return "";
+}
+
+extern "C" int hvit_linear_wgrad_group_patch_ok(int dt, int M, int n_out, int patch, int img_h, int img_w,
+                                                int img_c) {
+  if (patch <= 0 || cfg_ref() < 2 || !hvit_linear_wgrad_group_ok(dt, M, n_out, patch * patch * img_c)) return 0;
+  hvit_wgrad_prob_t q{};
+  q.n_out = n_out;
+  q.k_in = patch * patch * img_c;
+  q.patch = patch;
+  q.img_h = img_h;
+  q.img_w = img_w;
+  q.img_c = img_c;
+  BGeo g;
+  return *patch_geo(q, M, g) ? 0 : 1;
+}
+
 extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* probs, int nprobs, float* ws,
                                        long long ws_elems, unsigned* tickets, long long n_tickets, void* stream) {
   HVIT_CHECK(probs && nprobs >= 0, "hvit_linear_wgrad_group: null problem table");
   HVIT_CHECK(ws && ws_elems >= hvit_linear_wgrad_group_ws(), "hvit_linear_wgrad_group: workspace too small");
   HVIT_CHECK(tickets && n_tickets >= hvit_linear_wgrad_group_tickets(), "hvit_linear_wgrad_group: tickets");
   HVIT_CHECK(aligned16(ws), "hvit_linear_wgrad_group: workspace alignment");
+  const int cfg = cfg_ref();
   for (int i = 0; i < nprobs; ++i) {
     const hvit_wgrad_prob_t& q = probs[i];
     HVIT_CHECK(hvit_linear_wgrad_group_ok(dt, M, q.n_out, q.k_in),
@@ -398,13 +460,16 @@ extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* p
                i, M, q.n_out, q.k_in, BM);
     HVIT_CHECK(q.dy && q.x && q.dw && aligned16(q.dy) && aligned16(q.x) && aligned16(q.dw),
                "hvit_linear_wgrad_group: problem %d pointers (null or not 16-byte aligned)", i);
-    HVIT_CHECK(q.ldy >= q.n_out && q.ldx >= q.k_in && q.ldy % 8 == 0 && q.ldx % 8 == 0,
+    HVIT_CHECK(q.ldy >= q.n_out && q.ldy % 8 == 0 && (q.patch > 0 || (q.ldx >= q.k_in && q.ldx % 8 == 0)),
                "hvit_linear_wgrad_group: problem %d row pitches", i);
-    HVIT_CHECK((long long)M * q.ldy * 2 < (1LL << 31) && (long long)M * q.ldx * 2 < (1LL << 31),
+    HVIT_CHECK((long long)M * q.ldy * 2 < (1LL << 31) && (q.patch > 0 || (long long)M * q.ldx * 2 < (1LL << 31)),
                "hvit_linear_wgrad_group: problem %d operand too large for 32-bit offsets", i);
+    BGeo g;
+    const char* why = patch_geo(q, M, g);
+    HVIT_CHECK(!*why, "hvit_linear_wgrad_group: problem %d patch geometry: %s", i, why);
+    HVIT_CHECK(q.patch <= 0 || cfg >= 2, "hvit_linear_wgrad_group: patch problems need a 32-deep ring configuration");
   }
   hipStream_t st = (hipStream_t)stream;
-  const int cfg = cfg_ref();
   const int BN = cfg == 1 ? 128 : 256;
   for (int c0 = 0; c0 < nprobs; c0 += MAXP) {
     const int np = std::min(MAXP, nprobs - c0);
@@ -417,12 +482,11 @@ extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* p
       p.x = (const bf16_t*)q.x;
       p.dw = q.dw;
       p.ldy = q.ldy;
-      p.ldx = q.ldx;
-      p.n_out = q.n_out;
+      p.ldx = q.patch > 0 ? 0 : q.ldx;
       p.k_in = q.k_in;
-      p.tn = q.k_in / BN;
       p.tile0 = T;
-      T += (q.n_out / BM) * p.tn;
+      patch_geo(q, M, p.bg);
+      T += (q.n_out / BM) * (q.k_in / BN);
     }
     tb.np = np;
     tb.M = M;

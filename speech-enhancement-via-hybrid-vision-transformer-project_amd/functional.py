@@ -583,7 +583,7 @@ def side_ok(prefs) -> bool:
 # autograd adopts the handed view as .grad without a copy (a copy made before
 # the flush would copy unwritten memory: the flush re-copies such a .grad).
 WGRAD_GROUP = True
-_WG_QUEUE = {}    # device index -> [(dy, x, dw_view, n, k, M, pref)]
+_WG_QUEUE = {}    # device index -> [(dy, x, dw base, n, k, M, pref, patch, packed)]
 _WG_TASKS = set()  # autograd graph tasks that have the flush queued
 _WG_TICKETS = {}  # device index -> zeroed uint32 counters (left zeroed by every launch)
 WG_FIXUPS = 0  # gradients autograd copied instead of adopting (re-copied by the flush; tests expect none)
@@ -600,20 +600,28 @@ def wgrad_group_ok(dt, M, N, K, pref=None) -> bool:
     return bool(L.lib().hvit_linear_wgrad_group_ok(dt, M, N, K))
 
 
-def wgrad_enqueue(dy, x, M, N, K, dest=None, pref=None) -> torch.Tensor:
+def wgrad_enqueue(dy, x, M, N, K, dest=None, pref=None, patch=None) -> torch.Tensor:
     """Queue dW[N, K] = dy[M, :N]^T x[M, :K] (bf16 operands, row pitches taken
     from the tensors); returns the f32 gradient tensor, final once the queue
-    is flushed."""
+    is flushed.  ``patch`` = (P, weight shape): x is the NHWC feature map of a
+    patch embedding (Conv2d k = stride = P) and the result, computed in the
+    packed [N][ky][kx][c] order, is unpacked into the torch-layout weight
+    gradient by the flush."""
     dev = dy.device
     i = _dev_index(dev)
     # the queue holds the storage's base tensor, autograd gets a view of it: a
     # view keeps its base alive (._base), so holding a view of the RETURNED
     # tensor would count as a second reference to it and make AccumulateGrad
     # copy it (unwritten) instead of adopting it
-    base = dest if dest is not None else torch.empty(N * K, dtype=torch.float32, device=dev)
-    dw = base.view(N, K)
+    base = dest.view(-1) if dest is not None else torch.empty(N * K, dtype=torch.float32, device=dev)
+    if patch is not None:
+        dw = base.view(patch[1])
+        packed = torch.empty(N * K, dtype=torch.float32, device=dev)
+    else:
+        dw = base.view(N, K)
+        packed = None
     q = _WG_QUEUE.setdefault(i, [])
-    q.append((dy, x, base, N, K, M, pref))
+    q.append((dy, x, base, N, K, M, pref, patch, packed))
     task = torch._C._current_graph_task_id()
     if task >= 0 and task not in _WG_TASKS:
         _WG_TASKS.add(task)
@@ -646,8 +654,13 @@ def wgrad_flush(dev=None) -> None:
     for M, jobs in by_m.items():
         arr = (L.WgradProb * len(jobs))()
         flops = 0.0
-        for j, (dy, x, dw, n, k, _, _) in enumerate(jobs):
-            arr[j] = L.WgradProb(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), n, k)
+        for j, (dy, x, dw, n, k, _, _, patch, packed) in enumerate(jobs):
+            if patch is None:
+                arr[j] = L.WgradProb(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), n, k)
+            else:
+                _, H, W, C = x.shape
+                arr[j] = L.WgradProb(dy.data_ptr(), dy.stride(0), x.data_ptr(), 0, packed.data_ptr(), n, k,
+                                     patch[0], H, W, C)
             flops += 2.0 * M * n * k
 
         def launch(arr=arr, n=len(jobs), M=M, jobs=jobs):
@@ -657,13 +670,16 @@ def wgrad_flush(dev=None) -> None:
         with timed("vit_linear_wgrad", flops):
             launch()
         _record("vit_linear_wgrad", (lambda launch=launch, ws=ws: launch(), flops))
-    for dy, x, dw, n, k, _, pref in q:
+    for dy, x, dw, n, k, _, pref, patch, packed in q:
+        if patch is not None:  # [co][ky][kx][c] -> torch's [co][c][ky][kx]
+            co, ci, ks, _ = patch[1]
+            call("hvit_conv_weight_unpack", packed.data_ptr(), co, ci, ks, dw.data_ptr(), stream_ptr())
         p = pref() if pref is not None else None
         if p is not None and p.grad is not None and p.grad.data_ptr() != dw.data_ptr():
             # autograd copied the handed tensor before it was written
             global WG_FIXUPS
             WG_FIXUPS += 1
-            p.grad.copy_(dw.view(n, k))
+            p.grad.copy_(dw.view(p.grad.shape))
 
 
 class Deferred:
@@ -1069,7 +1085,13 @@ class PatchEmbedFn(torch.autograd.Function):
             dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
             call("hvit_reduce_rows", gd.data_ptr(), dt, N, Nt * D, Nt * D, 1, dpos.data_ptr(), s)
         g = geom(feat, C, None, 0, N, H, W, 1, Pp, Pp, 0, D)
-        dw = _conv_wgrad_maybe_side(ctx, dt, g, gd, w, (feat,))
+        if (not SIDE and dt == BF16 and wgrad_group_ok(dt, M, D, Pp * Pp * C, ctx.prefs[0])
+                and L.lib().hvit_linear_wgrad_group_patch_ok(dt, M, D, Pp, H, W, C)):
+            # queued with the ViT blocks' weight gradients (one grouped launch)
+            dw = wgrad_enqueue(gd, feat, M, D, Pp * Pp * C, grad_dest(*ctx.wid), ctx.prefs[0],
+                               patch=(Pp, tuple(w.shape)))
+        else:
+            dw = _conv_wgrad_maybe_side(ctx, dt, g, gd, w, (feat,))
         dfeat = None
         if ctx.needs_input_grad[0]:
             dfeat = _empty(feat.shape, dt, dev)

@@ -89,6 +89,42 @@ def test_wgrad_group_single_problem_many_pieces_and_strided_dy(hv, cfg):
     check(run_group(hv, probs, 8192), probs)
 
 
+@pytest.mark.parametrize("B,H,C,P", [(32, 64, 256, 4), (4, 64, 256, 4), (2, 32, 64, 4), (4, 32, 128, 2)])
+def test_wgrad_group_patch_embedding(hv, B, H, C, P):
+    """A patch-embedding weight gradient (Conv2d k = stride = P on an NHWC map) in
+    the same launch as ViT problems: packed [co][ky][kx][c] result vs torch fp32
+    on the explicitly gathered patches (components.py:275-280)."""
+    L = hv._lib
+    g = torch.Generator(device=DEV).manual_seed(11)
+    D = 512
+    Hp = H // P
+    M = B * Hp * Hp
+    feat = (torch.randn(B, H, H, C, device=DEV, generator=g) * 0.5).to(BF)
+    gd = (torch.randn(M, D, device=DEV, generator=g) * 0.5).to(BF)
+    assert L.lib().hvit_linear_wgrad_group_patch_ok(L.BF16, M, D, P, H, H, C) == 1
+    patches = feat.view(B, Hp, P, Hp, P, C).permute(0, 1, 3, 2, 4, 5).reshape(M, P * P * C)
+    ref = (gd.float().t() @ patches.float()).double()
+    vit = vit_problems(1, M, 512, 2048, seed=12)
+    arr = (L.WgradProb * (len(vit) + 1))()
+    outs = []
+    for i, (dy, x, n, k) in enumerate(vit):
+        dw = torch.full((n, k), float("nan"), device=DEV)
+        outs.append(dw)
+        arr[i] = L.WgradProb(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dw.data_ptr(), n, k)
+    dwp = torch.full((D, P * P * C), float("nan"), device=DEV)
+    arr[len(vit)] = L.WgradProb(gd.data_ptr(), D, feat.data_ptr(), 0, dwp.data_ptr(), D, P * P * C, P, H, H, C)
+    ws = torch.empty(int(L.lib().hvit_linear_wgrad_group_ws()), device=DEV)
+    tk = torch.zeros(int(L.lib().hvit_linear_wgrad_group_tickets()), dtype=torch.int32, device=DEV)
+    L.call("hvit_linear_wgrad_group", L.BF16, M, arr, len(vit) + 1, ws.data_ptr(), ws.numel(), tk.data_ptr(),
+           tk.numel(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    check(outs, vit)
+    d = (dwp.double() - ref).abs()
+    bound = ACC * ref.abs().max().item()
+    bad = int((d > bound).sum()) + int(torch.isnan(dwp).sum())
+    assert bad == 0, f"patch dW: {bad} elements off (max |d| {d.max().item():.3e}, bound {bound:.3e})"
+
+
 def test_wgrad_group_deterministic(hv, cfg):
     probs = vit_problems(6, 8192, 512, 2048, seed=5)
     a = run_group(hv, probs, 8192)
@@ -134,8 +170,9 @@ def test_model_grads_grouped_equal_per_linear(hv):
     assert HF.WG_FIXUPS == 0, "autograd must adopt the queued gradients (no copy of an unwritten tensor)"
     for n, g0 in grads[False].items():
         g1 = grads[True][n]
-        if n.startswith("transformer.blocks.") and n.endswith(("attn.qkv.weight", "attn.proj.weight",
-                                                              "mlp.net.0.weight", "mlp.net.3.weight")):
+        if n == "patch_embed.projection.weight" or (
+                n.startswith("transformer.blocks.") and n.endswith(("attn.qkv.weight", "attn.proj.weight",
+                                                                    "mlp.net.0.weight", "mlp.net.3.weight"))):
             bound = 1e-4 * g0.abs().max().item() + 1e-12
             assert (g1 - g0).abs().max().item() <= bound, n
         else:
