@@ -54,7 +54,7 @@ struct BGeo {
   int ext;  // bytes of x (buffer range)
 };
 
-template <int BM_, int BN_, int WM, int WN, int NB, bool PIPE>
+template <int BM_, int BN_, int WM, int WN, int NB>
 struct Ring32 {
   static constexpr int NW = WM * WN, NT = 64 * NW;
   using IA = DmaImg<BM_, false>;
@@ -138,59 +138,20 @@ struct Ring32 {
       const char* at = smem + (t % NB) * STAGE;
       const char* bt = at + ABYTES;
       u32x4 fa[FM], fb[FN];
-      if constexpr (!PIPE) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) fa[i] = IA::frag(at, wm * WTM + i * 16, 0, lane);
+      for (int i = 0; i < FM; ++i) fa[i] = IA::frag(at, wm * WTM + i * 16, 0, lane);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, 0, lane);
-        issue(t + NB - 1);
-        lgkm_wait0();
-        lds_pin(fa);
-        lds_pin(fb);
+      for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, 0, lane);
+      issue(t + NB - 1);
+      lgkm_wait0();
+      lds_pin(fa);
+      lds_pin(fb);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
-                                                                __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
-      } else {
-        // B fragments and the first half of the A fragments, then the second
-        // half's reads in flight under the first half's MFMAs (with the stage's
-        // DMA issue spread over them)
-        constexpr int H = FM / 2;
-        u32x4 fa0[H], fa1[H];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) fb[j] = IB::frag(bt, wn * WTN + j * 16, 0, lane);
-#pragma unroll
-        for (int i = 0; i < H; ++i) fa0[i] = IA::frag(at, wm * WTM + i * 16, 0, lane);
-        lgkm_wait0();
-        lds_pin(fb);
-        lds_pin(fa0);
-#pragma unroll
-        for (int i = 0; i < H; ++i) fa1[i] = IA::frag(at, wm * WTM + (H + i) * 16, 0, lane);
-        issue(t + NB - 1);
-#pragma unroll
-        for (int i = 0; i < H; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa0[i]),
-                                                                __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, H * 2, 0);  // the second half's fragment reads first
-#pragma unroll
-        for (int k = 0; k < INFL; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, (H * FN) / INFL, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                // one DMA piece
-        }
-        lgkm_wait0();
-        lds_pin(fa1);
-#pragma unroll
-        for (int i = 0; i < H; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[H + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa1[i]),
-                                                                    __builtin_bit_cast(s16x8, fb[j]), acc[H + i][j], 0, 0,
-                                                                    0);
-      }
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
+                                                              __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_waitcnt(vm_imm(0));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -206,11 +167,7 @@ struct CoreOf {
 };
 template <int BN, int WM, int WN, int NB>
 struct CoreOf<BN, WM, WN, NB, 1> {
-  using T = Ring32<256, BN, WM, WN, NB, false>;
-};
-template <int BN, int WM, int WN, int NB>
-struct CoreOf<BN, WM, WN, NB, 2> {
-  using T = Ring32<256, BN, WM, WN, NB, true>;
+  using T = Ring32<256, BN, WM, WN, NB>;
 };
 
 struct Prob {  // (kernel-argument table: kept small, MAXP of them)
@@ -240,15 +197,15 @@ __device__ __forceinline__ const Prob& find(const Table& tb, int t) {
   return tb.p[i];
 }
 
-// tile configurations: BN columns of dw per tile, WM x WN waves, NB ring stages
-//   0: 256 x 256, 2 x 4 waves, 2 stages (128 KiB: one stage in flight)
-//   1: 256 x 128, 4 x 2 waves, 3 stages (144 KiB: two stages in flight)
-//   2: 256 x 256, 2 x 4 waves, 32-deep stages, 4 in the ring (128 KiB: three 32 KiB stages in flight)
-//   3: the same with 5 stages (160 KiB: four in flight)
-//   4: cfg 2 with half of each stage's fragment reads under the other half's MFMAs
-//   5: cfg 4 with 3 stages
+// tile configurations (hvit_gemm_tune(7, v); all 256 x 256 tiles):
+//   0: gemm_ring.h's 64-deep ring, 2 x 4 waves, 2 stages (128 KiB: one stage in flight)
+//   2: the 32-deep ring, 2 x 4 waves, 4 stages (128 KiB: three 32 KiB stages in flight)
+//   6: the 32-deep ring, 4 x 4 waves (64 x 64 each, 114 VGPRs: four waves per SIMD), 4 stages -- default
+// Measured and dropped (tools/wgrad_group_probe.py, 6 blocks at B = 32): 256 x 128 tiles on a 3-stage
+// ring 368 vs 356 us (cfg 0); 5 stages 352 vs 333 (cfg 2); half of each stage's fragment reads under
+// the other half's MFMAs 336 vs 333; 16 waves with 5 stages 365 vs 350 (cfg 6).
 template <int BN, int WM, int WN, int NB, int DEEP>
-__global__ __launch_bounds__(512, 1) void wgrad_group_kernel(Table tb) {
+__global__ __launch_bounds__(64 * WM * WN, 1) void wgrad_group_kernel(Table tb) {
   using Core = typename CoreOf<BN, WM, WN, NB, DEEP>::T;
   constexpr int NT = Core::NT, FM = Core::FM, FN = Core::FN, WTM = Core::WTM, WTN = Core::WTN;
   constexpr int CP = BN + 4;  // LDS tile pitch (floats)
@@ -392,7 +349,9 @@ static void plan(Table& tb, int T, int M) {
 
 // tile configuration (hvit_gemm_tune(7, v), A/B measurements)
 static int& cfg_ref() {
-  static int c = 2;  // (isolated loop, tools/wgrad_group_probe.py: 6 blocks at B = 32 356 -> 333-341 us, config 5 770 -> 720)
+  // (isolated loop, tools/wgrad_group_probe.py, 6 blocks at B = 32: cfg 0 356, cfg 2 333-341 / 361 on a slower box,
+  // cfg 6 350 on that box (315 with L2-resident operands); in-step 364 -> 338 us, step 4.630 -> 4.622 ms)
+  static int c = 6;
   return c;
 }
 
@@ -402,7 +361,7 @@ using namespace hvit_wg;
 
 int hvit_wgrad_group_tune(int value) {
   const int old = cfg_ref();
-  if (value >= 0 && value <= 5) cfg_ref() = value;
+  if (value == 0 || value == 2 || value == 6) cfg_ref() = value;
   return old;
 }
 
@@ -470,7 +429,7 @@ extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* p
     HVIT_CHECK(q.patch <= 0 || cfg >= 2, "hvit_linear_wgrad_group: patch problems need a 32-deep ring configuration");
   }
   hipStream_t st = (hipStream_t)stream;
-  const int BN = cfg == 1 ? 128 : 256;
+  constexpr int BN = 256;
   for (int c0 = 0; c0 < nprobs; c0 += MAXP) {
     const int np = std::min(MAXP, nprobs - c0);
     Table tb{};
@@ -495,16 +454,10 @@ extern "C" int hvit_linear_wgrad_group(int dt, int M, const hvit_wgrad_prob_t* p
     plan(tb, T, M);
     if (T == 0) continue;
     const dim3 grid(tb.R * tb.G + 8 * tb.GB8);
-    if (cfg == 1)
-      hipLaunchKernelGGL((wgrad_group_kernel<128, 4, 2, 3, 0>), grid, dim3(512), 0, st, tb);
-    else if (cfg == 2)
+    if (cfg == 2)
       hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 4, 1>), grid, dim3(512), 0, st, tb);
-    else if (cfg == 3)
-      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 5, 1>), grid, dim3(512), 0, st, tb);
-    else if (cfg == 4)
-      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 4, 2>), grid, dim3(512), 0, st, tb);
-    else if (cfg == 5)
-      hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 3, 2>), grid, dim3(512), 0, st, tb);
+    else if (cfg == 6)
+      hipLaunchKernelGGL((wgrad_group_kernel<256, 4, 4, 4, 1>), grid, dim3(1024), 0, st, tb);
     else
       hipLaunchKernelGGL((wgrad_group_kernel<256, 2, 4, 2, 0>), grid, dim3(512), 0, st, tb);
     HVIT_LAUNCH_CHECK();

@@ -630,15 +630,47 @@ def wgrad_enqueue(dy, x, M, N, K, dest=None, pref=None, patch=None) -> torch.Ten
 
 
 def _wgrad_flush_all():
-    for i in list(_WG_QUEUE):
+    for i in set(_WG_QUEUE) | set(_SIDE_PENDING):
         wgrad_flush(torch.device("cuda", i))
     _WG_TASKS.clear()
+
+
+# Partial-row sums (Deferred side jobs) whose results were handed to autograd
+# before any launch summed them: the next launch that can carry one takes it
+# (side_take), the flush points run whatever is left as launches of their own.
+_SIDE_PENDING = {}  # device index -> [Deferred]
+
+
+def side_defer(job, dev):
+    i = _dev_index(dev)
+    _SIDE_PENDING.setdefault(i, []).append(job)
+    task = torch._C._current_graph_task_id()
+    if task >= 0 and task not in _WG_TASKS:
+        _WG_TASKS.add(task)
+        torch.autograd.Variable._execution_engine.queue_callback(_wgrad_flush_all)
+    return job
+
+
+def side_take(job, dev) -> bool:
+    """Claim a pending job for a launch about to carry it (False: already run)."""
+    q = _SIDE_PENDING.get(_dev_index(dev), [])
+    for k, j in enumerate(q):
+        if j is job:
+            del q[k]
+            return True
+    return False
+
+
+def _side_run_pending(i):
+    for j in _SIDE_PENDING.pop(i, []):
+        call("hvit_sum_slabs_strided", j.job.src, j.job.splits, j.job.stride, j.job.n, j.job.dst, stream_ptr())
 
 
 def wgrad_flush(dev=None) -> None:
     """Launch every queued weight gradient of ``dev`` (one grouped launch per
     token count) on the current stream."""
     i = _dev_index(dev) if dev is not None else torch.cuda.current_device()
+    _side_run_pending(i)
     q = _WG_QUEUE.pop(i, None)
     if not q:
         return
@@ -1195,16 +1227,27 @@ class GradHandoff:
     backward fills g and colsum; block l's backward (which runs after it) uses
     them instead of a dropout_scale pass.  Unfilled: block l falls back."""
 
-    __slots__ = ("drop", "rowscale", "rps", "dt", "g", "colsum")
+    __slots__ = ("drop", "rowscale", "rps", "dt", "g", "colsum", "job")
 
     def __init__(self):
-        self.drop = self.rowscale = self.rps = self.dt = self.g = self.colsum = None
+        self.drop = self.rowscale = self.rps = self.dt = self.g = self.colsum = self.job = None
 
-    def fuse(self, dy, x, mean, rstd, gw, resid, zs):
+    def fuse(self, dy, x, mean, rstd, gw, resid, zs, lnrefs=()):
         """The consumer's LN backward with this handoff's dropout fused; returns
-        (dx, dgamma, dbeta) like _ln_bwd."""
-        dx, dgw, dgb, g, cs = _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs, self.drop, self.rowscale, self.rps,
-                                           self.dt)
+        (dx, dgamma, dbeta) like _ln_bwd.  Under the grouped weight gradients its
+        [dgamma | dbeta | colsum] partial-row sum is deferred (``job``) to block
+        l's first data-gradient launch, which carries it as a side job (a pending
+        side job: every flush point runs it if no launch has).  ``lnrefs``: the
+        LayerNorm's parameters -- not deferred when one of them already holds a
+        .grad (autograd would add the unwritten sums at once)."""
+        if WGRAD_GROUP and not SIDE and dy.is_cuda and lnrefs and all(
+                (r() is None or r().grad is None) for r in lnrefs):
+            dx, dgw, dgb, g, cs, job = _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs, self.drop, self.rowscale,
+                                                    self.rps, self.dt, defer=True)
+            self.job = side_defer(job, dy.device)
+        else:
+            dx, dgw, dgb, g, cs = _ln_bwd_drop(dy, x, mean, rstd, gw, resid, zs, self.drop, self.rowscale, self.rps,
+                                               self.dt)
         self.g, self.colsum = g, cs
         return dx, dgw, dgb
 
@@ -1329,6 +1372,7 @@ class ViTBlockFn(torch.autograd.Function):
         # the parameters whose gradients the side stream may produce (side_ok)
         ctx.prefs = tuple(weakref.ref(p) for p in (qkvw, qkvb, pw, f1w, f1b, f2w))
         ctx.wrefs = tuple(weakref.ref(p) for p in (qkvw, pw, f1w, f2w))  # (the grouped weight gradients)
+        ctx.lnrefs = (weakref.ref(n1w), weakref.ref(n1b))
         ctx.kbits = kbits
         # the fc2 branch's dropout / DropPath of the incoming gradient, for the
         # next consumer of x2 to fuse into its LayerNorm backward (GradHandoff)
@@ -1359,9 +1403,12 @@ class ViTBlockFn(torch.autograd.Function):
         # MLP branch
         zln1, zln2, _, zf2b, zpb, zqb = ctx.zs
         ho_in, ho_out = ctx.ho
+        jho = None  # the consumer's deferred LN partial-row sum (GradHandoff.fuse), for a launch to carry
         if ho_out is not None and ho_out.g is not None:  # fused into the next consumer's LN backward
             g2, df2b = ho_out.g, ho_out.colsum
-            ho_out.g = ho_out.colsum = None
+            if ho_out.job is not None and side_take(ho_out.job, dev):
+                jho = ho_out.job
+            ho_out.g = ho_out.colsum = ho_out.job = None
         else:
             g2 = _empty((M, D), dt, dev)
             df2b = zf2b.take(dev)
@@ -1398,7 +1445,11 @@ class ViTBlockFn(torch.autograd.Function):
         nrow = (M + 63) // 64
         cparts = torch.empty((nrow, hid), dtype=torch.float32, device=dev)
         df1b = torch.empty(hid, dtype=torch.float32, device=dev)
-        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=None if FC1_FOLD else drf1, colsum=cparts, side=j2)
+        if jho is not None and j2 is not None:  # (one side job per launch)
+            call("hvit_sum_slabs_strided", jho.job.src, jho.job.splits, jho.job.stride, jho.job.n, jho.job.dst, s)
+            jho = None
+        e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=None if FC1_FOLD else drf1, colsum=cparts,
+                         side=j2 if j2 is not None else jho)
         _launch("vit_linear_dgrad", 2.0 * M * D * hid,
                 lambda e: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt, e,
                                s), e_fc2, (gh, cparts))
@@ -1482,7 +1533,7 @@ class ViTBlockFn(torch.autograd.Function):
                 lambda e: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
                                L.dt_of(dxn1), e, s), e_qkv)
         if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
-            dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1)
+            dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1, ctx.lnrefs)
         else:
             dx, dn1w, dn1b = _ln_bwd(dxn1, x2d, m1, r1, n1w, dx1, zln1)
         return (dx.view(B, Nt, D), dn1w, dn1b, dqkvw, dqkvb, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b,
@@ -1508,6 +1559,7 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(nw)
         ctx.t = (x2d, xn, m, r, W)
         ctx.prefs = (weakref.ref(w), weakref.ref(b))
+        ctx.lnrefs = (weakref.ref(nw), weakref.ref(nb))
         ctx.meta = (B, Nt, D, C, dt)
         ctx.ho = ho if LNDROP else None
         ctx.zs = _zs(ctx, 3 * D)
@@ -1525,7 +1577,7 @@ class HeadFn(torch.autograd.Function):
         call("hvit_linear_dgrad", dt, dy.data_ptr(), W.data_ptr(), M, C, D, dxn.data_ptr(), L.dt_of(dxn),
              epilogue(side=jw) if jw is not None else None, stream_ptr())  # (carries the wgrad's slab sum)
         if ctx.ho is not None and ctx.ho.drop is not None:  # the last block's fc2 dropout, fused
-            dx, dnw, dnb = ctx.ho.fuse(dxn, x2d, m, r, nw, None, ctx.zs)
+            dx, dnw, dnb = ctx.ho.fuse(dxn, x2d, m, r, nw, None, ctx.zs, ctx.lnrefs)
         else:
             dx, dnw, dnb = _ln_bwd(dxn, x2d, m, r, nw, None, ctx.zs)
         return dx.view(B, Nt, D), dnw, dnb, dw, db, None, None, None

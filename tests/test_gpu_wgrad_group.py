@@ -61,9 +61,9 @@ def check(outs, probs):
         assert bad == 0, f"problem {i} ({n}x{k}): {bad} elements off (max |d| {d.max().item():.3e}, bound {bound:.3e})"
 
 
-@pytest.fixture(params=[2, 0], ids=["ring32x4", "ring64x2"])
+@pytest.fixture(params=[6, 2, 0], ids=["ring32x4w16", "ring32x4", "ring64x2"])
 def cfg(request, hv):
-    """Tile configurations (hvit_gemm_tune(7, v)): the default 32-deep four-stage ring and the
+    """Tile configurations (hvit_gemm_tune(7, v)): the default 32-deep four-stage ring on 16 waves, on 8, and the
     64-deep two-stage ring of gemm_ring.h."""
     old = hv._lib.lib().hvit_gemm_tune(7, request.param)
     yield request.param
@@ -147,9 +147,8 @@ def test_wgrad_group_rejects_bad_shapes(hv):
 def test_model_grads_grouped_equal_per_linear(hv):
     """The bf16 train step's ViT weight gradients with the grouped launch equal
     the per-Linear split-K path's within the accumulation-order bar; every other
-    gradient is bit-identical (the data-gradient chain is the same, and the
-    bias / LayerNorm partial-row sums keep their job's order whichever launch
-    carries them)."""
+    gradient within f32 summation-order noise (the data-gradient chain is the
+    same launches)."""
     HF = sys.modules["hvit_amd.functional"]
     torch.manual_seed(0)
     m = hv.HybridViT(dropout=0.0, attn_dropout=0.0, drop_path_rate=0.0, precision="bf16").cuda().train()
@@ -168,6 +167,7 @@ def test_model_grads_grouped_equal_per_linear(hv):
             HF.WGRAD_GROUP = True
     assert not HF._WG_QUEUE, "the backward's final callback must flush the queue"
     assert HF.WG_FIXUPS == 0, "autograd must adopt the queued gradients (no copy of an unwritten tensor)"
+    assert not any(HF._SIDE_PENDING.values()), "pending side jobs must be carried or flushed"
     for n, g0 in grads[False].items():
         g1 = grads[True][n]
         if n == "patch_embed.projection.weight" or (
@@ -176,4 +176,7 @@ def test_model_grads_grouped_equal_per_linear(hv):
             bound = 1e-4 * g0.abs().max().item() + 1e-12
             assert (g1 - g0).abs().max().item() <= bound, n
         else:
-            assert torch.equal(g1, g0), n
+            # the data-gradient chain is the same; the LayerNorm / bias partial-row sums the grouped mode
+            # defers to a later launch add the same rows in another fixed order (a wave per granule)
+            bound = 1e-5 * g0.abs().max().item() + 1e-12
+            assert (g1 - g0).abs().max().item() <= bound, n
