@@ -977,7 +977,7 @@ struct GemmCoreDma {
   static constexpr int FM = WTM / 16, FN = WTN / 16;
   static constexpr int PA = IA::PIECES / 4, PB = IB::PIECES / 4;  // pieces per wave per stage
   static constexpr int SM_LOOP = NB * (IA::BYTES + IB::BYTES);
-  static_assert(NB == 1 || NB == 2, "one or two LDS stage buffers");
+  static_assert(NB >= 1 && NB <= 3, "one to three LDS stage buffers");
   static_assert(IA::PIECES % 4 == 0 && IB::PIECES % 4 == 0, "pieces per stage must split over 4 waves");
 
   template <class L>
@@ -1052,7 +1052,7 @@ struct GemmCoreDma {
       for (int i = 0; i < PA; ++i) va[i] = IA::src_off(wid + 4 * i, lane, la.ld);
     }
     auto issue = [&](int t) {
-      char* abuf = smem + (NB == 2 ? (t & 1) : 0) * (IA::BYTES + IB::BYTES);
+      char* abuf = smem + (NB >= 2 ? t % NB : 0) * (IA::BYTES + IB::BYTES);
       char* bbuf = abuf + IA::BYTES;
       const unsigned sb = ob + (unsigned)(t < nk ? t : nk - 1) * db;
       if constexpr (CONV) {
@@ -1106,7 +1106,7 @@ struct GemmCoreDma {
     // k-step 0's fragments, then k-step 1's reads in flight under k-step 0's
     // MFMAs (explicit lgkmcnt waits: the MN reads are asm, DmaImg::frag)
     auto compute = [&](int t) {
-      const char* at = smem + (NB == 2 ? (t & 1) : 0) * (IA::BYTES + IB::BYTES);
+      const char* at = smem + (NB >= 2 ? t % NB : 0) * (IA::BYTES + IB::BYTES);
       const char* bt = at + IA::BYTES;
       static_assert(BK == 64, "two k-steps per stage");
       u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
@@ -1149,14 +1149,21 @@ struct GemmCoreDma {
     // body is uniform; it is drained before the epilogue reuses LDS.
     // Measured (tools/ring_bench.py probes, 8192x2048, K = 2048): 853 -> 1042
     // TFLOP/s against the two-barrier loop with the DMA issued in a block.
+    // Three buffers (NB = 3, round 6: the long-K 128x64 / 64x64 kernels): stage
+    // t+2 is issued during stage t, so one stage stays in flight through the
+    // wait (a counted vmcnt of one stage's DMA instructions).
     constexpr int MPD = (FM * FN) / INFLIGHT > 0 ? (FM * FN) / INFLIGHT : 1;
     issue(0);
+    if constexpr (NB == 3) issue(1);
     for (int t = 0; t < nk; ++t) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): stage t landed (for this wave)
+      if constexpr (NB == 3)
+        __builtin_amdgcn_s_waitcnt(0x0F70 | (INFLIGHT & 15) | (((INFLIGHT >> 4) & 3) << 14));  // vmcnt(INFLIGHT)
+      else
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): stage t landed (for this wave)
       asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // ... for every wave; buffer (t+1) & 1 is free
+      __builtin_amdgcn_s_barrier();  // ... for every wave; buffer (t + NB - 1) % NB is free
       asm volatile("" ::: "memory");
-      const char* at = smem + (t & 1) * (IA::BYTES + IB::BYTES);
+      const char* at = smem + (t % NB) * (IA::BYTES + IB::BYTES);
       const char* bt = at + IA::BYTES;
       u32x4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
       load(at, bt, 0, fa0, fb0);
@@ -1164,7 +1171,7 @@ struct GemmCoreDma {
       lds_pin(fa0);
       lds_pin(fb0);
       load(at, bt, 1, fa1, fb1);
-      issue(t + 1);
+      issue(t + NB - 1);
       mma(fa0, fb0);
       __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);  // k-step 1 fragment reads first
 #pragma unroll
@@ -1237,7 +1244,8 @@ __device__ __forceinline__ TileId tile_of(int remap) {
 }
 
 // DMAK: 0 = register-staged K loop, 2 = LDS-DMA with two stage buffers (two
-// workgroups per CU), 1 = LDS-DMA with one stage buffer (three per CU)
+// workgroups per CU), 1 = LDS-DMA with one stage buffer (three per CU), 3 =
+// three stage buffers (long K, 128x64 / 64x64 tiles)
 template <typename T, int BM, int BN, class LA, class LB, int EK, bool RS = false, int DMAK = 0>
 __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG_OCC : 2)) void gemm_kernel(LA la, LB lb, int M, int N,
                                                                                             int K, int kps, Epi ep) {
@@ -1248,7 +1256,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
   // LDS-DMA K loop (DMAK kernels): dense bf16 operands, no row sums
   constexpr bool DMA =
       sizeof(T) == 2 && (IsDenseBf16<LA>::value || IsConvFBf16<LA>::value) && IsDenseBf16<LB>::value && !RS;
-  constexpr int SM_DMA = DMAK ? GemmCoreDma<BM, BN, LA::KC, LB::KC, DMAK == 1 ? 1 : 2>::SM_LOOP : 0;
+  constexpr int SM_DMA = DMAK ? GemmCoreDma<BM, BN, LA::KC, LB::KC, DMAK == 0 ? 2 : DMAK>::SM_LOOP : 0;
   constexpr int SM_LOOP = DMAK == 1 ? SM_DMA : (C::SM_LOOP > SM_DMA ? C::SM_LOOP : SM_DMA);
   constexpr int SM_EPI = (64 * (BN + 4) + (GEMM_THREADS / (BN / 4)) * BN) * 4;
   // the wide (8-column) epilogue's column-sum scratch follows the 64-row tile image
@@ -1344,7 +1352,7 @@ __global__ __launch_bounds__(GEMM_THREADS, (DMAK == 1 ? 3 : BM >= 128 ? HVIT_BIG
     // is compiled into the kernel, so it keeps its own register budget)
     static_assert(DMA, "DMA-only kernel needs dense bf16 operands");
     (void)interior;
-    GemmCoreDma<BM, BN, LA::KC, LB::KC, DMAK == 1 ? 1 : 2>::run(la, lb, smem, m0, n0, kbeg, kend, acc);
+    GemmCoreDma<BM, BN, LA::KC, LB::KC, DMAK == 0 ? 2 : DMAK>::run(la, lb, smem, m0, n0, kbeg, kend, acc);
   } else {
     if (interior) C::template run<false, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
     else C::template run<true, RS>(la, lb, smem, m0, n0, kbeg, kend, acc, rsacc, rs_on);
@@ -1829,6 +1837,15 @@ inline int plan_splits(int K, int splits, int* kps_out = nullptr) {
   return K > 0 ? (K + kps - 1) / kps : 1;
 }
 
+// LDS-DMA stage buffers of the 128x64 / 64x64 kernels on long K loops
+// (hvit_gemm_tune(8, v): 3 = three buffers from DEEP_MIN_STAGES stages on, 2 = two)
+inline int& dma_depth_ref() {
+  static int v = 3;
+  return v;
+}
+inline int dma_depth() { return dma_depth_ref(); }
+constexpr int DEEP_MIN_STAGES = 16;
+
 template <typename T, class LA, class LB>
 int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in, hipStream_t st,
                 int force_tile = 0) {
@@ -1926,6 +1943,13 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
             if constexpr (BMc == 128 && BNc == 128 && (EKc == EK_GELU_DUAL || EKc == EK_STORE)) {
               if (CONV_A ? (nb1c && ep.stats) : nb1) {
                 hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 1>), g, dim3(GEMM_THREADS), 0, st,
+                                   la, lb, M, N, K, kps, ep);
+                return;
+              }
+            }
+            if constexpr (!(BMc == 128 && BNc == 128)) {
+              if (dma_depth() == 3 && kps / 64 >= DEEP_MIN_STAGES) {
+                hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 3>), g, dim3(GEMM_THREADS), 0, st,
                                    la, lb, M, N, K, kps, ep);
                 return;
               }

@@ -267,6 +267,11 @@ extern "C" int hvit_gemm_tune(int what, int value) {
     wgrad_plan_ref() = value;
     return old;
   }
+  if (what == 8) {  // LDS-DMA stage buffers of the long-K 128x64 / 64x64 kernels (dma_depth_ref)
+    const int old = dma_depth_ref();
+    if (value == 2 || value == 3) dma_depth_ref() = value;
+    return old;
+  }
   if (what == 7) return hvit_wgrad_group_tune(value);  // grouped weight gradients: 0 256x256 tiles, 1 256x128
   if (what == 4) return hvit_attn_tune(value);  // attention backward for N <= 256: 1 single pass, 0 two kernels
   if (what == 5) return hvit_fp8_tune(value);  // fp8 attention forward: 0 round-4 kernel, 1 v2 16 waves, 2 v2 8 waves
