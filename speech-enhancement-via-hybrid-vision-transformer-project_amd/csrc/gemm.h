@@ -1838,9 +1838,12 @@ inline int plan_splits(int K, int splits, int* kps_out = nullptr) {
 }
 
 // LDS-DMA stage buffers of the 128x64 / 64x64 kernels on long K loops
-// (hvit_gemm_tune(8, v): 3 = three buffers from DEEP_MIN_STAGES stages on, 2 = two)
+// (hvit_gemm_tune(8, v): 3 = three buffers from DEEP_MIN_STAGES stages on, 4 = from 8 stages, 2 = two)
 inline int& dma_depth_ref() {
-  static int v = 3;
+  // same-box A/B (gpurun_out/r6n_dma*): two buffers 4.656-4.660 ms/step, three from 16 stages
+  // 4.543-4.551, three from 8 stages 4.509-4.524 (vit_linear_dgrad 0.784 -> 0.728, vit_linear_fwd
+  // 0.774 -> 0.741, conv_fwd 0.410 -> 0.388 ms/step)
+  static int v = 4;
   return v;
 }
 inline int dma_depth() { return dma_depth_ref(); }
@@ -1948,7 +1951,9 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
               }
             }
             if constexpr (!(BMc == 128 && BNc == 128)) {
-              if (dma_depth() == 3 && kps / 64 >= DEEP_MIN_STAGES) {
+              // (not the conv data gradients -- implicit im2col of dy without BN statistics:
+              // conv_dgrad 0.376 -> 0.394 ms/step with three buffers)
+              if (dma_depth() >= 3 && kps / 64 >= (dma_depth() == 4 ? 8 : DEEP_MIN_STAGES) && (!CONV_A || ep.stats)) {
                 hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 3>), g, dim3(GEMM_THREADS), 0, st,
                                    la, lb, M, N, K, kps, ep);
                 return;

@@ -269,7 +269,7 @@ extern "C" int hvit_gemm_tune(int what, int value) {
   }
   if (what == 8) {  // LDS-DMA stage buffers of the long-K 128x64 / 64x64 kernels (dma_depth_ref)
     const int old = dma_depth_ref();
-    if (value == 2 || value == 3) dma_depth_ref() = value;
+    if (value >= 2 && value <= 4) dma_depth_ref() = value;
     return old;
   }
   if (what == 7) return hvit_wgrad_group_tune(value);  // grouped weight gradients: 0 256x256 tiles, 1 256x128
