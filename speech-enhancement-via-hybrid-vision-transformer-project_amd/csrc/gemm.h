@@ -1951,9 +1951,12 @@ int launch_gemm(LA la, LB lb, int M, int N, int K, int splits, const Epi& ep_in,
               }
             }
             if constexpr (!(BMc == 128 && BNc == 128)) {
-              // (not the conv data gradients -- implicit im2col of dy without BN statistics:
-              // conv_dgrad 0.376 -> 0.394 ms/step with three buffers)
-              if (dma_depth() >= 3 && kps / 64 >= (dma_depth() == 4 ? 8 : DEEP_MIN_STAGES) && (!CONV_A || ep.stats)) {
+              // (not the conv data gradients -- implicit im2col of dy, plain store epilogue:
+              // conv_dgrad 0.376 -> 0.394 ms/step with three buffers, 72 KiB of LDS leaving
+              // two workgroups per CU where the 48 KiB two-buffer kernel keeps three; the
+              // patch-embedding forward, with its positional-row epilogue, does take them)
+              if (dma_depth() >= 3 && kps / 64 >= (dma_depth() == 4 ? 8 : DEEP_MIN_STAGES) &&
+                  (!CONV_A || ep.stats || ep.rowadd)) {
                 hipLaunchKernelGGL((gemm_kernel<T, BMc, BNc, LA, LB, EKc, false, 3>), g, dim3(GEMM_THREADS), 0, st,
                                    la, lb, M, N, K, kps, ep);
                 return;
