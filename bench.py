@@ -152,8 +152,11 @@ def measured_traffic(name):
         return None
     with open(p) as f:
         d = json.load(f)
-    same = all(d.get(k, v) == v for k, v in WORKLOAD.items())
-    return d.get("hbm_bytes_per_launch") if d.get("op") == name and same else None
+    if not all(d.get(k, v) == v for k, v in WORKLOAD.items()):
+        return None
+    if "ops" in d:  # several op classes, one PMC pair each (tools/roofline_pmc.py)
+        return d["ops"].get(name, {}).get("hbm_bytes_per_launch")
+    return d.get("hbm_bytes_per_launch") if d.get("op") == name else None
 
 
 def cpu_model():

@@ -86,7 +86,7 @@ def timed(name: str, work: float):
 
 
 # Launch recorder (measurement only): bench.py installs REPLAY = {} for one
-# step; the weight-gradient ops then also store a closure that re-issues the
+# step; the recorded ops (ViT linears, weight gradients) then also store a closure that re-issues the
 # same launch on the same tensors, so the dominant op class can be re-run in
 # isolation (bench.py --roofline-only, the rocprofv3 / PMC loop).
 REPLAY = None
@@ -98,8 +98,8 @@ def _record(name, fn):
 
 
 def _launch(name, work, fn, e=None, keep=()):
-    """One timed, recorded launch of op class ``name`` (the ViT data gradients:
-    re-runnable in isolation for the roofline loop).  ``fn(e)`` issues it with
+    """One timed, recorded launch of op class ``name`` (the ViT forward and
+    data-gradient linears: re-runnable in isolation for the roofline loop).  ``fn(e)`` issues it with
     epilogue ``e``.  The recorded replay runs the same launch without the
     epilogue's side job (the carried slab sum belongs to the step, and its
     slabs and destination are freed after the backward) and holds ``keep`` (the
@@ -1310,9 +1310,9 @@ class ViTBlockFn(torch.autograd.Function):
         xn1, m1, r1 = _ln(x2d, n1w, n1b, dt)
         Wqkv = cast(qkvw, dt)
         qkv = _empty((M, 3 * D), dt, dev)
-        with timed("vit_linear_fwd", 2.0 * M * 3 * D * D):
-            call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
-                 qkv.data_ptr(), dt, None, s)
+        _launch("vit_linear_fwd", 2.0 * M * 3 * D * D,
+                lambda e: call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
+                               qkv.data_ptr(), dt, e, s))
         o = _empty((M, D), dt, dev)
         lse = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         kbits = None
@@ -1341,9 +1341,10 @@ class ViTBlockFn(torch.autograd.Function):
                      lse.data_ptr(), ptr(probs), s)
         Wp = cast(pw, dt)
         x1 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        with timed("vit_linear_fwd", 2.0 * M * D * D):
-            call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D, x1.data_ptr(), F32,
-                 epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), s)
+        _launch("vit_linear_fwd", 2.0 * M * D * D,
+                lambda e: call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D,
+                               x1.data_ptr(), F32, e, s),
+                epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), (x2d, rs1))
         xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
         W1 = cast(f1w, dt)
         # the fc1 epilogue keeps gelu'(h) (not h) for the backward -- times the
@@ -1353,10 +1354,10 @@ class ViTBlockFn(torch.autograd.Function):
         a = _empty((M, hid), dt, dev)
         if not nograd:
             gh = _empty((M, hid), dt, dev)
-            with timed("vit_linear_fwd", 2.0 * M * hid * D):
-                call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, gh.data_ptr(),
-                     dt, epilogue(act=L.ACT_GELU_DUAL_DK if FC1_FOLD else L.ACT_GELU_DUAL_D, out2=a,
-                                  drop=d_fc1.c()), s)
+            _launch("vit_linear_fwd", 2.0 * M * hid * D,
+                    lambda e: call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D,
+                                   gh.data_ptr(), dt, e, s),
+                    epilogue(act=L.ACT_GELU_DUAL_DK if FC1_FOLD else L.ACT_GELU_DUAL_D, out2=a, drop=d_fc1.c()), (a,))
         else:
             gh = None
             with timed("vit_linear_fwd", 2.0 * M * hid * D):
@@ -1364,9 +1365,10 @@ class ViTBlockFn(torch.autograd.Function):
                      epilogue(act=L.ACT_GELU, drop=d_fc1.c()), s)
         W2 = cast(f2w, dt)
         x2 = torch.empty((M, D), dtype=torch.float32, device=dev)
-        with timed("vit_linear_fwd", 2.0 * M * D * hid):
-            call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid, x2.data_ptr(), F32,
-                 epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), s)
+        _launch("vit_linear_fwd", 2.0 * M * D * hid,
+                lambda e: call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid,
+                               x2.data_ptr(), F32, e, s),
+                epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), (x1, rs2))
         ctx.save_for_backward(n1w, n2w)
         ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
         # the parameters whose gradients the side stream may produce (side_ok)

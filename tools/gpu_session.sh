@@ -39,11 +39,11 @@ for s in "$@"; do
            --master-addr 127.0.0.1 --master-port 29531 bench.py --no-cpu-baseline > gpurun_out/${TAG}_dp1.log 2>&1 || exit $? ;;
     roof:*)  # roof:OP -- the op class re-run in isolation: rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE passes
       op=${s#roof:}
-      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof -o run --output-format csv -- \
-        python3 bench.py --roofline-only --roofline-op $op > gpurun_out/${TAG}_roofprof.log 2>&1 || exit $?
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_roofprof_$op -o run --output-format csv -- \
+        python3 bench.py --roofline-only --roofline-op $op > gpurun_out/${TAG}_roofprof_$op.log 2>&1 || exit $?
       for set in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/${TAG}_rpmc_$set -o run -- \
-          python3 bench.py --roofline-only --roofline-op $op > gpurun_out/${TAG}_rpmc_$set.log 2>&1 || exit $?
+        timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/${TAG}_rpmc_${op}_$set -o run -- \
+          python3 bench.py --roofline-only --roofline-op $op > gpurun_out/${TAG}_rpmc_${op}_$set.log 2>&1 || exit $?
       done ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $? ;;
     env:*)  # env:VAR=VAL[,VAR=VAL]: bench.py --no-cpu-baseline under those variables
