@@ -630,9 +630,31 @@ def wgrad_enqueue(dy, x, M, N, K, dest=None, pref=None, patch=None) -> torch.Ten
 
 
 def _wgrad_flush_all():
-    for i in set(_WG_QUEUE) | set(_SIDE_PENDING):
+    for i in set(_WG_QUEUE) | set(_SIDE_PENDING) | set(_WG_AFTER):
         wgrad_flush(torch.device("cuda", i))
     _WG_TASKS.clear()
+
+
+# Launches that read queued gradients and were held back until the grouped
+# launch (the DP buckets holding ViT weights: dp.GradAllReducer._launch), run
+# by the flush right after it, in the order they were deferred.
+_WG_AFTER = {}  # device index -> [callable]
+WG_LAUNCHES = 0  # grouped launches issued (tests: one per backward)
+
+
+def wgrad_pending(dev) -> bool:
+    """True while weight gradients of ``dev`` wait in the group queue."""
+    return bool(_WG_QUEUE.get(_dev_index(dev)))
+
+
+def wgrad_after_flush(dev, fn) -> None:
+    """Run ``fn()`` right after the next flush of ``dev``'s queue."""
+    i = _dev_index(dev)
+    _WG_AFTER.setdefault(i, []).append(fn)
+    task = torch._C._current_graph_task_id()
+    if task >= 0 and task not in _WG_TASKS:
+        _WG_TASKS.add(task)
+        torch.autograd.Variable._execution_engine.queue_callback(_wgrad_flush_all)
 
 
 # Partial-row sums (Deferred side jobs) whose results were handed to autograd
@@ -672,8 +694,14 @@ def wgrad_flush(dev=None) -> None:
     i = _dev_index(dev) if dev is not None else torch.cuda.current_device()
     _side_run_pending(i)
     q = _WG_QUEUE.pop(i, None)
-    if not q:
-        return
+    if q:
+        _wgrad_group_launch(i, q)
+    for fn in _WG_AFTER.pop(i, []):
+        fn()
+
+
+def _wgrad_group_launch(i, q):
+    global WG_LAUNCHES
     d = torch.device("cuda", i)
     tk = _WG_TICKETS.get(i)
     if tk is None:
@@ -701,6 +729,7 @@ def wgrad_flush(dev=None) -> None:
 
         with timed("vit_linear_wgrad", flops):
             launch()
+        WG_LAUNCHES += 1
         _record("vit_linear_wgrad", (lambda launch=launch, ws=ws: launch(), flops))
     for dy, x, dw, n, k, _, pref, patch, packed in q:
         if patch is not None:  # [co][ky][kx][c] -> torch's [co][c][ky][kx]
@@ -1130,6 +1159,9 @@ class PatchEmbedFn(torch.autograd.Function):
             call("hvit_conv_dgrad", dt, g, gd.data_ptr(), ctx.wp.data_ptr(), dfeat.data_ptr(), dt, s)
             if ctx.sg is not None:
                 ctx.sg.drain(dfeat)
+        # the ViT blocks' backward is done: their grouped weight gradients go now rather than at the end of
+        # backward, so the DP buckets holding them (deferred until the flush) reduce under the encoder backward
+        wgrad_flush(dev)
         return dfeat, dw, db, dpos, None, None, None, None, None
 
 

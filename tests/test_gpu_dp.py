@@ -146,6 +146,8 @@ def test_rccl_world1_bench_dp_branch():
     # the DP step is captured whole (bucket all-reduces from the hooks included)
     assert out["launch"] == "hipGraph replay of the whole step"
     assert out["value"] > 0 and abs(out["final_loss"]) < 1e3
+    # one grouped weight-gradient launch per step: the DP buckets wait for it instead of splitting it
+    assert out["op_table"]["vit_linear_wgrad"]["launches_per_step"] == 1, out["op_table"]["vit_linear_wgrad"]
 
 
 def test_rccl_world1_dp_graph_matches_eager():
@@ -162,6 +164,8 @@ def test_rccl_world1_dp_graph_matches_eager():
     assert r.returncode == 0, r.stderr[-4000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["dropout_state_equal"]
+    # the buckets holding ViT weights wait for the one grouped weight-gradient launch (not one launch per bucket)
+    assert out["group_launches_per_step"] == 1.0, out
     assert out["steps"] == 5.0  # 2 warm-up + 3 replays
     for a, b in out["losses"]:
         assert abs(a - b) <= 1e-6 * abs(b), out["losses"]

@@ -168,6 +168,7 @@ def test_model_grads_grouped_equal_per_linear(hv):
     assert not HF._WG_QUEUE, "the backward's final callback must flush the queue"
     assert HF.WG_FIXUPS == 0, "autograd must adopt the queued gradients (no copy of an unwritten tensor)"
     assert not any(HF._SIDE_PENDING.values()), "pending side jobs must be carried or flushed"
+    assert not any(HF._WG_AFTER.values()), "launches deferred to the flush must have run"
     for n, g0 in grads[False].items():
         g1 = grads[True][n]
         if n == "patch_embed.projection.weight" or (
