@@ -37,10 +37,13 @@ class CombinedLossFn(torch.autograd.Function):
         ctx.cfg = cfg
         comps = out[1:]
         ctx.mark_non_differentiable(comps)
+        ctx.set_materialize_grads(False)  # (no zero-filled gradient for the components: one launch fewer)
         return out[0], comps
 
     @staticmethod
     def backward(ctx, gtot, _gcomps=None):
+        if gtot is None:
+            return None, None, None
         pred, target, stats = ctx.saved_tensors
         B = pred.shape[0]
         P = pred.numel() // B
