@@ -99,8 +99,9 @@ def _record(name, fn):
 
 def _launch(name, work, fn, e=None, keep=()):
     """One timed, recorded launch of op class ``name`` (the ViT forward and
-    data-gradient linears: re-runnable in isolation for the roofline loop).  ``fn(e)`` issues it with
-    epilogue ``e``.  The recorded replay runs the same launch without the
+    data-gradient linears: re-runnable in isolation for the roofline loop).
+    ``fn(e[, stream])`` issues it with epilogue ``e`` (on the launch's own
+    stream unless one is given).  The recorded replay runs the same launch without the
     epilogue's side job (the carried slab sum belongs to the step, and its
     slabs and destination are freed after the backward) and holds ``keep`` (the
     tensors behind the epilogue's raw pointers, e.g. gelu'(h) and the bias-grad
@@ -112,7 +113,8 @@ def _launch(name, work, fn, e=None, keep=()):
         if e is not None:
             er = type(e).from_buffer_copy(e)
             er.side = L.SlabSum()
-        _record(name, ((lambda er=er, keep=keep: fn(er)), work))
+        # (the replay launches on the stream current at replay time: bench.py may capture it)
+        _record(name, ((lambda er=er, keep=keep: fn(er, stream_ptr())), work))
 
 
 def _empty(shape, dt, dev):
@@ -1343,8 +1345,8 @@ class ViTBlockFn(torch.autograd.Function):
         Wqkv = cast(qkvw, dt)
         qkv = _empty((M, 3 * D), dt, dev)
         _launch("vit_linear_fwd", 2.0 * M * 3 * D * D,
-                lambda e: call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
-                               qkv.data_ptr(), dt, e, s))
+                lambda e, st=s: call("hvit_linear_fwd", dt, xn1.data_ptr(), Wqkv.data_ptr(), qkvb.data_ptr(), M, 3 * D, D,
+                               qkv.data_ptr(), dt, e, st))
         o = _empty((M, D), dt, dev)
         lse = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
         kbits = None
@@ -1374,8 +1376,8 @@ class ViTBlockFn(torch.autograd.Function):
         Wp = cast(pw, dt)
         x1 = torch.empty((M, D), dtype=torch.float32, device=dev)
         _launch("vit_linear_fwd", 2.0 * M * D * D,
-                lambda e: call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D,
-                               x1.data_ptr(), F32, e, s),
+                lambda e, st=s: call("hvit_linear_fwd", dt, o.data_ptr(), Wp.data_ptr(), pb.data_ptr(), M, D, D,
+                               x1.data_ptr(), F32, e, st),
                 epilogue(drop=d_proj.c(), resid=x2d, rowscale=rs1, rps=Nt), (x2d, rs1))
         xn2, m2, r2 = _ln(x1, n2w, n2b, dt)
         W1 = cast(f1w, dt)
@@ -1387,19 +1389,20 @@ class ViTBlockFn(torch.autograd.Function):
         if not nograd:
             gh = _empty((M, hid), dt, dev)
             _launch("vit_linear_fwd", 2.0 * M * hid * D,
-                    lambda e: call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D,
-                                   gh.data_ptr(), dt, e, s),
+                    lambda e, st=s: call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D,
+                                   gh.data_ptr(), dt, e, st),
                     epilogue(act=L.ACT_GELU_DUAL_DK if FC1_FOLD else L.ACT_GELU_DUAL_D, out2=a, drop=d_fc1.c()), (a,))
         else:
             gh = None
-            with timed("vit_linear_fwd", 2.0 * M * hid * D):
-                call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D, a.data_ptr(), dt,
-                     epilogue(act=L.ACT_GELU, drop=d_fc1.c()), s)
+            _launch("vit_linear_fwd", 2.0 * M * hid * D,
+                    lambda e, st=s: call("hvit_linear_fwd", dt, xn2.data_ptr(), W1.data_ptr(), f1b.data_ptr(), M, hid, D,
+                                   a.data_ptr(), dt, e, st),
+                    epilogue(act=L.ACT_GELU, drop=d_fc1.c()))
         W2 = cast(f2w, dt)
         x2 = torch.empty((M, D), dtype=torch.float32, device=dev)
         _launch("vit_linear_fwd", 2.0 * M * D * hid,
-                lambda e: call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid,
-                               x2.data_ptr(), F32, e, s),
+                lambda e, st=s: call("hvit_linear_fwd", dt, a.data_ptr(), W2.data_ptr(), f2b.data_ptr(), M, D, hid,
+                               x2.data_ptr(), F32, e, st),
                 epilogue(drop=d_fc2.c(), resid=x1, rowscale=rs2, rps=Nt), (x1, rs2))
         ctx.save_for_backward(n1w, n2w)
         ctx.wid = tuple((id(p), tuple(p.shape)) for p in (qkvw, pw, f1w, f2w))
@@ -1485,8 +1488,8 @@ class ViTBlockFn(torch.autograd.Function):
         e_fc2 = epilogue(act=L.ACT_MUL_AUX, aux=gh, drop=None if FC1_FOLD else drf1, colsum=cparts,
                          side=j2 if j2 is not None else jho)
         _launch("vit_linear_dgrad", 2.0 * M * D * hid,
-                lambda e: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt, e,
-                               s), e_fc2, (gh, cparts))
+                lambda e, st=s: call("hvit_linear_dgrad", dt, g2.data_ptr(), W2.data_ptr(), M, D, hid, dh.data_ptr(), dt, e,
+                               st), e_fc2, (gh, cparts))
         jc = Deferred(L.SlabSum(cparts.data_ptr(), df1b.data_ptr(), hid, hid, nrow), cparts)
         if side:
             df1w = wdest(d1_id, hid, D)
@@ -1503,9 +1506,9 @@ class ViTBlockFn(torch.autograd.Function):
         dxn2 = _empty((M, D), dt if LN_DY_LOW else F32, dev)
         e_fc1 = epilogue(side=j1)
         _launch("vit_linear_dgrad", 2.0 * M * hid * D,
-                lambda e: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(),
+                lambda e, st=s: call("hvit_linear_dgrad", dt, dh.data_ptr(), W1.data_ptr(), M, hid, D, dxn2.data_ptr(),
                                L.dt_of(dxn2),
-                               e, s), e_fc1)
+                               e, st), e_fc1)
         jln = None
         if LNDROP:  # LN2 backward + the attention branch's dropout / DropPath scaling in one pass; its
             # [dgamma | dbeta | proj bias] partial rows summed by the proj weight-gradient launch (side job)
@@ -1529,7 +1532,7 @@ class ViTBlockFn(torch.autograd.Function):
         do = _empty((M, D), dt, dev)
         e_pr = epilogue(side=jp)
         _launch("vit_linear_dgrad", 2.0 * M * D * D,
-                lambda e: call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, e, s),
+                lambda e, st=s: call("hvit_linear_dgrad", dt, g1.data_ptr(), Wp.data_ptr(), M, D, D, do.data_ptr(), dt, e, st),
                 e_pr)
         dqkv = _empty((M, 3 * D), dt, dev)
         delta = torch.empty((B, H, Nt), dtype=torch.float32, device=dev)
@@ -1564,8 +1567,8 @@ class ViTBlockFn(torch.autograd.Function):
         dxn1 = _empty((M, D), dt if LN_DY_LOW else F32, dev)
         e_qkv = epilogue(side=jq)
         _launch("vit_linear_dgrad", 2.0 * M * 3 * D * D,
-                lambda e: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
-                               L.dt_of(dxn1), e, s), e_qkv)
+                lambda e, st=s: call("hvit_linear_dgrad", dt, dqkv.data_ptr(), Wqkv.data_ptr(), M, 3 * D, D, dxn1.data_ptr(),
+                               L.dt_of(dxn1), e, st), e_qkv)
         if ho_in is not None and ho_in.drop is not None:  # the previous block's fc2 dropout, fused
             dx, dn1w, dn1b = ho_in.fuse(dxn1, x2d, m1, r1, n1w, dx1, zln1, ctx.lnrefs)
         else:
