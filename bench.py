@@ -455,7 +455,11 @@ def main():
     roof = roofline_of(table) if rank == 0 else None
     if world == 1 and roof is not None:
         # the dominant class re-timed as a graph replay of its recorded launches (no per-launch events)
-        gr = roofline_graph(eager_step, roof["kernel"])
+        try:
+            gr = roofline_graph(eager_step, roof["kernel"])
+        except RuntimeError as exc:  # (the per-launch event figure stands; the line says why)
+            gr = None
+            roof["graph_timing_error"] = str(exc)[:200]
         if gr is not None:
             us, work = gr
             _, _, scale = PEAKS[roof["bound"]]
